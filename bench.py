@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""LMI search hot path on MI355X: queries/s on a 10k-query batch (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W] [--scale 10M|300K|...]
+
+One step = one search of the whole 10k-query batch exactly as the reference
+times it (search.py:116-141): router (K1) + per-(query, probe) bucket scan
+(K2) [+ RCCL all-gather + K3 merge for N > 1] + D2H of the lists + the replay
+of the reference's merge (host C++).  Inputs (corpus index, queries) are
+resident in HBM before the timed region.  N > 1: launched by torchrun, one
+process per GPU, the corpus striped over the ranks; all ranks search the same
+batch (strong scaling: value = nq / max-over-ranks step time).
+
+Besides the JSON fields of the driver contract the line carries:
+  roofline      K2 scan kernel: algorithmic bytes per launch / its average
+                duration (HIP events on the launch stream, every timed step)
+  cpu_baseline  the oracle restatement (oracle/lmi_oracle.py, "port") timed on
+                a bounded sample of the same workload on this host's cores
+  recall        recall@k of the returned ids against exact k-NN on a sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
+
+from li import _lib, synth  # noqa: E402
+from li.dist import init_from_env  # noqa: E402
+from li.index import DeviceIndex, DeviceRouter, Searcher  # noqa: E402
+
+METRIC = "queries/sec @ recall≥90% on 10M clip768, 10k-query batch; % HBM roofline"
+PUBLISHED_QPS_10M = 19.42  # README:17,30 — 514.91 s for 10k queries, EPYC 7532, 1 core
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+F16_PEAK_TFLOPS = 2500.0   # dense fp16 MFMA
+
+SCALES = {"10M": 10_000_000, "1M": 1_000_000, "300K": 300_000, "100K": 100_000}
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_workload(args, device, rank, world):
+    """Synthetic clip768/pca96 corpus + queries, a router fitted to k-means
+    buckets, object labels = router argmax (LearnedIndex.py:240)."""
+    n, d, C = SCALES[args.scale], 768, args.n_buckets
+    t0 = time.time()
+    x, cen = synth.torch_mixture(n, d, args.centres, seed=2023, device=device)
+    q, _ = synth.torch_mixture(args.nq, d, args.centres, seed=4242, device=device, centres=cen,
+                               out_dtype=torch.float32)
+    g = torch.Generator(device=device)
+    g.manual_seed(96)
+    P = torch.randn((d, 96), generator=g, device=device) / math.sqrt(d)
+    xn = synth.torch_nav(x, P)
+    qn = synth.torch_nav(q, P)
+    sub = xn[torch.randperm(n, generator=g, device=device)[: min(n, 400_000)]]
+    cent = synth.kmeans(sub, C, iters=20, seed=7)
+    d2 = (sub * sub).sum(1, keepdim=True) - 2 * sub @ cent.T + (cent * cent).sum(1)[None]
+    model = synth.train_router(sub, d2.argmin(1), synth.ARCHS[args.arch], C, steps=args.train_steps)
+    router = DeviceRouter.from_module(model, device=device)
+    labels = router.argmax(xn)
+    torch.cuda.synchronize()
+    log(f"[bench] workload n={n} built in {time.time() - t0:.1f}s")
+    t0 = time.time()
+    index = DeviceIndex(x, labels, C, device=device, chunk_rows=args.chunk_rows, rank=rank,
+                        world=world)
+    torch.cuda.synchronize()
+    log(f"[bench] index (rank {rank}/{world}, {index.n_rows} rows, {index.storage}) "
+        f"in {time.time() - t0:.1f}s; bucket sizes min/median/max = "
+        f"{index.bucket_size.min()}/{int(np.median(index.bucket_size))}/{index.bucket_size.max()}")
+    del xn
+    return x, q, qn, router, index, labels
+
+
+@torch.no_grad()
+def exact_knn(x, qs, k, chunk=1 << 20):
+    """Exact cosine k-NN of the sample queries (ids 1-based, Baseline.py:17-19)."""
+    qn = qs / qs.norm(dim=1, keepdim=True)
+    best_s = torch.full((qs.shape[0], k), -2.0, device=qs.device)
+    best_i = torch.zeros((qs.shape[0], k), dtype=torch.int64, device=qs.device)
+    for a in range(0, x.shape[0], chunk):
+        blk = x[a:a + chunk].float()
+        s = qn @ (blk / blk.norm(dim=1, keepdim=True)).T
+        v, i = s.topk(k, dim=1)
+        cs = torch.cat([best_s, v], 1)
+        ci = torch.cat([best_i, i + a], 1)
+        o = cs.topk(k, dim=1).indices
+        best_s, best_i = cs.gather(1, o), ci.gather(1, o)
+    return (best_i + 1).cpu().numpy()
+
+
+def algorithmic_bytes(index, classes, nq):
+    """K2 per launch: every probed bucket's rows once (d_pad*s + 4 B of 1/||y||)
+    + the queries as the scan reads them."""
+    probed = np.unique(classes)
+    loc = index.bucket_off_local.cpu().numpy()
+    rows = int(sum(loc[c + 1] - loc[c] for c in probed))
+    s = 2 if index.storage == "f16" else 4
+    byts = rows * (index.d_pad * s + 4) + nq * index.d_pad * s
+    sizes = np.diff(loc)
+    flops = 2.0 * index.d * float(sizes[classes].sum())
+    return byts, flops, rows
+
+
+def cpu_baseline(index, q, qn_classes, args, budget_s=15.0):
+    """Oracle port (oracle/lmi_oracle.py) on a bounded query sample of the same
+    workload: per-(query, probe) lists by the reference's per-group
+    normalize + GEMM (utils.py:10-11) and the replay (LearnedIndex.py:22-195)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import lmi_oracle as O
+    off = index.layout.bucket_off
+    corpus = index.corpus
+    qh = q.cpu().numpy()
+    R, k = args.R, args.k
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    t0 = time.time()
+    done = 0
+    cache = {}
+    while done < min(args.nq, 512) and (time.time() - t0 < budget_s or done < 4):
+        qq = done
+        lists_d = np.full((1, R, k), np.inf, np.float32)
+        lists_p = np.full((1, R, k), -1, np.int32)
+        for r in range(R):
+            c = int(qn_classes[qq, r])
+            a, b = int(off[c]), int(off[c + 1])
+            if a == b:
+                continue
+            if c not in cache:
+                if len(cache) > 16:
+                    cache.pop(next(iter(cache)))
+                cache[c] = corpus[a:b, : index.d].float().cpu().numpy()
+            D = O.pairwise_cosine(qh[qq:qq + 1], cache[c])[0]
+            pos = np.arange(a, b)
+            o = np.lexsort((pos, D))[:k]
+            lists_d[0, r, : o.size] = D[o]
+            lists_p[0, r, : o.size] = pos[o]
+        done += 1
+    t = time.time() - t0
+    return {"value": round(done / t, 3), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{done} of the {args.nq} queries of the same {args.scale} workload, R={R}, "
+                      f"k={k}: per-probe 1-cos (sklearn normalize + fp32 GEMM) and top-k "
+                      f"in numpy, {threads} BLAS threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scale", default="10M", choices=list(SCALES))
+    ap.add_argument("--nq", type=int, default=10_000)
+    ap.add_argument("--R", type=int, default=4)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--n-buckets", type=int, default=122)
+    ap.add_argument("--arch", default="MLP-5")
+    ap.add_argument("--centres", type=int, default=400)
+    ap.add_argument("--train-steps", type=int, default=300)
+    ap.add_argument("--chunk-rows", type=int, default=8192)
+    ap.add_argument("--recall-sample", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = init_from_env()
+    if world != args.gpus:
+        log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    group = None
+    x, q, qn, router, index, labels = build_workload(args, device, rank, world)
+    searcher = Searcher(index, router, group)
+
+    def step():
+        return searcher.search(qn, q, args.R, k=args.k, use_threshold=True)
+
+    for _ in range(args.warmup):
+        dists, anns = step()
+    lib = _lib.load()
+    lib.lmi_timing_read(None, 0)  # drop warmup records
+    lib.lmi_timing_enable(1)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dists, anns = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    lib.lmi_timing_enable(0)
+    ms = (_lib.C.c_float * max(args.steps, 1))()
+    n_ev = lib.lmi_timing_read(ms, args.steps)
+    scan_ms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    ms_step = el / args.steps * 1e3
+    value = args.nq / (el / args.steps)
+
+    classes, _ = router.topr(qn, args.R)
+    classes = classes.cpu().numpy()
+    byts, flops, rows = algorithmic_bytes(index, classes, args.nq)
+    if rank != 0:
+        if world > 1:
+            torch.distributed.barrier()
+        return
+    achieved = byts / (scan_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "scan_kernel (lmi_bucket_topk)", "kernel_ms": round(scan_ms, 4),
+            "algorithmic_bytes": int(byts), "flops": flops,
+            "mfma_tflops": round(flops / (scan_ms * 1e-3) / 1e12, 1),
+            "mfma_frac": round(flops / (scan_ms * 1e-3) / 1e12 / F16_PEAK_TFLOPS, 4)}
+    sample = min(args.recall_sample, args.nq)
+    truth = exact_knn(x, q[:sample], args.k)
+    recall = float(np.mean([len(set(anns[i][: args.k]) & set(truth[i])) / args.k
+                            for i in range(sample)]))
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(index, q, classes, args)
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "queries/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": round(value / PUBLISHED_QPS_10M, 1) if args.scale == "10M" else None,
+        "dtype": "f16", "data": "synthetic",
+        "config": {"workload": f"{args.scale} clip768-like synthetic (fp16-exact), {args.n_buckets} "
+                               f"buckets, R={args.R}, k={args.k}, {args.nq} queries, router "
+                               f"{args.arch}", "n": SCALES[args.scale], "d": 768, "nq": args.nq,
+                   "R": args.R, "k": args.k, "n_buckets": args.n_buckets, "router": args.arch,
+                   "parallelism": f"corpus striped over {world} GPU(s)",
+                   "chunk_rows": args.chunk_rows},
+        "roofline": roof, "cpu_baseline": cpu,
+        "recall": round(recall, 4), "recall_sample": sample,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+/*
+ * lmi_hip.h — C-ABI of liblmi_hip.so, the MI355X (gfx950) implementation of the
+ * LMI search hot path of TerkaSlan/sisap23-laion-challenge-learned-index.
+ *
+ * The reference has no native code and no FFI: its hot path is Python calling
+ * torch / sklearn / numpy.  Each entry point below replaces
+ * one piece of that Python path; the reference file:line it stands in for is
+ * cited per function.  The ctypes binding a maintainer adds on the reference
+ * side is in INTEGRATION.md; this repo's own binding is li/_lib.py.
+ *
+ * Conventions (all entry points):
+ *   - plain pointers and sizes only; "device" pointers are HIP device memory
+ *     owned by the caller; "host" pointers are ordinary host memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *     device entry points are asynchronous on that stream, never allocate and
+ *     never synchronise (workspace is passed in), so they can be captured in
+ *     a hipGraph;
+ *   - return 0 (LMI_OK) or an LMI_E_* code; lmi_last_error() gives text
+ *     (thread-local).  No C++ exception crosses the ABI.
+ *   - results are deterministic: no float atomics in any reduction; every
+ *     top-k list is ordered by (distance, position) ascending, which is the
+ *     reference's order on tie-free inputs (LearnedIndex.py:170, :91).
+ */
+#ifndef LMI_HIP_H
+#define LMI_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LMI_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define LMI_OK 0
+#define LMI_E_INVALID 1001     /* bad argument (shape, null pointer, range) */
+#define LMI_E_UNSUPPORTED 1002 /* valid request this build does not implement */
+#define LMI_E_WORKSPACE 1003   /* workspace too small */
+#define LMI_E_HIP 1004         /* a HIP runtime call failed */
+
+/* bits of the device status word written by lmi_bucket_topk */
+#define LMI_STATUS_QUERY_NOT_F16 1 /* qmode=LMI_Q_F16 but a query is not fp16-exact */
+
+/* ---- element types / modes ------------------------------------------ */
+#define LMI_F32 0
+#define LMI_F16 1
+
+#define LMI_ROUTER_TOPR 0   /* softmax + classes sorted by probability (predict_proba) */
+#define LMI_ROUTER_ARGMAX 1 /* argmax of logits (predict)                               */
+
+#define LMI_Q_F16 0 /* queries are fp16-representable: exact fp16 MFMA path        */
+#define LMI_Q_F32 1 /* general queries: exact-fp32 MFMA path (16x the MFMA time)   */
+
+#define LMI_MAX_LAYERS 8
+#define LMI_MAX_K 16 /* largest k the bucket scan keeps per list in this build */
+
+/* ---- router ----------------------------------------------------------- */
+/* A torch nn.Sequential of nn.Linear layers with ReLU between consecutive
+ * layers (reference model.py:18-83, class Model; the CLI's default 'MLP' is
+ * 96->128->ReLU->C, README/north_star's 'MLP-5' is 96->256->128->C). */
+typedef struct lmi_mlp_desc {
+    int32_t n_layers;                 /* number of nn.Linear layers, 1..LMI_MAX_LAYERS */
+    int32_t dims[LMI_MAX_LAYERS + 1]; /* dims[0]=input width ... dims[n_layers]=n_classes */
+    const float* W[LMI_MAX_LAYERS];   /* device, torch layout [out][in] row-major (y = x W^T + b) */
+    const float* b[LMI_MAX_LAYERS];   /* device, [out] */
+} lmi_mlp_desc;
+
+/* Router inference on nq rows of x (device, [nq][dims[0]] f32, row stride ldx).
+ * mode LMI_ROUTER_TOPR — replaces NeuralNetwork.predict_proba
+ *   (reference model.py:214-229 = softmax(dim=1) then topk(C)):
+ *   classes_out (device, [nq][R] int32) = classes by descending probability,
+ *   ties by ascending class index; probs_out (device, [nq][R] f32, nullable) =
+ *   the matching softmax probabilities.  1 <= R <= n_classes.
+ * mode LMI_ROUTER_ARGMAX — replaces NeuralNetwork.predict (model.py:201-212,
+ *   used for object labels at LearnedIndex.py:240): R must be 1,
+ *   classes_out[q] = argmax of logits (lowest index on ties); probs_out unused. */
+int lmi_router(const float* x, int32_t nq, int32_t ldx, const lmi_mlp_desc* mlp,
+               int32_t R, int32_t mode, int32_t* classes_out, float* probs_out,
+               void* stream);
+
+/* ---- bucket-sorted corpus (one shard) -------------------------------- */
+/* Rows of the search corpus (reference: data_search, clip768 'emb',
+ * search.py:79-84) ordered by bucket label, stable in row order, i.e. the
+ * order in which DataFrame.groupby('category') visits them
+ * (LearnedIndex.py:143-145).  A shard of a G-GPU index holds a contiguous
+ * slice of every bucket; `gpos` maps a local row to its global position in
+ * the unsharded order (the tie-break key; within a bucket it is monotone in
+ * the reference's g.index order). */
+typedef struct lmi_index_desc {
+    const void* corpus;        /* device, [n_rows][d_pad] of dtype, zero-padded past d */
+    int32_t dtype;             /* LMI_F16 (values fp16-exact) or LMI_F32 */
+    int32_t d;                 /* logical vector width (768 for clip768) */
+    int32_t d_pad;             /* row stride in elements, multiple of 32 */
+    int64_t n_rows;            /* rows held by this shard */
+    const float* inv_norm;     /* device [n_rows]: 1/||y|| with sklearn's zero rule */
+    const int32_t* gpos;       /* device [n_rows]: global position of each row */
+    int32_t n_buckets;         /* C (classes of the router) */
+    const int64_t* bucket_off; /* device [C+1]: rows of bucket c are [off[c], off[c+1]) */
+    int32_t chunk_rows;        /* rows per scan chunk (work unit along the corpus) */
+    const int32_t* chunk_first;/* device [C+1]: prefix of ceil(n_c/chunk_rows) (lmi_plan_chunks) */
+    int32_t n_chunks;          /* chunk_first[C] */
+    int32_t max_chunks;        /* max_c ceil(n_c/chunk_rows) */
+} lmi_index_desc;
+
+/* Host helper: fills chunk_first_out[C+1] from host bucket offsets and returns
+ * max chunks per bucket (>= 0) or a negative LMI_E_* code. */
+int32_t lmi_plan_chunks(const int64_t* bucket_off_host, int32_t n_buckets,
+                        int32_t chunk_rows, int32_t* chunk_first_out);
+
+/* Bytes of workspace lmi_bucket_topk needs for this shard and batch. */
+size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
+                                int32_t k, int32_t qmode);
+
+/* Per-(query, probe) exact top-k inside the probed bucket — the build contract
+ * K2 of SURVEY.md §8(a) A4.  Replaces, for every probe r < R of every query,
+ * utils.py:10-11 pairwise_cosine (sklearn normalize + BLAS GEMM), the full-row
+ * argsort at LearnedIndex.py:170-172 and the pandas .loc gathers at :152-153,
+ * :168.  Distances are 1 - cos(q, y) in fp32.
+ *   q        device [nq][ldq] f32, raw query rows (normalised inside, sklearn rule)
+ *   classes  device [nq][R] int32 bucket of probe r (router output)
+ *   out_d    device [nq][R][k] f32 ascending, +inf past the bucket's size
+ *   out_pos  device [nq][R][k] int32 global row positions, -1 past the end
+ *   status   device int32, OR-ed with LMI_STATUS_* bits (caller zeroes it)
+ * 1 <= k <= LMI_MAX_K. */
+int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                    const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
+                    float* out_d, int32_t* out_pos, int32_t* status,
+                    void* workspace, size_t ws_bytes, void* stream);
+
+/* Merge G per-shard lists of the same rows (K3): in
+ * device [G][rows][k] (d f32, pos int32, -1 = empty), out device [rows][k] =
+ * the k smallest by (d, pos).  Used after the RCCL all-gather of a G-GPU index. */
+int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
+                   int32_t k, float* out_d, int32_t* out_pos, void* stream);
+
+/* ---- host replay of the reference's multi-round merge ----------------- */
+/* Reproduces LearnedIndex.search (LearnedIndex.py:22-101) and search_single
+ * (:103-195) — thresholds, per-category groups, the <k padding quirk
+ * (:174-193), the 10000 fillers (utils.py:35-42) and the stable merge
+ * (:86-97) — from the per-(query, probe) lists of lmi_bucket_topk
+ * (SURVEY.md §8(a) A5).  All pointers are host memory.
+ *   classes   [nq][R] int32;  lists_d / lists_pos [nq][R][k_list] (from device)
+ *   k_round   length of one round's result: search_single's k.  search()
+ *             never passes its k down (LearnedIndex.py:75-81), so it is 10
+ *             there; search.py:134-140 passes k for the R == 1 path.
+ *   k_final   search()'s k: columns kept by every merge (LearnedIndex.py:91)
+ *   bucket_size [C] int64 objects per category (0 = category absent from
+ *               data_navigation, so groupby never visits it)
+ *   pos_to_id [n_total] int64  DataFrame index label of each global position
+ *   use_threshold  0/1 as the reference's argument (search.py:127 passes True)
+ *   thr_round0 [nq] float64 or NULL: search_single's threshold_dist argument
+ *             (LearnedIndex.py:110, :149-163) for a direct R == 1 call
+ *   dists_out [nq][w] float64, anns_out [nq][w] uint32 with w = k_round if
+ *             R == 1 else k_final (*w_out receives w).
+ * Returns LMI_E_INVALID where the reference's own assert (LearnedIndex.py:99)
+ * would fail (k_final larger than the merged width). */
+int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+               const float* lists_d, const int32_t* lists_pos, int32_t k_round,
+               int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
+               const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
+               const double* thr_round0, double* dists_out, uint32_t* anns_out,
+               int32_t* w_out);
+
+/* ---- kernel timing (measurement only) -------------------------------------- */
+/* While enabled, lmi_bucket_topk records a HIP event pair on its stream around
+ * its scan kernel (the roofline kernel).  lmi_timing_read waits for the pairs
+ * recorded so far, writes up to max_n durations (ms) and clears the record;
+ * it returns the number written or a negative LMI_E_* code.  Not for use
+ * under graph capture. */
+int lmi_timing_enable(int32_t on);
+int32_t lmi_timing_read(float* ms_out, int32_t max_n);
+
+/* ---- misc --------------------------------------------------------------- */
+const char* lmi_last_error(void);
+int32_t lmi_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LMI_HIP_H */

@@ -1,0 +1,353 @@
+"""CPU restatement of the reference's LMI search hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and only as the checker (or as the
+timed CPU baseline "port").  The product path (li/, liblmi_hip.so) never
+calls it; there is no CPU fallback.
+
+Every function restates a piece of TerkaSlan/sisap23-laion-challenge-learned-index
+(paths relative to that repository) with numpy, in the reference's dtypes:
+
+  normalize            sklearn.preprocessing.normalize as used by
+                       utils.py:10-11 (cosine_similarity) and search.py:50-52
+  pairwise_cosine      utils.py:10-11
+  pairwise_cosine_threshold  utils.py:14-43
+  mlp_forward / predict_proba / predict   model.py:15-83, :201-229
+  search_single_direct / search_direct   LearnedIndex.py:22-195, restated
+                       line by line (full distance matrices, no shortcut)
+  bucket_lists + replay  the decomposition the GPU path implements
+                       
+
+Parity is pinned: tests/test_oracle_golden.py checks search_direct and the
+router against fixtures produced by running the reference itself
+(tests/golden/gen_golden.py), and checks bucket_lists + replay against
+search_direct.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+FILL = 10_000.0  # LearnedIndex.py:138, utils.py:35
+
+
+# ---------------------------------------------------------------------------
+# distances (utils.py)
+# ---------------------------------------------------------------------------
+def _float_dtype(x, y):
+    # sklearn _return_float_dtype: float32 only if both are float32
+    return np.float32 if (x.dtype == np.float32 and y.dtype == np.float32) else np.float64
+
+
+def normalize(x: np.ndarray) -> np.ndarray:
+    """sklearn normalize(norm='l2'): x / sqrt(einsum(x*x)), norms < 10*eps -> 1."""
+    x = np.array(x, copy=True)
+    norms = np.sqrt(np.einsum("ij,ij->i", x, x))
+    norms[norms < 10 * np.finfo(norms.dtype).eps] = 1.0
+    x /= norms[:, None]
+    return x
+
+
+def pairwise_cosine(x, y):
+    """utils.py:10-11: 1 - cosine_similarity(x, y)."""
+    dt = _float_dtype(np.asarray(x), np.asarray(y))
+    xn = normalize(np.asarray(x, dtype=dt))
+    yn = normalize(np.asarray(y, dtype=dt))
+    return 1 - xn @ yn.T
+
+
+def pairwise_cosine_threshold(x, y, threshold, cat_idxs, k=10):
+    """utils.py:14-43 (returns (None, t) when nothing beats the threshold)."""
+    result = pairwise_cosine(x, y)
+    thresh_consistent = np.repeat(threshold[cat_idxs, np.newaxis], result.shape[1], 1)
+    relevant_dists = np.where(result < thresh_consistent)
+    relevant_object_ids = np.unique(relevant_dists[1])
+    max_idx = relevant_object_ids.shape[0]
+    if max_idx == 0:
+        return None, 0.0
+    max_idx = max_idx if max_idx > k else k
+    output_arr = np.full(shape=(result.shape[0], max_idx), fill_value=FILL, dtype=float)
+    mapping = dict(zip(relevant_object_ids, np.arange(relevant_object_ids.shape[0])))
+    output_arr_2nd_dim = np.array([mapping[v] for v in relevant_dists[1]])
+    to_be_added = result[relevant_dists[0], relevant_dists[1]]
+    output_arr[relevant_dists[0], output_arr_2nd_dim] = to_be_added
+    return output_arr, relevant_object_ids, 0.0
+
+
+# ---------------------------------------------------------------------------
+# router (model.py)
+# ---------------------------------------------------------------------------
+def mlp_forward(x: np.ndarray, layers) -> np.ndarray:
+    """Linear/ReLU stack, torch layout W[out][in]: y = x W^T + b (fp32)."""
+    h = np.asarray(x, dtype=np.float32)
+    for i, (w, b) in enumerate(layers):
+        h = h @ np.asarray(w, np.float32).T + np.asarray(b, np.float32)
+        if i + 1 < len(layers):
+            h = np.maximum(h, 0)
+    return h.astype(np.float32)
+
+
+def softmax(logits: np.ndarray) -> np.ndarray:
+    m = logits.max(axis=1, keepdims=True)
+    e = np.exp(logits - m)
+    return (e / e.sum(axis=1, keepdims=True)).astype(np.float32)
+
+
+def rank_classes(logits: np.ndarray) -> np.ndarray:
+    """Classes by descending logit, ties to the lower index (= topk of softmax)."""
+    n, c = logits.shape
+    idx = np.broadcast_to(np.arange(c), (n, c))
+    return np.lexsort((idx, -logits.astype(np.float64)), axis=1).astype(np.int64)
+
+
+def predict_proba(x, layers):
+    """model.py:214-229: (probs sorted desc, classes) over all classes."""
+    logits = mlp_forward(x, layers)
+    probs = softmax(logits)
+    classes = rank_classes(logits)
+    return np.take_along_axis(probs, classes, axis=1), classes
+
+
+def predict(x, layers):
+    """model.py:201-212: argmax of the logits (first index on ties)."""
+    return np.argmax(mlp_forward(x, layers), axis=1).astype(np.int64)
+
+
+# ---------------------------------------------------------------------------
+# literal restatement of LearnedIndex.search / search_single
+# ---------------------------------------------------------------------------
+def _stable_argsort_rows(a: np.ndarray) -> np.ndarray:
+    # the reference's quicksort on rows of <= 16 values is numpy<=1.24's
+    # insertion sort, i.e. stable; longer rows only matter through ties
+    return np.argsort(a, kind="stable", axis=-1)
+
+
+def search_single_direct(labels, ids, data_search, queries_search, pred_categories, k=10,
+                         threshold_dist=None):
+    """LearnedIndex.py:103-195 with data_navigation = (labels, ids) in row order
+    and data_search rows aligned with ids."""
+    labels = np.asarray(labels)
+    ids = np.asarray(ids)
+    nq = queries_search.shape[0]
+    nns = np.zeros((nq, k), dtype=np.uint32)
+    dists = np.full(shape=(nq, k), fill_value=FILL, dtype=float)
+    for cat in np.unique(labels):                          # groupby('category'), ascending
+        rows = np.nonzero(labels == cat)[0]                 # g, in row order
+        cat_idxs = np.where(pred_categories == cat)[0]      # :144
+        bucket_obj_indexes = ids[rows]                      # :145 g.index
+        if bucket_obj_indexes.shape[0] != 0 and cat_idxs.shape[0] != 0:
+            if threshold_dist is not None:
+                seq = pairwise_cosine_threshold(queries_search[cat_idxs], data_search[rows],
+                                                threshold_dist, cat_idxs, k)
+                if seq[0] is None:
+                    continue
+                bucket_obj_indexes = bucket_obj_indexes[seq[1]]
+                seq = seq[0]
+            else:
+                seq = pairwise_cosine(queries_search[cat_idxs], data_search[rows])
+            ann_relative = _stable_argsort_rows(seq)[:, :k if k < seq.shape[1] else seq.shape[1]]
+            if bucket_obj_indexes.shape[0] < k:             # :174-190
+                pad_needed = (k - bucket_obj_indexes.shape[0]) // 2 + 1
+                bucket_obj_indexes = np.pad(np.array(bucket_obj_indexes), pad_needed, "edge")[:k]
+                ann_relative = np.pad(ann_relative[0], pad_needed, "edge")[:k].reshape(1, -1)
+                seq = np.pad(seq[0], pad_needed, "edge")[:k].reshape(1, -1)
+                _, i = np.unique(seq, return_index=True)
+                duplicates_i = np.setdiff1d(np.arange(k), i)
+                seq[0][duplicates_i] = FILL
+            nns[cat_idxs] = np.array(bucket_obj_indexes)[ann_relative]
+            dists[cat_idxs] = np.take_along_axis(seq, ann_relative, axis=1)
+    return dists, nns
+
+
+def search_direct(labels, ids, data_search, queries_search, classes, n_buckets=1, k=10,
+                  use_threshold=False):
+    """LearnedIndex.py:22-101 given the router's classes (nq, >=R)."""
+    anns_final = dists_final = None
+    for bucket in range(n_buckets):
+        threshold_dist = dists_final.max(axis=1) if (bucket != 0 and use_threshold) else None
+        dists, anns = search_single_direct(labels, ids, data_search, queries_search,
+                                           classes[:, bucket], threshold_dist=threshold_dist)
+        if anns_final is None:
+            anns_final, dists_final = anns, dists
+        else:
+            anns_final = np.hstack((anns_final, anns))
+            dists_final = np.hstack((dists_final, dists))
+            idx_sorted = dists_final.argsort(kind="stable", axis=1)[:, :k]
+            dists_final = np.take_along_axis(dists_final, idx_sorted, axis=1)
+            anns_final = np.take_along_axis(anns_final, idx_sorted, axis=1)
+            assert anns_final.shape == dists_final.shape == (queries_search.shape[0], k)
+    return dists_final, anns_final
+
+
+# ---------------------------------------------------------------------------
+# decomposition: per-(query, probe) lists + replay
+# ---------------------------------------------------------------------------
+def layout(labels, n_buckets):
+    """Bucket-sorted order (stable in row order) and bucket offsets."""
+    lab = np.asarray(labels).astype(np.int64)
+    order = np.argsort(lab, kind="stable")
+    off = np.zeros(n_buckets + 1, np.int64)
+    np.cumsum(np.bincount(lab, minlength=n_buckets), out=off[1:])
+    return order, off
+
+
+def bucket_lists(labels, data_search, queries_search, classes, R, k, n_buckets):
+    """Exact per-(q, r) top-k inside bucket classes[q, r], ordered by
+    (distance, position), padded with (inf, -1).  Distances are computed per
+    (r, c) group with the same shapes the reference uses (LearnedIndex.py:166-169)."""
+    order, off = layout(labels, n_buckets)
+    nq = queries_search.shape[0]
+    out_d = np.full((nq, R, k), np.inf, np.float32)
+    out_p = np.full((nq, R, k), -1, np.int32)
+    for r in range(R):
+        col = classes[:, r]
+        for c in np.unique(col):
+            if c < 0 or c >= n_buckets:
+                continue
+            a, b = off[c], off[c + 1]
+            if a == b:
+                continue
+            G = np.nonzero(col == c)[0]
+            D = pairwise_cosine(queries_search[G], data_search[order[a:b]])
+            pos = np.arange(a, b)
+            for gi, q in enumerate(G):
+                row = D[gi]
+                o = np.lexsort((pos, row))[:k]
+                out_d[q, r, : o.size] = row[o]
+                out_p[q, r, : o.size] = pos[o]
+    return out_d, out_p
+
+
+def _edge_take(a, p, k):
+    return np.pad(np.asarray(a), p, "edge")[:k]
+
+
+def _quirk(row, u_pos, kr):
+    ann = np.argsort(np.asarray(row, dtype=np.float64), kind="stable")
+    p = (kr - len(u_pos)) // 2 + 1
+    ids_p = _edge_take(u_pos, p, kr)
+    ann_p = _edge_take(ann, p, kr)
+    row_p = _edge_take(np.asarray(row, np.float64), p, kr).copy()
+    _, i = np.unique(row_p, return_index=True)
+    row_p[np.setdiff1d(np.arange(kr), i)] = FILL
+    return row_p[ann_p], ids_p[ann_p]
+
+
+def replay(classes, lists_d, lists_pos, *, k_round, k_final, bucket_size, pos_to_id,
+           use_threshold, thr_round0=None):
+    """Python twin of lmi_replay (csrc/lmi_replay.cpp): LearnedIndex.py:22-195
+    replayed from the per-(query, probe) lists."""
+    classes = np.asarray(classes)
+    if classes.ndim == 1:
+        classes = classes[:, None]
+    nq, R = classes.shape
+    kr = k_round
+    lists_d = np.asarray(lists_d).reshape(nq, R, -1)
+    lists_pos = np.asarray(lists_pos).reshape(nq, R, -1)
+    F_d = F_p = None
+    for r in range(R):
+        Dd = np.full((nq, kr), FILL)
+        Dp = np.full((nq, kr), -1, np.int64)
+        thresholded = (r > 0 and use_threshold) or (r == 0 and thr_round0 is not None)
+        if thresholded:
+            thr = np.asarray(thr_round0, np.float64) if r == 0 else F_d.max(axis=1)
+        col = classes[:, r]
+        for c in range(len(bucket_size)):
+            G = np.nonzero(col == c)[0]
+            if G.size == 0 or bucket_size[c] <= 0:
+                continue
+            if thresholded:
+                B = {}
+                for q in G:
+                    sel = []
+                    for j in range(min(kr, lists_d.shape[2])):
+                        d, p = float(lists_d[q, r, j]), int(lists_pos[q, r, j])
+                        if p < 0 or not d < thr[q]:
+                            break
+                        sel.append((d, p))
+                    B[q] = sel
+                U = sorted({p for q in G for _, p in B[q]})
+                if not U:
+                    continue
+                if len(U) >= kr:
+                    for q in G:
+                        ent = list(B[q])[:kr]
+                        mine = {p for _, p in ent}
+                        ent += [(FILL, p) for p in U if p not in mine][: kr - len(ent)]
+                        Dd[q] = [e[0] for e in ent]
+                        Dp[q] = [e[1] for e in ent]
+                else:
+                    q0 = G[0]
+                    row = np.full(kr, FILL)
+                    for d, p in B[q0]:
+                        row[U.index(p)] = d
+                    dd, pp = _quirk(row, np.asarray(U), kr)
+                    Dd[G] = dd
+                    Dp[G] = pp
+            else:
+                n = int(bucket_size[c])
+                if n >= kr:
+                    Dd[G] = lists_d[G, r, :kr]
+                    Dp[G] = lists_pos[G, r, :kr]
+                else:
+                    q0 = G[0]
+                    ent = sorted((int(lists_pos[q0, r, j]), float(lists_d[q0, r, j])) for j in range(n))
+                    dd, pp = _quirk([e[1] for e in ent], np.asarray([e[0] for e in ent]), kr)
+                    Dd[G] = dd
+                    Dp[G] = pp
+        if r == 0:
+            F_d, F_p = Dd, Dp
+        else:
+            cd = np.hstack((F_d, Dd))
+            cp = np.hstack((F_p, Dp))
+            o = cd.argsort(kind="stable", axis=1)[:, :k_final]
+            F_d = np.take_along_axis(cd, o, axis=1)
+            F_p = np.take_along_axis(cp, o, axis=1)
+            assert F_d.shape == (nq, k_final)
+    anns = np.where(F_p >= 0, np.asarray(pos_to_id)[np.maximum(F_p, 0)], 0).astype(np.uint32)
+    return F_d.astype(np.float64), anns
+
+
+def search_via_lists(labels, ids, data_search, queries_search, classes, n_buckets, R, k=10,
+                     use_threshold=False, k_round=10):
+    """bucket_lists + replay: must equal search_direct."""
+    order, off = layout(labels, n_buckets)
+    d, p = bucket_lists(labels, data_search, queries_search, classes, R, k_round, n_buckets)
+    return replay(classes[:, :R], d, p, k_round=k_round, k_final=k,
+                  bucket_size=np.diff(off), pos_to_id=np.asarray(ids)[order],
+                  use_threshold=use_threshold)
+
+
+# ---------------------------------------------------------------------------
+# comparator
+# ---------------------------------------------------------------------------
+def compare_lists(d_a, p_a, d_b, p_b, *, atol=1e-5, tie=1e-6):
+    """Tie-aware comparison of per-row sorted lists.
+
+    A row matches when (a) the finite masks agree and |d_a - d_b| <= atol
+    elementwise, and (b) every position whose ids differ is explained by a
+    tie: list b's id sits elsewhere in list a at a distance within `tie` of
+    this position, or — if a does not hold it at all — its distance is within
+    `tie` of a's last entry (the k-th place was cut inside a run of ties).
+    Returns the number of rows that do not match."""
+    d_a = np.asarray(d_a, np.float64)
+    k = d_a.shape[-1]
+    d_a = d_a.reshape(-1, k)
+    d_b = np.asarray(d_b, np.float64).reshape(-1, k)
+    p_a = np.asarray(p_a).reshape(-1, k)
+    p_b = np.asarray(p_b).reshape(-1, k)
+    bad = 0
+    for i in range(d_a.shape[0]):
+        fa, fb = np.isfinite(d_a[i]), np.isfinite(d_b[i])
+        if not np.array_equal(fa, fb) or np.any(np.abs(d_a[i][fa] - d_b[i][fb]) > atol):
+            bad += 1
+            continue
+        for j in np.nonzero(p_a[i] != p_b[i])[0]:
+            where = np.nonzero(p_a[i] == p_b[i][j])[0]
+            if where.size:
+                ok = abs(d_a[i][where[0]] - d_a[i][j]) <= tie
+            else:
+                ok = abs(d_b[i][j] - d_a[i][fa][-1]) <= tie if fa.any() else False
+            if not ok:
+                bad += 1
+                break
+    return bad

@@ -1,0 +1,100 @@
+// Shared helpers of liblmi_hip.so: error plumbing for the C-ABI and the
+// (distance, position) key used by every top-k list on the device.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/lmi_hip.h"
+
+namespace lmi {
+
+// ---- error plumbing (no exception crosses the C-ABI) -------------------
+void set_error(const char* fmt, ...);
+
+#define LMI_CHECK_ARG(cond, ...)              \
+    do {                                      \
+        if (!(cond)) {                        \
+            ::lmi::set_error(__VA_ARGS__);    \
+            return LMI_E_INVALID;             \
+        }                                     \
+    } while (0)
+
+#define LMI_HIP_TRY(expr)                                                        \
+    do {                                                                         \
+        hipError_t e_ = (expr);                                                  \
+        if (e_ != hipSuccess) {                                                  \
+            ::lmi::set_error("%s failed: %s", #expr, hipGetErrorString(e_));     \
+            return LMI_E_HIP;                                                    \
+        }                                                                        \
+    } while (0)
+
+#define LMI_LAUNCH_CHECK(name)                                                   \
+    do {                                                                         \
+        hipError_t e_ = hipGetLastError();                                       \
+        if (e_ != hipSuccess) {                                                  \
+            ::lmi::set_error("launch of %s failed: %s", name, hipGetErrorString(e_)); \
+            return LMI_E_HIP;                                                    \
+        }                                                                        \
+    } while (0)
+
+// ---- keys ------------------------------------------------------------------
+// A list entry is one u64: high word = order-preserving image of the fp32
+// distance, low word = row position.  u64 "<" is then the reference's
+// (distance, position) order (LearnedIndex.py:170 argsort of a row whose
+// columns are in g.index order; :91 stable merge), and the all-ones key is
+// "empty" (sorts after every finite and infinite distance).
+constexpr uint64_t kEmptyKey = ~0ull;
+
+__host__ __device__ inline uint32_t f2ord(float f) {
+    uint32_t b;
+    __builtin_memcpy(&b, &f, 4);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+__host__ __device__ inline float ord2f(uint32_t o) {
+    uint32_t b = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+    float f;
+    __builtin_memcpy(&f, &b, 4);
+    return f;
+}
+
+__host__ __device__ inline uint64_t make_key(float d, uint32_t pos) {
+    return (static_cast<uint64_t>(f2ord(d)) << 32) | pos;
+}
+
+// Largest distance a candidate may have and still beat `thr` (conservative:
+// ord(d) <= hi(thr) is necessary for key < thr).
+__device__ inline float key_dist_bound(uint64_t thr) {
+    uint32_t hi = static_cast<uint32_t>(thr >> 32);
+    if (hi == 0xffffffffu) return __builtin_inff();
+    if (hi == 0u) return -__builtin_inff();
+    return ord2f(hi);
+}
+
+// Insert `x` into the ascending register list L[0..KL), dropping the largest.
+// Caller guarantees x < L[KL-1].  Fully unrolled: every index is a constant,
+// so the list stays in VGPRs (runtime-indexed arrays go to scratch).
+template <int KL>
+__device__ inline void list_insert(uint64_t (&L)[KL], uint64_t x) {
+#pragma unroll
+    for (int i = KL - 1; i > 0; --i) {
+        const uint64_t prev = L[i - 1];
+        const uint64_t cur = L[i];
+        L[i] = (x < prev) ? prev : ((x < cur) ? x : cur);
+    }
+    L[0] = (x < L[0]) ? x : L[0];
+}
+
+template <int KL>
+__device__ inline void list_clear(uint64_t (&L)[KL]) {
+#pragma unroll
+    for (int i = 0; i < KL; ++i) L[i] = kEmptyKey;
+}
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace lmi

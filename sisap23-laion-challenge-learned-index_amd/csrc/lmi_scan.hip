@@ -1,0 +1,765 @@
+// K2 — per-(query, probe) exact top-k inside the probed bucket (gfx950).
+//
+// Replaces, for every probe r < R of every query, the reference's
+//   utils.py:10-11   pairwise_cosine = 1 - sklearn cosine_similarity
+//                    (normalize both sides, BLAS GEMM),
+//   LearnedIndex.py:170-172  full-row argsort, first k,
+//   LearnedIndex.py:152-153, :168  pandas .loc gathers of the bucket rows,
+// with one bucket-major pass over the corpus.
+//
+// Pipeline (all on one stream, no host synchronisation, no allocation):
+//   prep_kernel        queries -> fp16 (or fp32) padded rows + 1/||q||;
+//                      output lists pre-filled with (+inf, -1)
+//   plan_count_kernel  (query, probe) pairs per bucket
+//   plan_fill_kernel   pairs grouped by bucket (ascending q), and the tile
+//                      list: tile = (bucket, chunk of <= chunk_rows rows,
+//                      block of <= QB pairs), chunk-major so the query blocks
+//                      that re-read one chunk run back to back (L2 / MALL)
+//   scan_kernel        persistent; each workgroup dequeues tiles.  The QB
+//                      query rows of a tile sit in LDS; each wave streams
+//                      32-row sub-tiles of the chunk from HBM straight into
+//                      MFMA A fragments and multiplies them against all QB
+//                      queries (v_mfma_f32_32x32x16_f16: exact fp16 products,
+//                      fp32 accumulation; or v_mfma_f32_32x32x2_f32 for fp32
+//                      data).  The top-k epilogue runs on the accumulators:
+//                      d = 1 - dot/(|q||y|), a threshold filter against the
+//                      query's current k-th key (shared by all partial lists
+//                      of the query through an LDS atomic-min), survivors
+//                      appended to a per-lane LDS queue and inserted into a
+//                      per-lane register list in lockstep.  At the end of the
+//                      tile the 8 partial lists of each query are merged and
+//                      written as the tile's chunk list.
+//   chunk_merge_kernel per pair: merge its bucket's chunk lists -> top-k,
+//                      positions -> global positions.
+#include "lmi_common.hpp"
+
+#include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+namespace lmi {
+namespace {
+
+using half8 = _Float16 __attribute__((ext_vector_type(8)));
+using half4 = _Float16 __attribute__((ext_vector_type(4)));
+using f32x16 = float __attribute__((ext_vector_type(16)));
+using f32x4 = float __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kWaves = 4;
+constexpr int kQCap = 16;      // queue entries per lane (= candidates of one 32x32 tile)
+
+struct Tile {
+    int32_t c;        // bucket
+    int32_t pp0;      // first pair position (into the bucket-grouped pair list)
+    int32_t np;       // pairs in this tile (<= QB)
+    int32_t chunk;    // chunk index inside the bucket
+};
+
+struct ScanArgs {
+    const void* corpus;
+    int32_t d_pad;
+    const float* inv_norm;
+    const int64_t* bucket_off;
+    int32_t chunk_rows;
+    int32_t max_chunks;
+    const void* qbuf;       // [nq][d_pad] f16 or f32
+    const float* invq;      // [nq]
+    const int32_t* pair_q;  // [P] pair id p = q*R + r, grouped by bucket
+    int32_t R;
+    const Tile* tiles;
+    const int32_t* ntiles;
+    int32_t* work;          // dequeue counter
+    uint64_t* partial;      // [P][max_chunks][KL]
+};
+
+// ---------------------------------------------------------------------------
+// prep
+// ---------------------------------------------------------------------------
+template <bool F16>
+__global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict__ q, int32_t nq,
+                                                        int32_t ldq, int32_t d, int32_t d_pad,
+                                                        void* __restrict__ qbuf,
+                                                        float* __restrict__ invq,
+                                                        int32_t* __restrict__ status,
+                                                        float* __restrict__ out_d,
+                                                        int32_t* __restrict__ out_pos,
+                                                        int32_t out_per_q) {
+    __shared__ float red[kThreads / 64];
+    const int row = blockIdx.x;
+    const int tid = threadIdx.x;
+    const float* src = q + (size_t)row * ldq;
+    float ss = 0.0f;
+    bool inexact = false;
+    for (int c = tid; c < d_pad; c += kThreads) {
+        const float v = (c < d) ? src[c] : 0.0f;
+        ss = fmaf(v, v, ss);
+        if constexpr (F16) {
+            const _Float16 h = (_Float16)v;
+            inexact |= ((float)h != v);
+            reinterpret_cast<_Float16*>(qbuf)[(size_t)row * d_pad + c] = h;
+        } else {
+            reinterpret_cast<float*>(qbuf)[(size_t)row * d_pad + c] = v;
+        }
+    }
+    // wave + block reduction of the squared norm
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    if constexpr (F16) {
+        if (__any(inexact) && (tid & 63) == 0) atomicOr(status, LMI_STATUS_QUERY_NOT_F16);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float t = 0.0f;
+        for (int w = 0; w < kThreads / 64; ++w) t += red[w];
+        const float n = sqrtf(t);
+        // sklearn _handle_zeros_in_scale: norms < 10*eps are replaced by 1
+        invq[row] = (n < 10.0f * 1.1920929e-07f) ? 1.0f : 1.0f / n;
+    }
+    for (int e = tid; e < out_per_q; e += kThreads) {
+        out_d[(size_t)row * out_per_q + e] = __builtin_inff();
+        out_pos[(size_t)row * out_per_q + e] = -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// plan
+// ---------------------------------------------------------------------------
+__device__ inline int block_sum(int v, int* sh) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < kThreads / 64; ++w) t += sh[w];
+    return t;
+}
+
+__global__ __launch_bounds__(kThreads) void plan_count_kernel(const int32_t* __restrict__ classes,
+                                                              int32_t P, int32_t* __restrict__ counts) {
+    __shared__ int sh[kThreads / 64];
+    const int c = blockIdx.x;
+    int n = 0;
+    for (int e = threadIdx.x; e < P; e += kThreads) n += (classes[e] == c) ? 1 : 0;
+    n = block_sum(n, sh);
+    if (threadIdx.x == 0) counts[c] = n;
+}
+
+__global__ __launch_bounds__(kThreads) void plan_fill_kernel(
+    const int32_t* __restrict__ classes, int32_t P, int32_t C, const int32_t* __restrict__ counts,
+    const int32_t* __restrict__ chunk_first, int32_t QB, int32_t* __restrict__ pair_q,
+    int32_t* __restrict__ pair_bucket, Tile* __restrict__ tiles, int32_t* __restrict__ ntiles,
+    int32_t* __restrict__ work) {
+    __shared__ int sh[kThreads / 64];
+    __shared__ int wcnt[kThreads / 64];
+    const int c = blockIdx.x;
+    const int tid = threadIdx.x;
+    auto tiles_of = [&](int b) {
+        const int nch = chunk_first[b + 1] - chunk_first[b];
+        return nch * ((counts[b] + QB - 1) / QB);
+    };
+    int off = 0, toff = 0;
+    for (int b = tid; b < c; b += kThreads) {
+        off += counts[b];
+        toff += tiles_of(b);
+    }
+    off = block_sum(off, sh);
+    toff = block_sum(toff, sh);
+    const int cnt = counts[c];
+    const int nch = chunk_first[c + 1] - chunk_first[c];
+    const int nqb = (cnt + QB - 1) / QB;
+    if (c == C - 1 && tid == 0) {
+        *ntiles = toff + nch * nqb;
+        *work = 0;
+    }
+    if (cnt == 0) return;
+    // ordered fill of this bucket's pairs (ascending pair id = ascending q)
+    const int lane = tid & 63, w = tid >> 6;
+    int run = 0;
+    for (int base = 0; base < P; base += kThreads) {
+        const int e = base + tid;
+        const bool pred = (e < P) && (classes[e] == c);
+        const uint64_t m = __ballot(pred);
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        __syncthreads();
+        if (lane == 0) wcnt[w] = __popcll(m);
+        __syncthreads();
+        int wpre = 0, tot = 0;
+        for (int i = 0; i < kThreads / 64; ++i) {
+            wpre += (i < w) ? wcnt[i] : 0;
+            tot += wcnt[i];
+        }
+        if (pred) {
+            pair_q[off + run + wpre + rank] = e;
+            pair_bucket[off + run + wpre + rank] = c;
+        }
+        run += tot;
+    }
+    for (int i = tid; i < nch * nqb; i += kThreads) {
+        const int j = i / nqb, b = i - j * nqb;
+        Tile t;
+        t.c = c;
+        t.pp0 = off + b * QB;
+        t.np = min(QB, cnt - b * QB);
+        t.chunk = j;
+        tiles[toff + i] = t;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// scan
+// ---------------------------------------------------------------------------
+template <int KL, bool F16MATH>
+struct ScanCfg {
+    static constexpr int QB = F16MATH ? 64 : 32;  // queries per tile
+    static constexpr int NQF = QB / 32;            // 32-query MFMA fragments per wave
+    static constexpr int QPAD = F16MATH ? 8 : 4;   // LDS row pad (elements): 16 B
+    using QT = typename std::conditional<F16MATH, _Float16, float>::type;
+};
+
+template <int KL, bool F16MATH>
+size_t scan_lds_bytes(int d_pad) {
+    using Cfg = ScanCfg<KL, F16MATH>;
+    const size_t qs = (size_t)Cfg::QB * (d_pad + Cfg::QPAD) * sizeof(typename Cfg::QT);
+    const size_t merge = (size_t)Cfg::QB * 2 * kWaves * KL * sizeof(uint64_t);
+    const size_t queue = (size_t)kWaves * kQCap * 64 * sizeof(uint64_t);
+    return std::max(qs, merge) + queue + Cfg::QB * (sizeof(uint64_t) + sizeof(float)) + 16;
+}
+
+// The epilogue of one 32x32 accumulator tile: lane holds query column
+// (lane & 31) and rows (reg&3) + 8*(reg>>2) + 4*(lane>>5), reg = 0..15
+// (C/D layout of the 32x32 MFMAs, dtype-independent on gfx950).
+template <int KL>
+__device__ inline void tile_epilogue(const f32x16& acc, uint64_t (&L)[KL], uint64_t* thr_slot,
+                                     float invq, const float* __restrict__ inv_norm,
+                                     uint32_t row_base, int valid_rows, uint64_t* queue,
+                                     int lane) {
+    const int h = lane >> 5;
+    uint64_t thr = *thr_slot;
+    float bound = key_dist_bound(thr);
+    int cnt = 0;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const bool valid = i < valid_rows;
+        const float inv = valid ? inv_norm[row_base + i] : 0.0f;
+        const float d = fmaf(-acc[reg], invq * inv, 1.0f);
+        if (valid && d <= bound) {
+            const uint64_t key = make_key(d, row_base + (uint32_t)i);
+            if (key < thr) {
+                queue[cnt * 64] = key;
+                ++cnt;
+            }
+        }
+    }
+    for (int i = 0; __any(i < cnt); ++i) {
+        if (i < cnt) {
+            const uint64_t key = queue[i * 64];
+            if (key < L[KL - 1]) list_insert<KL>(L, key);
+        }
+    }
+    // publish this partial list's k-th key; the query's bound is the min
+    // over its partial lists (the union's k-th is <= each partial k-th).
+    if (L[KL - 1] < thr) atomicMin(reinterpret_cast<unsigned long long*>(thr_slot),
+                                   (unsigned long long)L[KL - 1]);
+}
+
+template <int KL, bool F16MATH, typename TC>
+__global__ __launch_bounds__(kThreads, 1) void scan_kernel(ScanArgs a) {
+    using Cfg = ScanCfg<KL, F16MATH>;
+    using QT = typename Cfg::QT;
+    constexpr int QB = Cfg::QB, NQF = Cfg::NQF;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+    const int d_pad = a.d_pad;
+    const int ldq = d_pad + Cfg::QPAD;
+    const size_t qs_bytes = std::max((size_t)QB * ldq * sizeof(QT),
+                                     (size_t)QB * 2 * kWaves * KL * sizeof(uint64_t));
+    QT* Qs = reinterpret_cast<QT*>(smem);
+    uint64_t* mergebuf = reinterpret_cast<uint64_t*>(smem);  // aliases Qs after the scan
+    uint64_t* queue_all = reinterpret_cast<uint64_t*>(smem + qs_bytes);
+    uint64_t* thr_s = queue_all + kWaves * kQCap * 64;
+    float* invq_s = reinterpret_cast<float*>(thr_s + QB);
+    // no static __shared__ in this kernel: it would shift the dynamic base
+    // off 16-B alignment and every ds_read_b128 would replay (guide G17)
+    int& s_tile = *reinterpret_cast<int*>(invq_s + QB);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int h = lane >> 5;
+    const int col = lane & 31;
+    uint64_t* queue = queue_all + wave * kQCap * 64 + lane;
+
+    const TC* __restrict__ corpus = reinterpret_cast<const TC*>(a.corpus);
+    const QT* __restrict__ qbuf = reinterpret_cast<const QT*>(a.qbuf);
+    const int ntiles = *a.ntiles;
+
+    for (;;) {
+        if (tid == 0) s_tile = atomicAdd(a.work, 1);
+        __syncthreads();
+        const int t = s_tile;
+        if (t >= ntiles) break;
+        const Tile tile = a.tiles[t];
+        const int64_t bstart = a.bucket_off[tile.c];
+        const int64_t bend = a.bucket_off[tile.c + 1];
+        const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
+        const int nrows = (int)std::min<int64_t>(a.chunk_rows, bend - row0);
+
+        // ---- stage the tile's queries (16 B per lane per step) ----------
+        {
+            constexpr int EPV = 16 / sizeof(QT);
+            const int vpr = d_pad / EPV;
+            for (int e = tid; e < QB * vpr; e += kThreads) {
+                const int r = e / vpr, v = e - r * vpr;
+                uint4 val = make_uint4(0, 0, 0, 0);
+                if (r < tile.np) {
+                    const int q = a.pair_q[tile.pp0 + r] / a.R;
+                    val = *reinterpret_cast<const uint4*>(qbuf + (size_t)q * d_pad + v * EPV);
+                }
+                *reinterpret_cast<uint4*>(Qs + r * ldq + v * EPV) = val;
+            }
+            for (int r = tid; r < QB; r += kThreads) {
+                const bool live = r < tile.np;
+                invq_s[r] = live ? a.invq[a.pair_q[tile.pp0 + r] / a.R] : 0.0f;
+                thr_s[r] = live ? kEmptyKey : 0ull;  // dead slots reject everything
+            }
+        }
+        __syncthreads();
+
+        uint64_t L[NQF][KL];
+#pragma unroll
+        for (int f = 0; f < NQF; ++f) list_clear<KL>(L[f]);
+
+        const int nsub = (nrows + 31) / 32;
+        for (int st = wave; st < nsub; st += kWaves) {
+            const int sub0 = st * 32;
+            const int myrow = std::min(sub0 + col, nrows - 1);
+            const TC* yrow = corpus + (size_t)(row0 + myrow) * d_pad;
+            f32x16 acc[NQF];
+#pragma unroll
+            for (int f = 0; f < NQF; ++f)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[f][i] = 0.0f;
+
+            if constexpr (F16MATH) {
+                // 64-wide k block: lane half h covers k = kb + 32h + [0, 32);
+                // MFMA step s (0..3), element j  <->  k = kb + 32h + 8s + j.
+                // A and B use the same permutation of k, so the dot is exact.
+                static_assert(sizeof(TC) == 2, "fp16 math needs an fp16 corpus");
+                const half8* ysrc = reinterpret_cast<const half8*>(yrow) + 4 * h;
+                half8 acur[4], anext[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) acur[s] = ysrc[s];
+                const int nkb = d_pad / 64;
+                for (int kb = 0; kb < nkb; ++kb) {
+                    if (kb + 1 < nkb) {
+#pragma unroll
+                        for (int s = 0; s < 4; ++s) anext[s] = ysrc[(kb + 1) * 8 + s];
+                    }
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                        for (int f = 0; f < NQF; ++f) {
+                            const half8 b = *reinterpret_cast<const half8*>(
+                                Qs + (32 * f + col) * ldq + kb * 64 + 32 * h + 8 * s);
+                            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(acur[s], b, acc[f], 0, 0, 0);
+                        }
+                    }
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) acur[s] = anext[s];
+                }
+                // d_pad is a multiple of 32: a trailing 32-wide half block
+                if (d_pad % 64) {
+                    const int kb = nkb;
+                    // only lane-half h covers k = kb*64 + 16h + [0,16) here
+                    const half8* ys2 = reinterpret_cast<const half8*>(yrow + kb * 64) + 2 * h;
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const half8 av = ys2[s];
+#pragma unroll
+                        for (int f = 0; f < NQF; ++f) {
+                            const half8 b = *reinterpret_cast<const half8*>(
+                                Qs + (32 * f + col) * ldq + kb * 64 + 16 * h + 8 * s);
+                            acc[f] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, b, acc[f], 0, 0, 0);
+                        }
+                    }
+                }
+            } else {
+                // fp32 math, 32-wide k block: lane half h covers kb + 16h + [0,16);
+                // group s (0..3) of 4 MFMAs 32x32x2, element j <-> k = kb + 16h + 4s + j.
+                const int nkb = d_pad / 32;
+                for (int kb = 0; kb < nkb; ++kb) {
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        f32x4 av;
+                        if constexpr (sizeof(TC) == 2) {
+                            const half4 hv = *reinterpret_cast<const half4*>(yrow + kb * 32 + 16 * h + 4 * s);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) av[j] = (float)hv[j];
+                        } else {
+                            av = *reinterpret_cast<const f32x4*>(yrow + kb * 32 + 16 * h + 4 * s);
+                        }
+#pragma unroll
+                        for (int f = 0; f < NQF; ++f) {
+                            const f32x4 b = *reinterpret_cast<const f32x4*>(
+                                Qs + (32 * f + col) * ldq + kb * 32 + 16 * h + 4 * s);
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                acc[f] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], b[j], acc[f], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+
+            const uint32_t row_base = (uint32_t)(row0 + sub0);
+            const int valid_rows = nrows - sub0;
+#pragma unroll
+            for (int f = 0; f < NQF; ++f) {
+                const int qslot = 32 * f + col;
+                tile_epilogue<KL>(acc[f], L[f], &thr_s[qslot], invq_s[qslot], a.inv_norm, row_base,
+                                  valid_rows, queue, lane);
+            }
+        }
+        __syncthreads();  // all waves done with Qs -> reuse as merge buffer
+
+        // ---- merge the 2*kWaves partial lists of every query --------------
+        // list index of (wave, half) = 2*wave + h; layout [qslot][list][KL]
+#pragma unroll
+        for (int f = 0; f < NQF; ++f) {
+            uint64_t* dst = mergebuf + ((size_t)(32 * f + col) * (2 * kWaves) + 2 * wave + h) * KL;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) dst[i] = L[f][i];
+        }
+        __syncthreads();
+        if (tid < tile.np) {
+            const uint64_t* src = mergebuf + (size_t)tid * (2 * kWaves) * KL;
+            uint64_t M[KL];
+#pragma unroll
+            for (int i = 0; i < KL; ++i) M[i] = src[i];
+            for (int l = 1; l < 2 * kWaves; ++l) {
+                for (int i = 0; i < KL; ++i) {
+                    const uint64_t key = src[l * KL + i];
+                    if (key >= M[KL - 1]) break;
+                    list_insert<KL>(M, key);
+                }
+            }
+            uint64_t* out = a.partial + ((size_t)(tile.pp0 + tid) * a.max_chunks + tile.chunk) * KL;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) out[i] = M[i];
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// chunk merge
+// ---------------------------------------------------------------------------
+template <int KL>
+__global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
+    const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
+    const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ counts_total_src,
+    const int32_t* __restrict__ chunk_first, const int32_t* __restrict__ gpos, int32_t P, int32_t k,
+    float* __restrict__ out_d, int32_t* __restrict__ out_pos) {
+    const int pp = blockIdx.x * kThreads + threadIdx.x;
+    if (pp >= P) return;
+    const int c = pair_bucket[pp];
+    if (c < 0) return;
+    const int nch = chunk_first[c + 1] - chunk_first[c];
+    uint64_t M[KL];
+    list_clear<KL>(M);
+    for (int j = 0; j < nch; ++j) {
+        const uint64_t* src = partial + ((size_t)pp * max_chunks + j) * KL;
+        for (int i = 0; i < KL; ++i) {
+            const uint64_t key = src[i];
+            if (key >= M[KL - 1]) break;
+            list_insert<KL>(M, key);
+        }
+    }
+    const size_t o = (size_t)pair_q[pp] * k;
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+        if (i < k) {
+            const uint64_t key = M[i];
+            const bool empty = key == kEmptyKey;
+            out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
+            out_pos[o + i] = empty ? -1 : gpos[(uint32_t)key];
+        }
+    }
+    (void)counts_total_src;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct WsLayout {
+    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, ntiles, work, partial, total;
+    int32_t max_tiles;
+};
+
+int pick_kl(int k) { return k <= 10 ? 10 : 16; }
+
+WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
+    WsLayout w{};
+    const int KL = pick_kl(k);
+    const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
+    const int QB = f16math ? 64 : 32;
+    const size_t P = (size_t)nq * R;
+    const size_t esz = f16math ? 2 : 4;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = off;
+        off = align_up(off + bytes, 256);
+        return at;
+    };
+    w.qbuf = take((size_t)nq * idx->d_pad * esz);
+    w.invq = take((size_t)nq * 4);
+    w.counts = take((size_t)idx->n_buckets * 4);
+    w.pair_q = take(P * 4);
+    w.pair_bucket = take(P * 4);
+    // tiles <= sum_c nch_c * ceil(cnt_c/QB) <= sum_c nch_c * (cnt_c/QB + 1)
+    const size_t mt = (P / QB + 1) * (size_t)std::max(idx->max_chunks, 1) + (size_t)idx->n_chunks;
+    w.max_tiles = (int32_t)std::min<size_t>(mt, (size_t)INT32_MAX);
+    w.tiles = take((size_t)w.max_tiles * sizeof(Tile));
+    w.ntiles = take(4);
+    w.work = take(4);
+    w.partial = take(P * (size_t)std::max(idx->max_chunks, 1) * KL * sizeof(uint64_t));
+    w.total = off;
+    return w;
+}
+
+int num_cus() {
+    static int n = 0;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 256;
+    });
+    return n > 0 ? n : 256;
+}
+
+// ---- optional event timing of the scan kernel ------------------------------
+struct Timing {
+    std::mutex mu;
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending, pool;
+};
+Timing& timing() {
+    static Timing t;
+    return t;
+}
+
+int timing_record(hipStream_t s, bool start, std::pair<hipEvent_t, hipEvent_t>& pr) {
+    if (start) {
+        Timing& t = timing();
+        std::lock_guard<std::mutex> g(t.mu);
+        if (!t.pool.empty()) {
+            pr = t.pool.back();
+            t.pool.pop_back();
+        } else {
+            LMI_HIP_TRY(hipEventCreate(&pr.first));
+            LMI_HIP_TRY(hipEventCreate(&pr.second));
+        }
+        LMI_HIP_TRY(hipEventRecord(pr.first, s));
+    } else {
+        LMI_HIP_TRY(hipEventRecord(pr.second, s));
+        Timing& t = timing();
+        std::lock_guard<std::mutex> g(t.mu);
+        t.pending.push_back(pr);
+    }
+    return LMI_OK;
+}
+
+template <int KL, bool F16MATH, typename TC>
+int launch_scan(const ScanArgs& a, int d_pad, hipStream_t s) {
+    const size_t lds = scan_lds_bytes<KL, F16MATH>(d_pad);
+    if (lds > 160 * 1024) {
+        set_error("d_pad=%d needs %zu B of LDS per workgroup", d_pad, lds);
+        return LMI_E_UNSUPPORTED;
+    }
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+        attr_err = hipFuncSetAttribute((const void*)scan_kernel<KL, F16MATH, TC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    LMI_HIP_TRY(attr_err);
+    const bool timed = timing().on;
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (timed) {
+        const int rc = timing_record(s, true, ev);
+        if (rc != LMI_OK) return rc;
+    }
+    hipLaunchKernelGGL((scan_kernel<KL, F16MATH, TC>), dim3(num_cus()), dim3(kThreads), lds, s, a);
+    LMI_LAUNCH_CHECK("scan_kernel");
+    if (timed) return timing_record(s, false, ev);
+    return LMI_OK;
+}
+
+}  // namespace
+}  // namespace lmi
+
+extern "C" int32_t lmi_plan_chunks(const int64_t* bucket_off_host, int32_t n_buckets,
+                                   int32_t chunk_rows, int32_t* chunk_first_out) {
+    using namespace lmi;
+    if (!bucket_off_host || !chunk_first_out || n_buckets < 1 || chunk_rows < 32 || chunk_rows % 32) {
+        set_error("lmi_plan_chunks: bad arguments");
+        return -LMI_E_INVALID;
+    }
+    int32_t maxc = 0;
+    int64_t acc = 0;
+    for (int c = 0; c < n_buckets; ++c) {
+        chunk_first_out[c] = (int32_t)acc;
+        const int64_t n = bucket_off_host[c + 1] - bucket_off_host[c];
+        if (n < 0) {
+            set_error("lmi_plan_chunks: bucket offsets not ascending at %d", c);
+            return -LMI_E_INVALID;
+        }
+        const int64_t nch = (n + chunk_rows - 1) / chunk_rows;
+        maxc = std::max<int32_t>(maxc, (int32_t)nch);
+        acc += nch;
+    }
+    chunk_first_out[n_buckets] = (int32_t)acc;
+    return maxc;
+}
+
+extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
+                                           int32_t k, int32_t qmode) {
+    if (!idx || nq < 0 || R < 1 || k < 1) return 0;
+    return lmi::ws_layout(idx, nq, R, k, qmode).total;
+}
+
+extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                               const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
+                               float* out_d, int32_t* out_pos, int32_t* status, void* workspace,
+                               size_t ws_bytes, void* stream) {
+    using namespace lmi;
+    LMI_CHECK_ARG(idx != nullptr, "null index");
+    LMI_CHECK_ARG(idx->dtype == LMI_F16 || idx->dtype == LMI_F32, "bad corpus dtype");
+    LMI_CHECK_ARG(idx->d >= 1 && idx->d_pad >= idx->d && idx->d_pad % 32 == 0, "bad d/d_pad");
+    LMI_CHECK_ARG(idx->n_buckets >= 1, "n_buckets < 1");
+    LMI_CHECK_ARG(idx->chunk_rows >= 32 && idx->chunk_rows % 32 == 0, "chunk_rows must be a multiple of 32");
+    LMI_CHECK_ARG(idx->n_rows >= 0 && idx->n_rows < (int64_t)UINT32_MAX, "n_rows out of range");
+    LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(qmode == LMI_Q_F16 || qmode == LMI_Q_F32, "bad qmode");
+    LMI_CHECK_ARG(ldq >= idx->d, "ldq < d");
+    if (nq == 0) return LMI_OK;
+    LMI_CHECK_ARG(q && classes && out_d && out_pos && status && workspace, "null pointer");
+    LMI_CHECK_ARG(idx->n_rows == 0 || (idx->corpus && idx->inv_norm && idx->gpos), "null corpus arrays");
+    LMI_CHECK_ARG(idx->bucket_off && idx->chunk_first, "null bucket tables");
+
+    const WsLayout w = ws_layout(idx, nq, R, k, qmode);
+    if (ws_bytes < w.total) {
+        set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
+        return LMI_E_WORKSPACE;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
+    const int QB = f16math ? 64 : 32;
+    const int P = nq * R;
+    const int KL = pick_kl(k);
+
+    if (f16math) {
+        hipLaunchKernelGGL(prep_kernel<true>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
+                           idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
+                           out_pos, R * k);
+    } else {
+        hipLaunchKernelGGL(prep_kernel<false>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
+                           idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
+                           out_pos, R * k);
+    }
+    LMI_LAUNCH_CHECK("prep_kernel");
+    if (idx->n_rows == 0) return LMI_OK;
+
+    int32_t* counts = (int32_t*)(ws + w.counts);
+    int32_t* pair_q = (int32_t*)(ws + w.pair_q);
+    int32_t* pair_bucket = (int32_t*)(ws + w.pair_bucket);
+    Tile* tiles = (Tile*)(ws + w.tiles);
+    int32_t* ntiles = (int32_t*)(ws + w.ntiles);
+    int32_t* work = (int32_t*)(ws + w.work);
+    const int C = idx->n_buckets;
+
+    // pair_bucket = -1 marks pairs whose class is out of range (never filled)
+    LMI_HIP_TRY(hipMemsetAsync(pair_bucket, 0xff, (size_t)P * 4, s));
+    hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kThreads), 0, s, classes, P, counts);
+    LMI_LAUNCH_CHECK("plan_count_kernel");
+    hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kThreads), 0, s, classes, P, C, counts,
+                       idx->chunk_first, QB, pair_q, pair_bucket, tiles, ntiles, work);
+    LMI_LAUNCH_CHECK("plan_fill_kernel");
+
+    ScanArgs a{};
+    a.corpus = idx->corpus;
+    a.d_pad = idx->d_pad;
+    a.inv_norm = idx->inv_norm;
+    a.bucket_off = idx->bucket_off;
+    a.chunk_rows = idx->chunk_rows;
+    a.max_chunks = std::max(idx->max_chunks, 1);
+    a.qbuf = ws + w.qbuf;
+    a.invq = (const float*)(ws + w.invq);
+    a.pair_q = pair_q;
+    a.R = R;
+    a.tiles = tiles;
+    a.ntiles = ntiles;
+    a.work = work;
+    a.partial = (uint64_t*)(ws + w.partial);
+
+    int rc;
+    if (f16math) {
+        rc = (KL == 10) ? launch_scan<10, true, _Float16>(a, idx->d_pad, s)
+                        : launch_scan<16, true, _Float16>(a, idx->d_pad, s);
+    } else if (idx->dtype == LMI_F16) {
+        rc = (KL == 10) ? launch_scan<10, false, _Float16>(a, idx->d_pad, s)
+                        : launch_scan<16, false, _Float16>(a, idx->d_pad, s);
+    } else {
+        rc = (KL == 10) ? launch_scan<10, false, float>(a, idx->d_pad, s)
+                        : launch_scan<16, false, float>(a, idx->d_pad, s);
+    }
+    if (rc != LMI_OK) return rc;
+
+    const int grid = (P + kThreads - 1) / kThreads;
+    if (KL == 10) {
+        hipLaunchKernelGGL(chunk_merge_kernel<10>, dim3(grid), dim3(kThreads), 0, s, a.partial,
+                           a.max_chunks, pair_q, pair_bucket, nullptr, idx->chunk_first, idx->gpos, P,
+                           k, out_d, out_pos);
+    } else {
+        hipLaunchKernelGGL(chunk_merge_kernel<16>, dim3(grid), dim3(kThreads), 0, s, a.partial,
+                           a.max_chunks, pair_q, pair_bucket, nullptr, idx->chunk_first, idx->gpos, P,
+                           k, out_d, out_pos);
+    }
+    LMI_LAUNCH_CHECK("chunk_merge_kernel");
+    return LMI_OK;
+}
+
+extern "C" int lmi_timing_enable(int32_t on) {
+    lmi::Timing& t = lmi::timing();
+    std::lock_guard<std::mutex> g(t.mu);
+    t.on = on != 0;
+    return LMI_OK;
+}
+
+extern "C" int32_t lmi_timing_read(float* ms_out, int32_t max_n) {
+    using namespace lmi;
+    Timing& t = timing();
+    std::lock_guard<std::mutex> g(t.mu);
+    int32_t n = 0;
+    for (auto& pr : t.pending) {
+        if (hipEventSynchronize(pr.second) != hipSuccess) {
+            set_error("hipEventSynchronize failed");
+            return -LMI_E_HIP;
+        }
+        float ms = 0.0f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) != hipSuccess) {
+            set_error("hipEventElapsedTime failed");
+            return -LMI_E_HIP;
+        }
+        if (ms_out && n < max_n) ms_out[n] = ms;
+        ++n;
+        t.pool.push_back(pr);
+    }
+    t.pending.clear();
+    return std::min(n, max_n);
+}

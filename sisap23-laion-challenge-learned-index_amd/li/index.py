@@ -1,0 +1,394 @@
+"""Device-resident LMI index and the search pipeline over liblmi_hip.so.
+
+This is the host side of the hot path (SURVEY.md §3 "Build-side equivalent"):
+
+    queries (HBM) --K1 lmi_router--> classes[:, :R]
+                  --K2 lmi_bucket_topk--> per-(query, probe) top-k lists
+                  [--RCCL all_gather + K3 lmi_merge_topk, G > 1 ranks]
+                  --D2H (nq*R*k*8 B)--> lmi_replay (host C++) --> dists, anns
+
+Layout in HBM (one shard): the search corpus sorted by bucket label, stable in
+row order — the order in which the reference's ``groupby('category')`` visits
+objects (LearnedIndex.py:143-145) — stored fp16 when every value is exactly
+fp16-representable (then the fp16 MFMA products are exact) and fp32 otherwise,
+rows padded to a multiple of 32 elements; per-row 1/||y|| (sklearn's
+``normalize`` zero rule, utils.py:11); the global position of every row (the
+tie-break key); bucket offsets and the chunk table of the scan.
+
+A G-rank index stripes every bucket: rank g holds the g-th contiguous slice of
+each bucket's rows (np.array_split boundaries), so every rank scans 1/G of
+every probed bucket whatever the bucket popularity.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+DEFAULT_CHUNK_ROWS = 8192
+
+
+def _as_torch(x, device=None, dtype=None) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(np.asarray(x)))
+    if dtype is not None and t.dtype != dtype:
+        t = t.to(dtype)
+    if device is not None:
+        t = t.to(device)
+    return t.contiguous()
+
+
+def fp16_exact(x: torch.Tensor) -> bool:
+    """True when every value of the float tensor round-trips through fp16."""
+    x = x.float()
+    return bool(torch.equal(x.half().float(), x))
+
+
+# ---------------------------------------------------------------------------
+# bucket layout (host arithmetic, shared by every rank)
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class BucketLayout:
+    """Bucket-sorted order of the corpus.  Global position p holds row order[p]."""
+
+    n_buckets: int
+    order: np.ndarray        # int64 [n]: row index of each global position
+    bucket_off: np.ndarray   # int64 [C+1] global offsets
+
+    @classmethod
+    def from_labels(cls, labels, n_buckets: int) -> "BucketLayout":
+        lab = np.asarray(labels).astype(np.int64, copy=False).ravel()
+        if lab.size and (lab.min() < 0 or lab.max() >= n_buckets):
+            raise ValueError(f"labels must lie in [0, {n_buckets})")
+        order = np.argsort(lab, kind="stable").astype(np.int64)
+        size = np.bincount(lab, minlength=n_buckets).astype(np.int64)
+        off = np.zeros(n_buckets + 1, np.int64)
+        np.cumsum(size, out=off[1:])
+        return cls(n_buckets, order, off)
+
+    @property
+    def bucket_size(self) -> np.ndarray:
+        return np.diff(self.bucket_off)
+
+    def shard(self, rank: int, world: int):
+        """(global positions of the shard's rows, local bucket offsets [C+1])."""
+        if world == 1:
+            return np.arange(self.bucket_off[-1], dtype=np.int64), self.bucket_off.copy()
+        parts, loc = [], np.zeros(self.n_buckets + 1, np.int64)
+        for c in range(self.n_buckets):
+            a, b = self.bucket_off[c], self.bucket_off[c + 1]
+            n = b - a
+            lo = a + (n * rank) // world
+            hi = a + (n * (rank + 1)) // world
+            parts.append(np.arange(lo, hi, dtype=np.int64))
+            loc[c + 1] = loc[c] + (hi - lo)
+        return (np.concatenate(parts) if parts else np.zeros(0, np.int64)), loc
+
+
+# ---------------------------------------------------------------------------
+# device index
+# ---------------------------------------------------------------------------
+class DeviceIndex:
+    """One shard of the bucket-sorted search corpus, resident in HBM."""
+
+    def __init__(self, data, labels, n_buckets: int, *, ids=None, device=None,
+                 storage: str = "auto", chunk_rows: int = DEFAULT_CHUNK_ROWS,
+                 rank: int = 0, world: int = 1):
+        _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        lab = labels.cpu().numpy() if isinstance(labels, torch.Tensor) else np.asarray(labels)
+        self.layout = BucketLayout.from_labels(lab, n_buckets)
+        self.n_buckets = n_buckets
+        n = int(self.layout.bucket_off[-1])
+        self.n_total = n
+        if ids is None:
+            ids = np.arange(1, n + 1, dtype=np.int64)  # DataFrame.index += 1 (search.py:72)
+        ids = np.asarray(ids).astype(np.int64, copy=False)
+        if ids.shape != (n,):
+            raise ValueError("ids must have one entry per corpus row")
+        self.pos_to_id = ids[self.layout.order]
+        self.bucket_size = self.layout.bucket_size.copy()
+        self.rank, self.world = rank, world
+
+        gpos, loc_off = self.layout.shard(rank, world)
+        rows = torch.from_numpy(self.layout.order[gpos])
+        src = data if isinstance(data, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(data, dtype=np.float32)))
+        if src.dim() != 2 or src.shape[0] != n:
+            raise ValueError("data must be [n, d] with one row per label")
+        if src.dtype not in (torch.float16, torch.float32):
+            src = src.float()
+        self.d = int(src.shape[1])
+        self.d_pad = (self.d + 31) // 32 * 32
+        step = 1 << 20
+        if storage == "auto":
+            storage = "f16" if src.dtype == torch.float16 or all(
+                fp16_exact(src[a:a + step].to(self.device)) for a in range(0, n, step)) else "f32"
+        if storage not in ("f16", "f32"):
+            raise ValueError("storage must be 'auto', 'f16' or 'f32'")
+        self.storage = storage
+        tdt = torch.float16 if storage == "f16" else torch.float32
+        n_rows = int(gpos.size)
+        self.corpus = torch.zeros((n_rows, self.d_pad), dtype=tdt, device=self.device)
+        self.inv_norm = torch.empty((n_rows,), dtype=torch.float32, device=self.device)
+        eps10 = 10 * float(np.finfo(np.float32).eps)
+        for a in range(0, n_rows, step):
+            blk = src.index_select(0, rows[a:a + step].to(src.device)).to(self.device)
+            f = blk.float()
+            if storage == "f16" and blk.dtype != torch.float16 and not fp16_exact(f):
+                raise ValueError("storage='f16' needs fp16-representable data (exact products)")
+            self.corpus[a:a + step, : self.d] = blk.to(tdt)
+            # sklearn normalize: sqrt(einsum(x*x)), norms < 10*eps -> 1 (utils.py:11)
+            norm = torch.sqrt((f * f).sum(dim=1))
+            norm = torch.where(norm < eps10, torch.ones_like(norm), norm)
+            self.inv_norm[a:a + step] = 1.0 / norm
+            del blk, f
+        self.gpos = torch.from_numpy(gpos.astype(np.int32)).to(self.device)
+        self.n_rows = int(gpos.size)
+        self.chunk_rows = int(chunk_rows)
+        cf = np.zeros(n_buckets + 1, np.int32)
+        lib = _lib.load()
+        mx = lib.lmi_plan_chunks(loc_off.ctypes.data, n_buckets, self.chunk_rows, cf.ctypes.data)
+        if mx < 0:
+            check("lmi_plan_chunks", -mx)
+        self.max_chunks = int(mx)
+        self.n_chunks = int(cf[-1])
+        self.bucket_off_local = torch.from_numpy(loc_off).to(self.device)
+        self.chunk_first = torch.from_numpy(cf).to(self.device)
+        self._desc = IndexDescHolder(self)
+        self._ws = {}
+
+    @property
+    def desc(self) -> _lib.IndexDesc:
+        return self._desc.desc
+
+    def workspace(self, nq: int, R: int, k: int, qmode: int) -> torch.Tensor:
+        lib = _lib.load()
+        need = lib.lmi_scan_workspace_bytes(C.byref(self.desc), nq, R, k, qmode)
+        ws = self._ws.get("buf")
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+            self._ws["buf"] = ws
+        return ws
+
+
+class IndexDescHolder:
+    def __init__(self, ix: DeviceIndex):
+        d = _lib.IndexDesc()
+        d.corpus = ptr(ix.corpus)
+        d.dtype = _lib.LMI_F16 if ix.storage == "f16" else _lib.LMI_F32
+        d.d = ix.d
+        d.d_pad = ix.d_pad
+        d.n_rows = ix.n_rows
+        d.inv_norm = ptr(ix.inv_norm)
+        d.gpos = ptr(ix.gpos)
+        d.n_buckets = ix.n_buckets
+        d.bucket_off = ptr(ix.bucket_off_local)
+        d.chunk_rows = ix.chunk_rows
+        d.chunk_first = ptr(ix.chunk_first)
+        d.n_chunks = ix.n_chunks
+        d.max_chunks = ix.max_chunks
+        self.desc = d
+
+
+# ---------------------------------------------------------------------------
+# router
+# ---------------------------------------------------------------------------
+class DeviceRouter:
+    """Weights of a Linear/ReLU stack in HBM, evaluated by K1 (lmi_router)."""
+
+    def __init__(self, layers: Sequence, device=None):
+        _lib.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if not 1 <= len(layers) <= _lib.LMI_MAX_LAYERS:
+            raise ValueError("1..8 Linear layers supported")
+        self.W, self.b = [], []
+        dims = [int(_as_torch(layers[0][0]).shape[1])]
+        for (w, b) in layers:
+            w = _as_torch(w, self.device, torch.float32)
+            b = _as_torch(b, self.device, torch.float32)
+            if w.shape[1] != dims[-1] or b.shape != (w.shape[0],):
+                raise ValueError("inconsistent layer shapes")
+            dims.append(int(w.shape[0]))
+            self.W.append(w)
+            self.b.append(b)
+        self.dims = dims
+        self.n_classes = dims[-1]
+        m = _lib.MlpDesc()
+        m.n_layers = len(self.W)
+        for i, v in enumerate(dims):
+            m.dims[i] = v
+        for i, (w, b) in enumerate(zip(self.W, self.b)):
+            m.W[i] = ptr(w)
+            m.b[i] = ptr(b)
+        self._desc = m
+
+    @classmethod
+    def from_module(cls, module: torch.nn.Module, device=None) -> "DeviceRouter":
+        """From a reference-shaped ``Model`` (model.py:15-83): ``layers`` is a
+        Sequential of Linear with ReLU between consecutive Linears."""
+        seq = getattr(module, "layers", module)
+        mods = list(seq.children()) if isinstance(seq, torch.nn.Sequential) else [seq]
+        layers = []
+        for i, m in enumerate(mods):
+            if isinstance(m, torch.nn.Linear):
+                layers.append((m.weight.detach(), m.bias.detach()))
+            elif isinstance(m, torch.nn.ReLU):
+                if not layers or i == len(mods) - 1:
+                    raise ValueError("ReLU must sit between Linear layers")
+            else:
+                raise ValueError(f"unsupported router layer {type(m).__name__}")
+        for a, b in zip(mods, mods[1:]):
+            if isinstance(a, torch.nn.Linear) and not isinstance(b, torch.nn.ReLU):
+                raise ValueError("expected ReLU after every hidden Linear")
+        return cls(layers, device)
+
+    def topr(self, x: torch.Tensor, R: int, with_probs: bool = False, stream=None):
+        x = _as_torch(x, self.device, torch.float32)
+        nq = x.shape[0]
+        classes = torch.empty((nq, R), dtype=torch.int32, device=self.device)
+        probs = torch.empty((nq, R), dtype=torch.float32, device=self.device) if with_probs else None
+        s = stream if stream is not None else _lib.stream_handle(self.device)
+        check("lmi_router", _lib.load().lmi_router(ptr(x), nq, x.stride(0), C.byref(self._desc), R,
+                                                   _lib.LMI_ROUTER_TOPR, ptr(classes), ptr(probs), s))
+        return classes, probs
+
+    def argmax(self, x: torch.Tensor, stream=None) -> torch.Tensor:
+        x = _as_torch(x, self.device, torch.float32)
+        nq = x.shape[0]
+        out = torch.empty((nq,), dtype=torch.int32, device=self.device)
+        s = stream if stream is not None else _lib.stream_handle(self.device)
+        check("lmi_router", _lib.load().lmi_router(ptr(x), nq, x.stride(0), C.byref(self._desc), 1,
+                                                   _lib.LMI_ROUTER_ARGMAX, ptr(out), 0, s))
+        return out
+
+
+# ---------------------------------------------------------------------------
+# scan / merge / replay
+# ---------------------------------------------------------------------------
+def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
+                qmode: Optional[int] = None, stream=None):
+    """K2 on one shard.  Returns (d [nq,R,k] f32, pos [nq,R,k] int32, status int32 tensor)."""
+    lib = _lib.load()
+    q = _as_torch(q, index.device, torch.float32)
+    classes = _as_torch(classes, index.device, torch.int32)
+    nq, R = classes.shape
+    if q.shape[0] != nq or q.shape[1] != index.d:
+        raise ValueError("query shape does not match the index")
+    if qmode is None:
+        qmode = _lib.LMI_Q_F16 if index.storage == "f16" else _lib.LMI_Q_F32
+    out_d = torch.empty((nq, R, k), dtype=torch.float32, device=index.device)
+    out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
+    status = torch.zeros((1,), dtype=torch.int32, device=index.device)
+    ws = index.workspace(nq, R, k, qmode)
+    s = stream if stream is not None else _lib.stream_handle(index.device)
+    check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(index.desc), ptr(q), nq, q.stride(0),
+                                                 ptr(classes), R, k, qmode, ptr(out_d),
+                                                 ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
+    return out_d, out_pos, status
+
+
+def merge_topk(d_in: torch.Tensor, pos_in: torch.Tensor, k: int, stream=None):
+    """K3: merge [G, rows, k] lists -> [rows, k] by (distance, global position)."""
+    G = d_in.shape[0]
+    rows = d_in[0].numel() // k
+    out_d = torch.empty(d_in.shape[1:], dtype=torch.float32, device=d_in.device)
+    out_pos = torch.empty(d_in.shape[1:], dtype=torch.int32, device=d_in.device)
+    s = stream if stream is not None else _lib.stream_handle(d_in.device)
+    check("lmi_merge_topk", _lib.load().lmi_merge_topk(ptr(d_in.contiguous()), ptr(pos_in.contiguous()),
+                                                       G, rows, k, ptr(out_d), ptr(out_pos), s))
+    return out_d, out_pos
+
+
+def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k_round: int,
+           k_final: int, bucket_size: np.ndarray, pos_to_id: np.ndarray, use_threshold: bool,
+           thr_round0: Optional[np.ndarray] = None):
+    """A5 on the host (lmi_replay): per-(query, probe) lists -> reference output."""
+    classes = np.ascontiguousarray(classes, dtype=np.int32)
+    if classes.ndim == 1:
+        classes = classes[:, None]
+    nq, R = classes.shape
+    lists_d = np.ascontiguousarray(lists_d, dtype=np.float32).reshape(nq, R, -1)
+    lists_pos = np.ascontiguousarray(lists_pos, dtype=np.int32).reshape(nq, R, -1)
+    k_list = lists_d.shape[2]
+    bucket_size = np.ascontiguousarray(bucket_size, dtype=np.int64)
+    pos_to_id = np.ascontiguousarray(pos_to_id, dtype=np.int64)
+    w = k_round if R == 1 else k_final
+    dists = np.empty((nq, w), np.float64)
+    anns = np.empty((nq, w), np.uint32)
+    thr = None
+    if thr_round0 is not None:
+        thr = np.ascontiguousarray(np.asarray(thr_round0, dtype=np.float64).ravel())
+        if thr.shape != (nq,):
+            raise ValueError("threshold_dist must have one value per query")
+    w_out = C.c_int32(0)
+    check("lmi_replay", _lib.load().lmi_replay(
+        classes.ctypes.data, nq, R, k_list, lists_d.ctypes.data, lists_pos.ctypes.data,
+        k_round, k_final, bucket_size.ctypes.data, bucket_size.size, pos_to_id.ctypes.data,
+        pos_to_id.size, int(bool(use_threshold)), ptr(thr), dists.ctypes.data, anns.ctypes.data,
+        C.byref(w_out)))
+    return dists, anns
+
+
+class Searcher:
+    """Runs the whole hot path for one shard set (one process per GPU).
+
+    ``search`` times like search.py:116-141 (router + scan + merge + replay)."""
+
+    def __init__(self, index: DeviceIndex, router: DeviceRouter, group=None):
+        self.index = index
+        self.router = router
+        self.group = group
+        self._pinned = {}
+
+    def _host(self, name, shape, dtype):
+        buf = self._pinned.get(name)
+        if buf is None or tuple(buf.shape) != tuple(shape) or buf.dtype != dtype:
+            buf = torch.empty(shape, dtype=dtype, pin_memory=torch.cuda.is_available())
+            self._pinned[name] = buf
+        return buf
+
+    def lists(self, q_nav: torch.Tensor, q_search: torch.Tensor, R: int, k_list: int,
+              classes: Optional[torch.Tensor] = None):
+        """Device part: router + scan (+ RCCL merge).  Returns device tensors."""
+        if classes is None:
+            classes, _ = self.router.topr(q_nav, R)
+        d, pos, status = bucket_topk(self.index, q_search, classes, k_list)
+        if self.index.world > 1:
+            from .dist import gather_merge
+            d, pos = gather_merge(d, pos, k_list, self.group)
+        return classes, d, pos, status
+
+    def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
+               use_threshold: bool = True, classes: Optional[torch.Tensor] = None):
+        k_list = k_round
+        classes, d, pos, status = self.lists(q_nav, q_search, R, k_list, classes)
+        nq = classes.shape[0]
+        h_cls = self._host("cls", (nq, R), torch.int32)
+        h_d = self._host("d", tuple(d.shape), torch.float32)
+        h_pos = self._host("pos", tuple(pos.shape), torch.int32)
+        h_st = self._host("st", (1,), torch.int32)
+        h_cls.copy_(classes, non_blocking=True)
+        h_d.copy_(d, non_blocking=True)
+        h_pos.copy_(pos, non_blocking=True)
+        h_st.copy_(status, non_blocking=True)
+        torch.cuda.current_stream(self.index.device).synchronize()
+        if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
+            # queries are not fp16-exact: redo the scan with exact fp32 MFMA
+            d, pos, _ = bucket_topk(self.index, q_search, classes, k_list, qmode=_lib.LMI_Q_F32)
+            if self.index.world > 1:
+                from .dist import gather_merge
+                d, pos = gather_merge(d, pos, k_list, self.group)
+            h_d.copy_(d)
+            h_pos.copy_(pos)
+        return replay(h_cls.numpy(), h_d.numpy(), h_pos.numpy(), k_round=k_round, k_final=k,
+                      bucket_size=self.index.bucket_size, pos_to_id=self.index.pos_to_id,
+                      use_threshold=use_threshold)

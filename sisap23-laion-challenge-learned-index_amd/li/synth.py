@@ -1,0 +1,134 @@
+"""Synthetic LAION-like workloads; no dataset is reachable offline.
+
+clip768-like vectors: a Gaussian mixture (centres ~ N(0,1)^d, points =
+centre + noise * N(0,1)), L2-normalised and rounded to fp16 (stored as fp32,
+so every value is fp16-representable, as the SISAP'23 clip768v2 `emb` is
+believed to be).  pca96-like navigation vectors: X @ P with P ~ N(0,1)/sqrt(d)
+fixed by the seed, then L2-normalised (search.py:50-52).
+
+Two generators: a numpy PCG64 one for small, bit-reproducible test cases and
+fixtures, and a torch one that builds 10M-row corpora directly in HBM for the
+benchmark (chunked, counter-free but seeded).  Index building helpers (GPU
+k-means, short router training) stand in for the reference's faiss k-means +
+MLP training (LearnedIndex.py:197-282), which is outside the hot path.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+# ---------------------------------------------------------------------------
+# numpy (small, reproducible)
+# ---------------------------------------------------------------------------
+def np_mixture(n: int, d: int, n_centres: int, seed: int, noise: float = 0.9,
+               centres: np.ndarray | None = None):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    if centres is None:
+        centres = rng.standard_normal((n_centres, d)).astype(np.float32)
+    lab = rng.integers(0, centres.shape[0], n)
+    x = centres[lab] + noise * rng.standard_normal((n, d)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    return x.astype(np.float16).astype(np.float32), centres
+
+
+def np_projection(d: int, d_nav: int, seed: int) -> np.ndarray:
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return (rng.standard_normal((d, d_nav)) / math.sqrt(d)).astype(np.float32)
+
+
+def np_nav(x: np.ndarray, P: np.ndarray) -> np.ndarray:
+    v = (x @ P).astype(np.float32)
+    n = np.sqrt(np.einsum("ij,ij->i", v, v))
+    n[n < 10 * np.finfo(np.float32).eps] = 1.0
+    return (v / n[:, None]).astype(np.float32)
+
+
+def np_router_layers(arch, n_classes: int, seed: int, d_nav: int = 96):
+    """torch-nn.Linear-like init (U(-1/sqrt(in), 1/sqrt(in))), seeded numpy."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    dims = [d_nav] + list(arch) + [n_classes]
+    layers = []
+    for a, b in zip(dims, dims[1:]):
+        bound = 1.0 / math.sqrt(a)
+        layers.append((rng.uniform(-bound, bound, (b, a)).astype(np.float32),
+                       rng.uniform(-bound, bound, (b,)).astype(np.float32)))
+    return layers
+
+
+ARCHS = {"MLP": (128,), "MLP-2": (64,), "MLP-3": (256,), "MLP-4": (512,), "MLP-5": (256, 128),
+         "MLP-6": (32,), "MLP-7": (16,), "MLP-8": (8,)}
+
+
+# ---------------------------------------------------------------------------
+# torch (large, on device)
+# ---------------------------------------------------------------------------
+@torch.no_grad()
+def torch_mixture(n: int, d: int, n_centres: int, seed: int, device, noise: float = 0.9,
+                  centres: torch.Tensor | None = None, out_dtype=torch.float16,
+                  chunk: int = 1 << 20):
+    """n x d fp16-exact rows on `device` (returned in `out_dtype`)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    if centres is None:
+        centres = torch.randn((n_centres, d), generator=g, device=device)
+    out = torch.empty((n, d), dtype=out_dtype, device=device)
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        lab = torch.randint(0, centres.shape[0], (b - a,), generator=g, device=device)
+        x = centres[lab] + noise * torch.randn((b - a, d), generator=g, device=device)
+        x /= x.norm(dim=1, keepdim=True)
+        out[a:b] = x.half().to(out_dtype)
+    return out, centres
+
+
+@torch.no_grad()
+def torch_nav(x: torch.Tensor, P: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
+    out = torch.empty((x.shape[0], P.shape[1]), dtype=torch.float32, device=x.device)
+    for a in range(0, x.shape[0], chunk):
+        v = x[a:a + chunk].float() @ P
+        n = v.norm(dim=1, keepdim=True)
+        n[n < 10 * 1.1920929e-07] = 1.0
+        out[a:a + chunk] = v / n
+    return out
+
+
+@torch.no_grad()
+def kmeans(x: torch.Tensor, k: int, iters: int, seed: int) -> torch.Tensor:
+    """Lloyd's k-means (squared L2), returns centroids [k, d]."""
+    g = torch.Generator(device=x.device)
+    g.manual_seed(seed)
+    cent = x[torch.randperm(x.shape[0], generator=g, device=x.device)[:k]].clone()
+    for _ in range(iters):
+        d2 = (x * x).sum(1, keepdim=True) - 2 * x @ cent.T + (cent * cent).sum(1)[None]
+        lab = d2.argmin(1)
+        s = torch.zeros_like(cent).index_add_(0, lab, x)
+        cnt = torch.bincount(lab, minlength=k).float()[:, None]
+        cent = torch.where(cnt > 0, s / cnt.clamp(min=1), cent)
+    return cent
+
+
+def train_router(x_nav: torch.Tensor, labels: torch.Tensor, arch, n_classes: int, *,
+                 steps: int = 300, batch: int = 4096, lr: float = 0.009, seed: int = 2023):
+    """A short Adam/cross-entropy fit of the reference's Model architecture."""
+    torch.manual_seed(seed)
+    dims = [x_nav.shape[1]] + list(arch) + [n_classes]
+    mods = []
+    for i, (a, b) in enumerate(zip(dims, dims[1:])):
+        mods.append(torch.nn.Linear(a, b))
+        if i + 2 < len(dims):
+            mods.append(torch.nn.ReLU())
+    model = torch.nn.Sequential(*mods).to(x_nav.device)
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    lossf = torch.nn.CrossEntropyLoss()
+    g = torch.Generator(device=x_nav.device)
+    g.manual_seed(seed)
+    for _ in range(steps):
+        idx = torch.randint(0, x_nav.shape[0], (batch,), generator=g, device=x_nav.device)
+        loss = lossf(model(x_nav[idx]), labels[idx])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    return model.eval()

@@ -1,0 +1,101 @@
+"""GPU parity: K1 router, K2 bucket scan, K3 merge and the full search against
+the CPU oracle (oracle/lmi_oracle.py), through the C-ABI (liblmi_hip.so)."""
+import numpy as np
+import pytest
+import torch
+
+import lmi_oracle as O
+import workloads
+from li import _lib
+from li.index import DeviceIndex, DeviceRouter, Searcher, bucket_topk, merge_topk
+
+pytestmark = pytest.mark.gpu
+
+
+def _router_mismatch(classes_gpu, logits, R, gap=1e-5):
+    """Rows whose top-R differs from the oracle and is not explained by a
+    near-tie of logits at the cut."""
+    ref = O.rank_classes(logits)[:, :R]
+    bad = 0
+    for i in np.nonzero((classes_gpu != ref).any(axis=1))[0]:
+        srt = np.sort(logits[i])[::-1]
+        if np.min(np.abs(np.diff(srt[: R + 1]))) > gap:
+            bad += 1
+    return bad
+
+
+@pytest.mark.parametrize("arch", ["MLP", "MLP-5"])
+def test_router_topr_and_argmax(arch):
+    w = workloads.clustered(n=4000, nq=700, C=122, arch=arch, seed=11)
+    r = DeviceRouter(w["layers"])
+    logits = O.mlp_forward(w["qn"], w["layers"])
+    for R in (1, 4, 7, 122):
+        cls, probs = r.topr(torch.from_numpy(w["qn"]).cuda(), R, with_probs=True)
+        cls = cls.cpu().numpy()
+        assert _router_mismatch(cls, logits, R) == 0
+        ref_p = np.take_along_axis(O.softmax(logits), cls.astype(np.int64), axis=1)
+        np.testing.assert_allclose(probs.cpu().numpy(), ref_p, rtol=1e-5, atol=1e-7)
+    am = r.argmax(torch.from_numpy(w["xn"]).cuda()).cpu().numpy()
+    assert (am != O.predict(w["xn"], w["layers"])).sum() <= 1
+
+
+@pytest.mark.parametrize("label_mode", ["router", "skewed"])
+@pytest.mark.parametrize("storage", ["f16", "f32"])
+@pytest.mark.parametrize("k", [10, 3, 16])
+def test_bucket_topk_matches_oracle(label_mode, storage, k):
+    w = workloads.clustered(n=6000, nq=257, C=16, seed=5, label_mode=label_mode)
+    R = 4
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    ix = DeviceIndex(w["x"], w["labels"], w["C"], storage=storage, chunk_rows=512)
+    d, pos, st = bucket_topk(ix, torch.from_numpy(w["q"]).cuda(),
+                             torch.from_numpy(classes.astype(np.int32)).cuda(), k)
+    assert int(st.item()) == 0
+    ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, w["C"])
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), pos.cpu().numpy()) == 0
+
+
+def test_bucket_topk_nonf16_queries_fall_back_exactly():
+    w = workloads.clustered(n=3000, nq=64, C=8, seed=9, label_mode="skewed")
+    q = w["q"] + np.float32(1e-4)  # no longer fp16-representable
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :2]
+    ix = DeviceIndex(w["x"], w["labels"], w["C"], storage="f16", chunk_rows=256)
+    qt = torch.from_numpy(q).cuda()
+    ct = torch.from_numpy(classes.astype(np.int32)).cuda()
+    _, _, st = bucket_topk(ix, qt, ct, 10)
+    assert int(st.item()) & _lib.LMI_STATUS_QUERY_NOT_F16
+    d, pos, _ = bucket_topk(ix, qt, ct, 10, qmode=_lib.LMI_Q_F32)
+    ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], q, classes, 2, 10, w["C"])
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), pos.cpu().numpy()) == 0
+
+
+def test_shard_merge_equals_single_gpu():
+    """Striping + K3 merge gives bitwise the single-shard lists (any G)."""
+    w = workloads.clustered(n=5000, nq=150, C=16, seed=3, label_mode="skewed")
+    R, k = 3, 10
+    classes = torch.from_numpy(
+        O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R].astype(np.int32)).cuda()
+    q = torch.from_numpy(w["q"]).cuda()
+    full = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=256)
+    d1, p1, _ = bucket_topk(full, q, classes, k)
+    for G in (2, 3, 8):
+        parts = [bucket_topk(DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=256, rank=g, world=G),
+                             q, classes, k)[:2] for g in range(G)]
+        dm, pm = merge_topk(torch.stack([p[0] for p in parts]), torch.stack([p[1] for p in parts]), k)
+        assert torch.equal(dm, d1) and torch.equal(pm, p1)
+
+
+@pytest.mark.parametrize("use_threshold", [True, False])
+@pytest.mark.parametrize("R", [1, 4])
+def test_full_search_matches_direct_oracle(use_threshold, R):
+    w = workloads.clustered(n=6000, nq=300, C=16, seed=21, label_mode="skewed")
+    ids = np.arange(1, w["x"].shape[0] + 1)
+    router = DeviceRouter(w["layers"])
+    ix = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=1024)
+    s = Searcher(ix, router)
+    dists, anns = s.search(torch.from_numpy(w["qn"]).cuda(), torch.from_numpy(w["q"]).cuda(), R,
+                           k=10, use_threshold=use_threshold)
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))
+    ref_d, ref_a = O.search_direct(w["labels"], ids, w["x"], w["q"], classes, n_buckets=R, k=10,
+                                   use_threshold=use_threshold)
+    assert dists.shape == ref_d.shape and anns.dtype == np.uint32
+    assert O.compare_lists(ref_d, ref_a, dists, anns) == 0
