@@ -208,6 +208,11 @@ def main():
     ms_step = el / args.steps * 1e3
     value = args.nq / (el / args.steps)
 
+    # per-stage breakdown (separate, synchronised passes; not the timed loop)
+    tm = {}
+    for _ in range(3):
+        searcher.search(qn, q, args.R, k=args.k, use_threshold=True, timings=tm)
+    breakdown = {kk: round(v / 3, 3) for kk, v in tm.items()}
     classes, _ = router.topr(qn, args.R)
     classes = classes.cpu().numpy()
     byts, flops, rows = algorithmic_bytes(index, classes, args.nq)
@@ -242,7 +247,7 @@ def main():
                    "parallelism": f"corpus striped over {world} GPU(s)",
                    "chunk_rows": args.chunk_rows},
         "roofline": roof, "cpu_baseline": cpu,
-        "recall": round(recall, 4), "recall_sample": sample,
+        "recall": round(recall, 4), "recall_sample": sample, "breakdown_ms": breakdown,
     }
     print(json.dumps(out), flush=True)
     if world > 1:

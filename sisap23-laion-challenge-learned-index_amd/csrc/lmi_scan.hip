@@ -34,6 +34,7 @@
 #include "lmi_common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -454,6 +455,263 @@ __global__ __launch_bounds__(kThreads, 1) void scan_kernel(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// scan v2 (fp16 corpus, fp16-exact queries, d_pad == 768): queries in
+// registers, object rows staged once per workgroup through an LDS ring by
+// global_load_lds DMA, shared by the 4 waves (128 queries per staged row).
+//
+//   per wave : 32 queries; their 48 MFMA B fragments (K = 768) live in VGPRs
+//              for the whole tile (192 registers)
+//   per stage: 32 object rows x 256 k (16 KiB) + each wave's copy of the 32
+//              rows' 1/||y||; 7-slot ring, 4 stages in flight, one raw
+//              s_barrier per stage (never __syncthreads inside the ring: its
+//              vmcnt(0) would drain the DMA, guide §5 "Pipelining")
+//   LDS image: row r, 16-B chunk c stored at chunk c ^ (r & 15) (the XOR
+//              is applied to the DMA *source* address, LDS stays lane-linear),
+//              so the 32-row A-fragment ds_read_b128 is bank-conflict free
+//   per block of 32 rows: 48 x v_mfma_f32_32x32x16_f16 per wave, then the
+//              top-k epilogue of v1 with 1/||y|| read from LDS
+// A per-pair threshold in global memory (min over the k-th keys published
+// by finished tiles of the same pair) seeds every tile's filter.
+// ---------------------------------------------------------------------------
+namespace v2 {
+constexpr int D = 768;
+constexpr int KSEG = 256;
+constexpr int NST = D / KSEG;          // stages per 32-row block
+constexpr int ROWB = KSEG * 2;         // bytes of one row in one stage
+constexpr int TRAIL = 4 * 256;         // per-wave copies of the 32 norms
+constexpr int STAGE = 32 * ROWB + TRAIL;
+constexpr int NSLOT = 7;
+constexpr int QB = 128;
+constexpr int NQF = D / 16;            // B fragments per lane
+
+template <int KL>
+constexpr size_t lds_bytes() {
+    return (size_t)NSLOT * STAGE + (size_t)kWaves * kQCap * 64 * 8 + QB * (8 + 4) + 16;
+}
+}  // namespace v2
+
+struct Scan2Args {
+    const _Float16* corpus;
+    const float* inv_norm;
+    const int64_t* bucket_off;
+    int32_t chunk_rows;
+    int32_t max_chunks;
+    const _Float16* qbuf;
+    const float* invq;
+    const int32_t* pair_q;
+    int32_t R;
+    const Tile* tiles;
+    const int32_t* ntiles;
+    int32_t* work;
+    uint64_t* partial;
+    unsigned long long* thr_g;  // [P] per-pair bound, EMPTY at start
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ inline void vm_wait(int n_stages_after) {
+    // wait until at most n*GLDS of this wave's DMA are outstanding
+    switch (n_stages_after) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    }
+}
+
+// MFMA with the B operand (query fragment) and the accumulator in AGPRs.
+// hipcc pads no hazards inside asm: the chain needs none (the previous MFMA's
+// D is this one's C), the first MFMA of a block takes C = 0 (no
+// v_accvgpr_write -> MFMA hazard), and mfma_drain adds the 18 wait states a
+// 16-pass MFMA result needs before a v_accvgpr_read (cdna4_isa §4.2).
+__device__ __forceinline__ f32x16 mfma_first(const half8& a, const half8& b) {
+    f32x16 d;
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&a"(d) : "v"(a), "a"(b));
+    return d;
+}
+__device__ __forceinline__ f32x16 mfma_acc(const f32x16& c, const half8& a, const half8& b) {
+    f32x16 d = c;
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "a"(b));
+    return d;
+}
+__device__ __forceinline__ f32x16 mfma_drain(const f32x16& c) {
+    f32x16 d = c;
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+a"(d));
+    return d;
+}
+
+template <int KL>
+__global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
+    using namespace v2;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* ring = smem;
+    uint64_t* queue_all = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
+    uint64_t* thr_s = queue_all + kWaves * kQCap * 64;
+    float* invq_s = reinterpret_cast<float*>(thr_s + QB);
+    int& s_tile = *reinterpret_cast<int*>(invq_s + QB);
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int h = lane >> 5;
+    const int col = lane & 31;
+    uint64_t* queue = queue_all + wave * kQCap * 64 + lane;
+    const int ntiles = *a.ntiles;
+
+    for (;;) {
+        if (tid == 0) s_tile = atomicAdd(a.work, 1);
+        __syncthreads();
+        const int t = s_tile;
+        if (t >= ntiles) break;
+        const Tile tile = a.tiles[t];
+        const int64_t bstart = a.bucket_off[tile.c];
+        const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
+        const int nrows = (int)std::min<int64_t>(a.chunk_rows, a.bucket_off[tile.c + 1] - row0);
+        const int slot_q = 32 * wave + col;
+        const bool live = slot_q < tile.np;
+        const bool wave_live = 32 * wave < tile.np;
+
+        // ---- this lane's query fragments (B operand), 1/||q||, bound ------
+        half8 qf[NQF];
+        {
+            const int q = live ? a.pair_q[tile.pp0 + slot_q] / a.R : 0;
+            const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
+#pragma unroll
+            for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
+        }
+        if (h == 0) {
+            invq_s[slot_q] = live ? a.invq[a.pair_q[tile.pp0 + slot_q] / a.R] : 0.0f;
+            thr_s[slot_q] = live ? (uint64_t)a.thr_g[tile.pp0 + slot_q] : 0ull;
+        }
+        uint64_t L[KL];
+        list_clear<KL>(L);
+        __syncthreads();
+        const float my_invq = invq_s[slot_q];
+
+        // ---- DMA of one stage: this wave's 8 rows + its copy of the norms --
+        const int nblk = (nrows + 31) / 32;
+        const int T = nblk * NST;
+        auto issue = [&](int st) {
+            const int blk = st / NST, j = st - blk * NST;
+            unsigned char* sl = ring + (st % NSLOT) * STAGE;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = 8 * wave + 2 * i + h;
+                const int grow = std::min(blk * 32 + row, nrows - 1);
+                const int chunk = col ^ (row & 15);
+                const _Float16* src = a.corpus + (size_t)(row0 + grow) * D + j * KSEG + chunk * 8;
+                __builtin_amdgcn_global_load_lds((const void*)src,
+                                                 (lds_ptr_t)(sl + (8 * wave + 2 * i) * ROWB), 16, 0, 0);
+            }
+            const int nrow = std::min(blk * 32 + col, nrows - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(a.inv_norm + row0 + nrow),
+                                             (lds_ptr_t)(sl + 32 * ROWB + wave * 256), 4, 0, 0);
+        };
+
+        const int pro = std::min(T, NSLOT - 1);
+        for (int st = 0; st < pro; ++st) issue(st);
+
+        f32x16 acc;
+        // one iteration = one 32-row block = NST stages, unrolled so the
+        // accumulator stays in one AGPR tuple through its 48 MFMAs
+        for (int blk = 0; blk < nblk; ++blk) {
+#pragma unroll
+            for (int j = 0; j < NST; ++j) {
+                const int s = blk * NST + j;
+                const int issued = std::min(T - 1, s + NSLOT - 2);
+                vm_wait(issued - std::min(s + 1, T - 1));
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (s + NSLOT - 1 < T) issue(s + NSLOT - 1);
+                if (wave_live) {
+                    const unsigned char* rp = ring + (s % NSLOT) * STAGE + col * ROWB;
+                    // A fragment of step tt: row `col`, logical chunk 2tt+h (XOR-swizzled)
+#define LMI_A(tt) (*reinterpret_cast<const half8*>(rp + (((2 * (tt) + h) ^ (col & 15)) << 4)))
+                    if (j == 0) acc = mfma_first(LMI_A(0), qf[0]);
+                    else acc = mfma_acc(acc, LMI_A(0), qf[j * 16]);
+#pragma unroll
+                    for (int tt = 1; tt < 16; ++tt) acc = mfma_acc(acc, LMI_A(tt), qf[j * 16 + tt]);
+#undef LMI_A
+                }
+            }
+            if (wave_live) {
+                const int s = blk * NST + NST - 1;
+                const unsigned char* sl = ring + (s % NSLOT) * STAGE;
+                {
+                    acc = mfma_drain(acc);  // MFMA result -> VALU reader wait states
+                    // ---- top-k epilogue of the 32-row block ------------------
+                    const float* nrm = reinterpret_cast<const float*>(sl + 32 * ROWB + wave * 256);
+                    const int sub0 = blk * 32;
+                    const uint32_t row_base = (uint32_t)(row0 + sub0);
+                    const int valid_rows = nrows - sub0;
+                    uint64_t* thr_slot = &thr_s[slot_q];
+                    const uint64_t thr = *thr_slot;
+                    const float bound = key_dist_bound(thr);
+                    float dv[16];
+                    bool anyp = false;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const f32x4 inv4 = *reinterpret_cast<const f32x4*>(nrm + 8 * g + 4 * h);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const int reg = 4 * g + e;
+                            const int i = e + 8 * g + 4 * h;
+                            const float d = fmaf(-acc[reg], my_invq * inv4[e], 1.0f);
+                            dv[reg] = (i < valid_rows) ? d : __builtin_inff();
+                            anyp |= dv[reg] <= bound;
+                        }
+                    }
+                    if (__any(anyp)) {
+                        int cnt = 0;
+#pragma unroll
+                        for (int reg = 0; reg < 16; ++reg) {
+                            const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                            if (dv[reg] <= bound) {
+                                const uint64_t key = make_key(dv[reg], row_base + (uint32_t)i);
+                                if (key < thr) {
+                                    queue[cnt * 64] = key;
+                                    ++cnt;
+                                }
+                            }
+                        }
+                        for (int i = 0; __any(i < cnt); ++i) {
+                            if (i < cnt) {
+                                const uint64_t key = queue[i * 64];
+                                if (key < L[KL - 1]) list_insert<KL>(L, key);
+                            }
+                        }
+                        if (L[KL - 1] < thr)
+                            atomicMin(reinterpret_cast<unsigned long long*>(thr_slot),
+                                      (unsigned long long)L[KL - 1]);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // ring drained: every DMA was waited for above
+
+        // ---- merge the two partial lists of each query (lanes col, col+32) ----
+        uint64_t* mb = queue_all + (size_t)wave * 64 * KL;
+#pragma unroll
+        for (int i = 0; i < KL; ++i) mb[i * 64 + lane] = L[i];
+        __syncthreads();
+        if (h == 0 && live) {
+#pragma unroll
+            for (int i = 0; i < KL; ++i) {
+                const uint64_t key = mb[i * 64 + lane + 32];
+                if (key >= L[KL - 1]) break;
+                list_insert<KL>(L, key);
+            }
+            const int pp = tile.pp0 + slot_q;
+            uint64_t* out = a.partial + ((size_t)pp * a.max_chunks + tile.chunk) * KL;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) out[i] = L[i];
+            if (L[KL - 1] != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)L[KL - 1]);
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // chunk merge
 // ---------------------------------------------------------------------------
 template <int KL>
@@ -494,9 +752,16 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
 // host side
 // ---------------------------------------------------------------------------
 struct WsLayout {
-    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, ntiles, work, partial, total;
+    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, ntiles, work, partial, thr_g, total;
     int32_t max_tiles;
+    int32_t qb;      // queries per tile
+    bool use_v2;     // scan2_kernel
 };
+
+bool v2_eligible(const lmi_index_desc* idx, int qmode) {
+    if (getenv("LMI_SCAN_V1")) return false;  // diagnostic switch: force the general kernel
+    return idx->dtype == LMI_F16 && qmode == LMI_Q_F16 && idx->d_pad == v2::D;
+}
 
 int pick_kl(int k) { return k <= 10 ? 10 : 16; }
 
@@ -504,7 +769,9 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     WsLayout w{};
     const int KL = pick_kl(k);
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
-    const int QB = f16math ? 64 : 32;
+    w.use_v2 = v2_eligible(idx, qmode);
+    const int QB = w.use_v2 ? v2::QB : (f16math ? 64 : 32);
+    w.qb = QB;
     const size_t P = (size_t)nq * R;
     const size_t esz = f16math ? 2 : 4;
     size_t off = 0;
@@ -525,6 +792,7 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     w.ntiles = take(4);
     w.work = take(4);
     w.partial = take(P * (size_t)std::max(idx->max_chunks, 1) * KL * sizeof(uint64_t));
+    w.thr_g = take(P * sizeof(uint64_t));
     w.total = off;
     return w;
 }
@@ -598,6 +866,29 @@ int launch_scan(const ScanArgs& a, int d_pad, hipStream_t s) {
     return LMI_OK;
 }
 
+template <int KL>
+int launch_scan2(const Scan2Args& b, hipStream_t s) {
+    constexpr size_t lds = v2::lds_bytes<KL>();
+    static_assert(lds <= 160 * 1024, "scan2 LDS budget");
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+        attr_err = hipFuncSetAttribute((const void*)scan2_kernel<KL>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    LMI_HIP_TRY(attr_err);
+    const bool timed = timing().on;
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (timed) {
+        const int rc = timing_record(s, true, ev);
+        if (rc != LMI_OK) return rc;
+    }
+    hipLaunchKernelGGL(scan2_kernel<KL>, dim3(num_cus()), dim3(kThreads), lds, s, b);
+    LMI_LAUNCH_CHECK("scan2_kernel");
+    if (timed) return timing_record(s, false, ev);
+    return LMI_OK;
+}
+
 }  // namespace
 }  // namespace lmi
 
@@ -659,7 +950,7 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     auto* ws = reinterpret_cast<unsigned char*>(workspace);
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
-    const int QB = f16math ? 64 : 32;
+    const int QB = w.qb;
     const int P = nq * R;
     const int KL = pick_kl(k);
 
@@ -708,7 +999,25 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     a.partial = (uint64_t*)(ws + w.partial);
 
     int rc;
-    if (f16math) {
+    if (w.use_v2) {
+        Scan2Args b{};
+        b.corpus = reinterpret_cast<const _Float16*>(idx->corpus);
+        b.inv_norm = idx->inv_norm;
+        b.bucket_off = idx->bucket_off;
+        b.chunk_rows = idx->chunk_rows;
+        b.max_chunks = a.max_chunks;
+        b.qbuf = reinterpret_cast<const _Float16*>(ws + w.qbuf);
+        b.invq = a.invq;
+        b.pair_q = pair_q;
+        b.R = R;
+        b.tiles = tiles;
+        b.ntiles = ntiles;
+        b.work = work;
+        b.partial = a.partial;
+        b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
+        LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
+        rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
+    } else if (f16math) {
         rc = (KL == 10) ? launch_scan<10, true, _Float16>(a, idx->d_pad, s)
                         : launch_scan<16, true, _Float16>(a, idx->d_pad, s);
     } else if (idx->dtype == LMI_F16) {

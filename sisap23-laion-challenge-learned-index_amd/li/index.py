@@ -368,9 +368,33 @@ class Searcher:
         return classes, d, pos, status
 
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
-               use_threshold: bool = True, classes: Optional[torch.Tensor] = None):
+               use_threshold: bool = True, classes: Optional[torch.Tensor] = None,
+               timings: Optional[dict] = None):
+        """Whole hot path for one batch -> (dists f64 [nq, w], anns u32 [nq, w]).
+
+        `timings` (measurement only) receives per-stage wall times in ms; the
+        stages are then separated by stream synchronisations."""
+        import time
         k_list = k_round
-        classes, d, pos, status = self.lists(q_nav, q_search, R, k_list, classes)
+        dev = self.index.device
+        sync = (lambda: torch.cuda.current_stream(dev).synchronize()) if timings is not None else None
+        t0 = time.perf_counter()
+        if classes is None:
+            classes, _ = self.router.topr(q_nav, R)
+        if sync:
+            sync()
+            t1 = time.perf_counter()
+            timings["router"] = timings.get("router", 0.0) + (t1 - t0) * 1e3
+            t0 = t1
+        d, pos, status = bucket_topk(self.index, q_search, classes, k_list)
+        if self.index.world > 1:
+            from .dist import gather_merge
+            d, pos = gather_merge(d, pos, k_list, self.group)
+        if sync:
+            sync()
+            t1 = time.perf_counter()
+            timings["scan"] = timings.get("scan", 0.0) + (t1 - t0) * 1e3
+            t0 = t1
         nq = classes.shape[0]
         h_cls = self._host("cls", (nq, R), torch.int32)
         h_d = self._host("d", tuple(d.shape), torch.float32)
@@ -380,7 +404,11 @@ class Searcher:
         h_d.copy_(d, non_blocking=True)
         h_pos.copy_(pos, non_blocking=True)
         h_st.copy_(status, non_blocking=True)
-        torch.cuda.current_stream(self.index.device).synchronize()
+        torch.cuda.current_stream(dev).synchronize()
+        if timings is not None:
+            t1 = time.perf_counter()
+            timings["d2h"] = timings.get("d2h", 0.0) + (t1 - t0) * 1e3
+            t0 = t1
         if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
             # queries are not fp16-exact: redo the scan with exact fp32 MFMA
             d, pos, _ = bucket_topk(self.index, q_search, classes, k_list, qmode=_lib.LMI_Q_F32)
@@ -389,6 +417,9 @@ class Searcher:
                 d, pos = gather_merge(d, pos, k_list, self.group)
             h_d.copy_(d)
             h_pos.copy_(pos)
-        return replay(h_cls.numpy(), h_d.numpy(), h_pos.numpy(), k_round=k_round, k_final=k,
-                      bucket_size=self.index.bucket_size, pos_to_id=self.index.pos_to_id,
-                      use_threshold=use_threshold)
+        out = replay(h_cls.numpy(), h_d.numpy(), h_pos.numpy(), k_round=k_round, k_final=k,
+                     bucket_size=self.index.bucket_size, pos_to_id=self.index.pos_to_id,
+                     use_threshold=use_threshold)
+        if timings is not None:
+            timings["replay"] = timings.get("replay", 0.0) + (time.perf_counter() - t0) * 1e3
+        return out
