@@ -233,9 +233,14 @@ def _quirk(row, u_pos, kr):
 
 
 def replay(classes, lists_d, lists_pos, *, k_round, k_final, bucket_size, pos_to_id,
-           use_threshold, thr_round0=None):
+           use_threshold, thr_round0=None, stats=None):
     """Python twin of lmi_replay (csrc/lmi_replay.cpp): LearnedIndex.py:22-195
-    replayed from the per-(query, probe) lists."""
+    replayed from the per-(query, probe) lists.  `stats` (a dict) counts the
+    branches taken: groups, quirk0 (bucket < k), quirk_thr (|U| < k),
+    skipped (no object beats the threshold), fillers."""
+    st = stats if stats is not None else {}
+    for key in ("groups", "quirk0", "quirk_thr", "skipped", "fillers"):
+        st.setdefault(key, 0)
     classes = np.asarray(classes)
     if classes.ndim == 1:
         classes = classes[:, None]
@@ -255,6 +260,7 @@ def replay(classes, lists_d, lists_pos, *, k_round, k_final, bucket_size, pos_to
             G = np.nonzero(col == c)[0]
             if G.size == 0 or bucket_size[c] <= 0:
                 continue
+            st["groups"] += 1
             if thresholded:
                 B = {}
                 for q in G:
@@ -267,15 +273,19 @@ def replay(classes, lists_d, lists_pos, *, k_round, k_final, bucket_size, pos_to
                     B[q] = sel
                 U = sorted({p for q in G for _, p in B[q]})
                 if not U:
+                    st["skipped"] += 1
                     continue
                 if len(U) >= kr:
                     for q in G:
                         ent = list(B[q])[:kr]
                         mine = {p for _, p in ent}
-                        ent += [(FILL, p) for p in U if p not in mine][: kr - len(ent)]
+                        fill = [(FILL, p) for p in U if p not in mine][: kr - len(ent)]
+                        st["fillers"] += len(fill)
+                        ent += fill
                         Dd[q] = [e[0] for e in ent]
                         Dp[q] = [e[1] for e in ent]
                 else:
+                    st["quirk_thr"] += 1
                     q0 = G[0]
                     row = np.full(kr, FILL)
                     for d, p in B[q0]:
@@ -289,6 +299,7 @@ def replay(classes, lists_d, lists_pos, *, k_round, k_final, bucket_size, pos_to
                     Dd[G] = lists_d[G, r, :kr]
                     Dp[G] = lists_pos[G, r, :kr]
                 else:
+                    st["quirk0"] += 1
                     q0 = G[0]
                     ent = sorted((int(lists_pos[q0, r, j]), float(lists_d[q0, r, j])) for j in range(n))
                     dd, pp = _quirk([e[1] for e in ent], np.asarray([e[0] for e in ent]), kr)

@@ -138,7 +138,9 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
         }
     }
 
-    std::vector<Entry> F((size_t)nq * w), Dr((size_t)nq * kr);
+    // F holds round 0 (k_round wide) and every merge (k_final wide)
+    const int fs = std::max(kr, w);
+    std::vector<Entry> F((size_t)nq * fs), Dr((size_t)nq * kr);
     int wF = 0;
     std::vector<int> order(nq), start(n_buckets + 1);
     std::vector<double> thr(nq);
@@ -151,8 +153,8 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
             for (int q = 0; q < nq; ++q) thr[q] = thr_round0[q];
         } else if (thresholded) {
             for (int q = 0; q < nq; ++q) {
-                double m = F[(size_t)q * w].d;
-                for (int j = 1; j < wF; ++j) m = std::max(m, F[(size_t)q * w + j].d);
+                double m = F[(size_t)q * fs].d;
+                for (int j = 1; j < wF; ++j) m = std::max(m, F[(size_t)q * fs + j].d);
                 thr[q] = m;
             }
         }
@@ -278,24 +280,24 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
         // merge (LearnedIndex.py:82-97)
         if (r == 0) {
             for (int q = 0; q < nq; ++q)
-                for (int j = 0; j < kr; ++j) F[(size_t)q * w + j] = Dr[(size_t)q * kr + j];
+                for (int j = 0; j < kr; ++j) F[(size_t)q * fs + j] = Dr[(size_t)q * kr + j];
             wF = kr;
         } else {
             const int wn = std::min(k_final, wF + kr);
             cat.resize(wF + kr);
             for (int q = 0; q < nq; ++q) {
-                for (int j = 0; j < wF; ++j) cat[j] = F[(size_t)q * w + j];
+                for (int j = 0; j < wF; ++j) cat[j] = F[(size_t)q * fs + j];
                 for (int j = 0; j < kr; ++j) cat[wF + j] = Dr[(size_t)q * kr + j];
                 std::stable_sort(cat.begin(), cat.end(),
                                  [](const Entry& a, const Entry& b) { return a.d < b.d; });
-                for (int j = 0; j < wn; ++j) F[(size_t)q * w + j] = cat[j];
+                for (int j = 0; j < wn; ++j) F[(size_t)q * fs + j] = cat[j];
             }
             wF = wn;
         }
     }
     for (int q = 0; q < nq; ++q) {
         for (int j = 0; j < w; ++j) {
-            const Entry& e = F[(size_t)q * w + j];
+            const Entry& e = F[(size_t)q * fs + j];
             dists_out[(size_t)q * w + j] = e.d;
             int64_t id = 0;
             if (e.pos >= 0) {
