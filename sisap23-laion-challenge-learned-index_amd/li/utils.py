@@ -1,0 +1,47 @@
+"""I/O helpers of the reference's search/li/utils.py that sit around the hot path.
+
+The distance helpers of the reference (pairwise_cosine, utils.py:10-11, and
+pairwise_cosine_threshold, :14-43) are replaced as a whole by the GPU scan
+(lmi_bucket_topk) plus the host replay; they are not re-exported here so that
+no CPU distance path exists in the product package.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+from pathlib import Path
+
+
+def save_as_pickle(filename: str, obj):
+    """utils.py:46-60."""
+    with open(filename, "wb") as f:
+        pickle.dump(obj, f)
+
+
+def prepare(kind, size):
+    """utils.py:71-82 downloads the SISAP'23 files; offline builds only accept
+    files that are already in place."""
+    for version in ("query", "dataset"):
+        target = os.path.join("data", kind, size, f"{version}.h5")
+        if not os.path.exists(target):
+            raise FileNotFoundError(
+                f"{target} missing: this build has no network access (utils.py:63-82 would download it)")
+
+
+def store_results(dst, algo, kind, dists, anns, buildtime, querytime, params, size):
+    """utils.py:85-97: HDF5 with attrs algo/data/buildtime/querytime/size/params
+    and datasets knns (anns dtype, uint32) and dists (float64), read by eval/."""
+    try:
+        import h5py
+    except ImportError as e:
+        raise ImportError("store_results needs h5py (eval/ reads HDF5 result files)") from e
+    os.makedirs(Path(dst).parent, exist_ok=True)
+    with h5py.File(dst, "w") as f:
+        f.attrs["algo"] = algo
+        f.attrs["data"] = kind
+        f.attrs["buildtime"] = buildtime
+        f.attrs["querytime"] = querytime
+        f.attrs["size"] = size
+        f.attrs["params"] = params
+        f.create_dataset("knns", anns.shape, dtype=anns.dtype)[:] = anns
+        f.create_dataset("dists", dists.shape, dtype=dists.dtype)[:] = dists
