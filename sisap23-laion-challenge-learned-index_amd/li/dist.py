@@ -41,11 +41,12 @@ def init_from_env(backend: Optional[str] = None):
 def all_gather_lists(d: torch.Tensor, pos: torch.Tensor, group=None):
     """[nq, R, k] per rank -> [G, nq, R, k] on every rank."""
     G = dist.get_world_size(group)
-    gd = torch.empty((G,) + tuple(d.shape), dtype=d.dtype, device=d.device)
-    gp = torch.empty((G,) + tuple(pos.shape), dtype=pos.dtype, device=pos.device)
+    # concatenated along dim 0 (the form both RCCL and gloo accept), viewed [G, ...]
+    gd = torch.empty((G * d.shape[0],) + tuple(d.shape[1:]), dtype=d.dtype, device=d.device)
+    gp = torch.empty((G * pos.shape[0],) + tuple(pos.shape[1:]), dtype=pos.dtype, device=pos.device)
     dist.all_gather_into_tensor(gd, d.contiguous(), group=group)
     dist.all_gather_into_tensor(gp, pos.contiguous(), group=group)
-    return gd, gp
+    return gd.view((G,) + tuple(d.shape)), gp.view((G,) + tuple(pos.shape))
 
 
 def gather_merge(d: torch.Tensor, pos: torch.Tensor, k: int, group=None,

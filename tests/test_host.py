@@ -1,0 +1,90 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every symbol
+include/lmi_hip.h declares, argument validation, host helpers, bucket striping."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from li import _lib
+from li.index import BucketLayout
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    hdr = open(os.path.join(ROOT, "include", "lmi_hip.h")).read()
+    declared = set(re.findall(r"^\w[\w\s\*]*?\b(lmi_\w+)\(", hdr, flags=re.M))
+    assert declared == set(_lib.EXPORTS)
+    for name in declared:
+        assert getattr(lib, name) is not None
+    assert lib.lmi_abi_version() == 1
+
+
+def test_invalid_arguments_fail_loudly_without_a_device():
+    lib = _lib.load()
+    rc = lib.lmi_merge_topk(None, None, 0, 10, 10, None, None, None)
+    assert rc == _lib.LMI_E_INVALID
+    assert b"bad G" in lib.lmi_last_error()
+    rc = lib.lmi_merge_topk(None, None, 2, 10, 17, None, None, None)
+    assert rc == _lib.LMI_E_INVALID and b"k=17" in lib.lmi_last_error()
+    d = _lib.IndexDesc()
+    rc = lib.lmi_bucket_topk(C.byref(d), None, 4, 768, None, 2, 10, 0, None, None, None, None, 0, None)
+    assert rc == _lib.LMI_E_INVALID
+
+
+def test_plan_chunks():
+    lib = _lib.load()
+    off = np.array([0, 0, 5, 70, 70, 200], np.int64)
+    cf = np.zeros(6, np.int32)
+    mx = lib.lmi_plan_chunks(off.ctypes.data, 5, 32, cf.ctypes.data)
+    assert mx == 5  # bucket 4 has 130 rows -> 5 chunks of 32
+    assert cf.tolist() == [0, 0, 1, 4, 4, 9]
+    assert lib.lmi_plan_chunks(off.ctypes.data, 5, 33, cf.ctypes.data) < 0
+
+
+def test_workspace_size_is_monotone():
+    lib = _lib.load()
+    d = _lib.IndexDesc()
+    d.dtype, d.d, d.d_pad, d.n_rows, d.n_buckets = _lib.LMI_F16, 768, 768, 10**6, 122
+    d.chunk_rows, d.n_chunks, d.max_chunks = 8192, 200, 5
+    a = lib.lmi_scan_workspace_bytes(C.byref(d), 1000, 4, 10, _lib.LMI_Q_F16)
+    b = lib.lmi_scan_workspace_bytes(C.byref(d), 10000, 4, 10, _lib.LMI_Q_F16)
+    assert 0 < a < b
+
+
+def test_replay_rejects_the_reference_assert_case():
+    """k larger than the merged width: the reference asserts (LearnedIndex.py:99)."""
+    from li.index import replay
+    nq, R = 3, 2
+    cls = np.zeros((nq, R), np.int32)
+    d = np.zeros((nq, R, 10), np.float32)
+    p = np.zeros((nq, R, 10), np.int32)
+    with pytest.raises(_lib.LmiError):
+        replay(cls, d, p, k_round=10, k_final=25, bucket_size=np.array([20]),
+               pos_to_id=np.arange(1, 21), use_threshold=True)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_bucket_stripes_partition_every_bucket(world):
+    rng = np.random.default_rng(0)
+    lab = rng.integers(0, 7, 1000)
+    lab[lab == 3] = 4  # an empty bucket
+    L = BucketLayout.from_labels(lab, 7)
+    seen = []
+    for r in range(world):
+        gpos, loc = L.shard(r, world)
+        assert loc[-1] == gpos.size and np.all(np.diff(loc) >= 0)
+        for c in range(7):
+            part = gpos[loc[c]:loc[c + 1]]
+            assert np.all((part >= L.bucket_off[c]) & (part < L.bucket_off[c + 1]))
+            assert np.all(np.diff(part) == 1)  # contiguous slice, ascending
+        seen.append(gpos)
+    allp = np.sort(np.concatenate(seen))
+    assert np.array_equal(allp, np.arange(1000))
+    # stable in row order inside every bucket (groupby order, LearnedIndex.py:143-145)
+    for c in range(7):
+        rows = L.order[L.bucket_off[c]:L.bucket_off[c + 1]]
+        assert np.all(np.diff(rows) > 0) and np.all(lab[rows] == c)
