@@ -657,7 +657,9 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
                             const int reg = 4 * g + e;
                             const int i = e + 8 * g + 4 * h;
                             const float d = fmaf(-acc[reg], my_invq * inv4[e], 1.0f);
-                            dv[reg] = (i < valid_rows) ? d : __builtin_inff();
+                            // rows past the chunk end: NaN fails every compare
+                            // (+inf would pass `<= bound` while the list is empty)
+                            dv[reg] = (i < valid_rows) ? d : __builtin_nanf("");
                             anyp |= dv[reg] <= bound;
                         }
                     }
