@@ -52,23 +52,15 @@ def log(*a):
 
 def build_workload(args, device, rank, world):
     """Synthetic clip768/pca96 corpus + queries, a router fitted to k-means
-    buckets, object labels = router argmax (LearnedIndex.py:240)."""
-    n, d, C = SCALES[args.scale], 768, args.n_buckets
+    buckets, object labels = router argmax (LearnedIndex.py:240); deterministic."""
+    n, C = SCALES[args.scale], args.n_buckets
     t0 = time.time()
-    x, cen = synth.torch_mixture(n, d, args.centres, seed=2023, device=device)
-    q, _ = synth.torch_mixture(args.nq, d, args.centres, seed=4242, device=device, centres=cen,
-                               out_dtype=torch.float32)
-    g = torch.Generator(device=device)
-    g.manual_seed(96)
-    P = torch.randn((d, 96), generator=g, device=device) / math.sqrt(d)
-    xn = synth.torch_nav(x, P)
-    qn = synth.torch_nav(q, P)
-    sub = xn[torch.randperm(n, generator=g, device=device)[: min(n, 400_000)]]
-    cent = synth.kmeans(sub, C, iters=20, seed=7)
-    d2 = (sub * sub).sum(1, keepdim=True) - 2 * sub @ cent.T + (cent * cent).sum(1)[None]
-    model = synth.train_router(sub, d2.argmin(1), synth.ARCHS[args.arch], C, steps=args.train_steps)
-    router = DeviceRouter.from_module(model, device=device)
+    x, q, qn, xn, layers = synth.build_lmi_workload(n, args.nq, C, args.arch, device,
+                                                    centres=args.centres,
+                                                    train_steps=args.train_steps)
+    router = DeviceRouter(layers, device=device)
     labels = router.argmax(xn)
+    del xn
     torch.cuda.synchronize()
     log(f"[bench] workload n={n} built in {time.time() - t0:.1f}s")
     t0 = time.time()
@@ -78,7 +70,6 @@ def build_workload(args, device, rank, world):
     log(f"[bench] index (rank {rank}/{world}, {index.n_rows} rows, {index.storage}) "
         f"in {time.time() - t0:.1f}s; bucket sizes min/median/max = "
         f"{index.bucket_size.min()}/{int(np.median(index.bucket_size))}/{index.bucket_size.max()}")
-    del xn
     return x, q, qn, router, index, labels
 
 
@@ -164,7 +155,7 @@ def main():
     ap.add_argument("--n-buckets", type=int, default=122)
     ap.add_argument("--arch", default="MLP-5")
     ap.add_argument("--centres", type=int, default=400)
-    ap.add_argument("--train-steps", type=int, default=300)
+    ap.add_argument("--train-steps", type=int, default=200)
     ap.add_argument("--chunk-rows", type=int, default=8192)
     ap.add_argument("--recall-sample", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")

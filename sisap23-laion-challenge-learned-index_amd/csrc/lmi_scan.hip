@@ -486,7 +486,7 @@ constexpr int NQF = D / 16;            // B fragments per lane
 
 template <int KL>
 constexpr size_t lds_bytes() {
-    return (size_t)NSLOT * STAGE + (size_t)kWaves * kQCap * 64 * 8 + QB * (8 + 4) + 16;
+    return (size_t)NSLOT * STAGE + (size_t)kWaves * 64 * 16 * 8 + QB * (8 + 4) + 16;
 }
 }  // namespace v2
 
@@ -506,8 +506,6 @@ struct Scan2Args {
     uint64_t* partial;
     unsigned long long* thr_g;  // [P] per-pair bound, EMPTY at start
 };
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 __device__ inline void vm_wait(int n_stages_after) {
     // wait until at most n*GLDS of this wave's DMA are outstanding
@@ -541,13 +539,44 @@ __device__ __forceinline__ f32x16 mfma_drain(const f32x16& c) {
     return d;
 }
 
+typedef __attribute__((address_space(3))) void* lds_t;
+
+// Candidate filter of one accumulator register: d = 1 - dot/(|q||y|); rows
+// past the chunk end become NaN so every compare rejects them.
+__device__ __forceinline__ float cand_dist(float dot, float invq, float invy, int i, int valid_rows) {
+    const float d = fmaf(-dot, invq * invy, 1.0f);
+    return (i < valid_rows) ? d : __builtin_nanf("");
+}
+
+// Insert the block's surviving candidates into the lane's register list.
+// Branches are on wave-uniform ballots, one per accumulator register, so a
+// register nobody passes costs a compare and a scalar branch; a passing one
+// costs one unrolled list insertion for the lanes holding it.
 template <int KL>
+__device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bound,
+                                                 uint32_t row_base, int h, uint64_t (&L)[KL]) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const bool pass = dv[reg] <= bound;
+        if (__any(pass)) {
+            const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const uint64_t key = make_key(dv[reg], row_base + (uint32_t)i);
+            if (pass && key < L[KL - 1]) list_insert<KL>(L, key);
+        }
+    }
+}
+
+// ABL (diagnostic builds only, -DLMI_ABLATION): 1 = no top-k insertion,
+// 2 = no MFMA / LDS reads (DMA + barriers only), 3 = no DMA (compute on
+// whatever the ring holds).  Results are wrong for ABL != 0: timing only.
+template <int KL, int ABL = 0>
 __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
     using namespace v2;
+    constexpr int XCH = 32;  // blocks between global threshold exchanges
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
-    uint64_t* queue_all = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
-    uint64_t* thr_s = queue_all + kWaves * kQCap * 64;
+    uint64_t* merge_all = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
+    uint64_t* thr_s = merge_all + kWaves * 64 * 16;
     float* invq_s = reinterpret_cast<float*>(thr_s + QB);
     int& s_tile = *reinterpret_cast<int*>(invq_s + QB);
 
@@ -556,8 +585,18 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = lane >> 5;
     const int col = lane & 31;
-    uint64_t* queue = queue_all + wave * kQCap * 64 + lane;
     const int ntiles = *a.ntiles;
+
+    // per-lane constant DMA offsets: this wave stages rows 8w..8w+7 of every
+    // stage; lane writes LDS chunk `col` of row (8w + 2i + h) and reads the
+    // source chunk col ^ (row & 15) (XOR swizzle applied on the source side)
+    uint32_t voff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = 8 * wave + 2 * i + h;
+        voff[i] = (uint32_t)(row * (D * 2) + ((col ^ (row & 15)) << 4));
+    }
+    const uint32_t voff_n = (uint32_t)(col * 4);
 
     for (;;) {
         if (tid == 0) s_tile = atomicAdd(a.work, 1);
@@ -567,132 +606,153 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
         const Tile tile = a.tiles[t];
         const int64_t bstart = a.bucket_off[tile.c];
         const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
-        const int nrows = (int)std::min<int64_t>(a.chunk_rows, a.bucket_off[tile.c + 1] - row0);
+        const int nrows = __builtin_amdgcn_readfirstlane(
+            (int)std::min<int64_t>(a.chunk_rows, a.bucket_off[tile.c + 1] - row0));
+        const uint32_t r0lo = __builtin_amdgcn_readfirstlane((uint32_t)row0);
+        const uint32_t r0hi = __builtin_amdgcn_readfirstlane((uint32_t)(row0 >> 32));
+        const int64_t row0u = (int64_t)(((uint64_t)r0hi << 32) | r0lo);
         const int slot_q = 32 * wave + col;
         const bool live = slot_q < tile.np;
         const bool wave_live = 32 * wave < tile.np;
+        const int pp = tile.pp0 + slot_q;
 
-        // ---- this lane's query fragments (B operand), 1/||q||, bound ------
+        // ---- this lane's query fragments (B operand, AGPRs), 1/||q||, bound --
         half8 qf[NQF];
         {
-            const int q = live ? a.pair_q[tile.pp0 + slot_q] / a.R : 0;
+            const int q = live ? a.pair_q[pp] / a.R : 0;
             const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
 #pragma unroll
             for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
         }
         if (h == 0) {
-            invq_s[slot_q] = live ? a.invq[a.pair_q[tile.pp0 + slot_q] / a.R] : 0.0f;
-            thr_s[slot_q] = live ? (uint64_t)a.thr_g[tile.pp0 + slot_q] : 0ull;
+            invq_s[slot_q] = live ? a.invq[a.pair_q[pp] / a.R] : 0.0f;
+            thr_s[slot_q] = live ? (uint64_t)a.thr_g[pp] : 0ull;
         }
         uint64_t L[KL];
         list_clear<KL>(L);
         __syncthreads();
         const float my_invq = invq_s[slot_q];
+        uint64_t* thr_slot = &thr_s[slot_q];
 
-        // ---- DMA of one stage: this wave's 8 rows + its copy of the norms --
+        // buffer descriptors over this chunk (<= chunk_rows rows: far below the
+        // 4 GiB record limit); the range check zero-fills rows past the end
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.corpus + row0u * D), (short)0, nrows * D * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.inv_norm + row0u), (short)0, nrows * 4, 0x00020000);
+
         const int nblk = (nrows + 31) / 32;
         const int T = nblk * NST;
-        auto issue = [&](int st) {
+        // one DMA piece (i = 0..3: two rows x 512 B; i = 4: the 32 norms)
+        auto dma = [&](int st, int i) {
+            if (ABL == 3 || st >= T) return;
             const int blk = st / NST, j = st - blk * NST;
             unsigned char* sl = ring + (st % NSLOT) * STAGE;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int row = 8 * wave + 2 * i + h;
-                const int grow = std::min(blk * 32 + row, nrows - 1);
-                const int chunk = col ^ (row & 15);
-                const _Float16* src = a.corpus + (size_t)(row0 + grow) * D + j * KSEG + chunk * 8;
-                __builtin_amdgcn_global_load_lds((const void*)src,
-                                                 (lds_ptr_t)(sl + (8 * wave + 2 * i) * ROWB), 16, 0, 0);
-            }
-            const int nrow = std::min(blk * 32 + col, nrows - 1);
-            __builtin_amdgcn_global_load_lds((const void*)(a.inv_norm + row0 + nrow),
-                                             (lds_ptr_t)(sl + 32 * ROWB + wave * 256), 4, 0, 0);
+            if (i < 4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (lds_t)(sl + (8 * wave + 2 * i) * ROWB), 16, voff[i],
+                    blk * (32 * D * 2) + j * ROWB, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(sl + 32 * ROWB + wave * 256), 4,
+                                                         voff_n, blk * 128, 0, 0);
         };
 
         const int pro = std::min(T, NSLOT - 1);
-        for (int st = 0; st < pro; ++st) issue(st);
+        for (int st = 0; st < pro; ++st)
+            for (int i = 0; i < 5; ++i) dma(st, i);
 
-        f32x16 acc;
-        // one iteration = one 32-row block = NST stages, unrolled so the
-        // accumulator stays in one AGPR tuple through its 48 MFMAs
+        f32x16 acc, accp;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) accp[i] = 0.0f;
+        f32x4 nrmp[4] = {};
+        uint32_t rbp = 0;   // row base of the pending block
+        int vrp = 0;        // valid rows of the pending block (0: nothing pending)
+
         for (int blk = 0; blk < nblk; ++blk) {
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
                 const int s = blk * NST + j;
                 const int issued = std::min(T - 1, s + NSLOT - 2);
-                vm_wait(issued - std::min(s + 1, T - 1));
+                if (ABL != 3) vm_wait(issued - std::min(s + 1, T - 1));
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                if (s + NSLOT - 1 < T) issue(s + NSLOT - 1);
-                if (wave_live) {
-                    const unsigned char* rp = ring + (s % NSLOT) * STAGE + col * ROWB;
-                    // A fragment of step tt: row `col`, logical chunk 2tt+h (XOR-swizzled)
-#define LMI_A(tt) (*reinterpret_cast<const half8*>(rp + (((2 * (tt) + h) ^ (col & 15)) << 4)))
-                    if (j == 0) acc = mfma_first(LMI_A(0), qf[0]);
-                    else acc = mfma_acc(acc, LMI_A(0), qf[j * 16]);
-#pragma unroll
-                    for (int tt = 1; tt < 16; ++tt) acc = mfma_acc(acc, LMI_A(tt), qf[j * 16 + tt]);
-#undef LMI_A
+                const int nx = s + NSLOT - 1;  // stage whose DMA rides in this stage
+                if (ABL == 2 || !wave_live) {
+                    for (int i = 0; i < 5; ++i) dma(nx, i);
+                    continue;
                 }
-            }
-            if (wave_live) {
-                const int s = blk * NST + NST - 1;
-                const unsigned char* sl = ring + (s % NSLOT) * STAGE;
-                {
-                    acc = mfma_drain(acc);  // MFMA result -> VALU reader wait states
-                    // ---- top-k epilogue of the 32-row block ------------------
-                    const float* nrm = reinterpret_cast<const float*>(sl + 32 * ROWB + wave * 256);
-                    const int sub0 = blk * 32;
-                    const uint32_t row_base = (uint32_t)(row0 + sub0);
-                    const int valid_rows = nrows - sub0;
-                    uint64_t* thr_slot = &thr_s[slot_q];
-                    const uint64_t thr = *thr_slot;
-                    const float bound = key_dist_bound(thr);
+                const unsigned char* rp = ring + (s % NSLOT) * STAGE + col * ROWB;
+#define LMI_A(tt) (*reinterpret_cast<const half8*>(rp + (((2 * (tt) + h) ^ (col & 15)) << 4)))
+                half8 af[16];
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) af[tt] = LMI_A(tt);
+                if (j == 0) {
+                    // block start: the previous block's filter rides in the
+                    // shadow of this block's first 16 MFMAs, with the DMA
                     float dv[16];
                     bool anyp = false;
+                    const uint64_t thr = *thr_slot;
+                    const float bound = key_dist_bound(thr);
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const f32x4 inv4 = *reinterpret_cast<const f32x4*>(nrm + 8 * g + 4 * h);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const int reg = 4 * g + e;
-                            const int i = e + 8 * g + 4 * h;
-                            const float d = fmaf(-acc[reg], my_invq * inv4[e], 1.0f);
-                            // rows past the chunk end: NaN fails every compare
-                            // (+inf would pass `<= bound` while the list is empty)
-                            dv[reg] = (i < valid_rows) ? d : __builtin_nanf("");
-                            anyp |= dv[reg] <= bound;
-                        }
+                    for (int tt = 0; tt < 16; ++tt) {
+                        if (tt + 8 < 16) af[tt + 8] = LMI_A(tt + 8);
+                        acc = (tt == 0) ? mfma_first(af[0], qf[0]) : mfma_acc(acc, af[tt], qf[tt]);
+                        if (tt % 3 == 2) dma(nx, tt / 3);
+                        const int reg = tt;
+                        const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                        dv[reg] = cand_dist(accp[reg], my_invq, nrmp[reg >> 2][reg & 3], i, vrp);
+                        anyp |= dv[reg] <= bound;
                     }
-                    if (__any(anyp)) {
-                        int cnt = 0;
-#pragma unroll
-                        for (int reg = 0; reg < 16; ++reg) {
-                            const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-                            if (dv[reg] <= bound) {
-                                const uint64_t key = make_key(dv[reg], row_base + (uint32_t)i);
-                                if (key < thr) {
-                                    queue[cnt * 64] = key;
-                                    ++cnt;
-                                }
-                            }
-                        }
-                        for (int i = 0; __any(i < cnt); ++i) {
-                            if (i < cnt) {
-                                const uint64_t key = queue[i * 64];
-                                if (key < L[KL - 1]) list_insert<KL>(L, key);
-                            }
-                        }
+                    if (ABL != 1 && __any(anyp)) {
+                        insert_survivors<KL>(dv, bound, rbp, h, L);
                         if (L[KL - 1] < thr)
                             atomicMin(reinterpret_cast<unsigned long long*>(thr_slot),
                                       (unsigned long long)L[KL - 1]);
                     }
+                } else {
+#pragma unroll
+                    for (int tt = 0; tt < 16; ++tt) {
+                        if (tt + 8 < 16) af[tt + 8] = LMI_A(tt + 8);
+                        acc = mfma_acc(acc, af[tt], qf[j * 16 + tt]);
+                        if (tt % 3 == 2) dma(nx, tt / 3);
+                    }
                 }
+#undef LMI_A
             }
+            if (ABL != 2 && wave_live) {
+                // park this block: its accumulator, norms, row range
+                accp = mfma_drain(acc);
+                const int s = blk * NST + NST - 1;
+                const float* nrm = reinterpret_cast<const float*>(ring + (s % NSLOT) * STAGE +
+                                                                  32 * ROWB + wave * 256);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) nrmp[g] = *reinterpret_cast<const f32x4*>(nrm + 8 * g + 4 * h);
+                rbp = (uint32_t)(row0u + blk * 32);
+                vrp = nrows - blk * 32;
+            }
+            if (ABL == 0 && live && h == 0 && (blk % XCH) == XCH - 1) {
+                // share the query's bound with the concurrent tiles of the same
+                // pair (other chunks of its bucket): publish ours, adopt theirs
+                const unsigned long long mine = *thr_slot;
+                const unsigned long long g = atomicMin(&a.thr_g[pp], mine);
+                if (g < mine) atomicMin(reinterpret_cast<unsigned long long*>(thr_slot), g);
+            }
+        }
+        if (ABL == 0 && wave_live && vrp > 0) {
+            // the last block's epilogue (nothing left to hide it behind)
+            float dv[16];
+            const uint64_t thr = *thr_slot;
+            const float bound = key_dist_bound(thr);
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+                dv[reg] = cand_dist(accp[reg], my_invq, nrmp[reg >> 2][reg & 3], i, vrp);
+            }
+            insert_survivors<KL>(dv, bound, rbp, h, L);
         }
         __syncthreads();  // ring drained: every DMA was waited for above
 
         // ---- merge the two partial lists of each query (lanes col, col+32) ----
-        uint64_t* mb = queue_all + (size_t)wave * 64 * KL;
+        uint64_t* mb = merge_all + (size_t)wave * 64 * KL;
 #pragma unroll
         for (int i = 0; i < KL; ++i) mb[i * 64 + lane] = L[i];
         __syncthreads();
@@ -703,7 +763,6 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
                 if (key >= L[KL - 1]) break;
                 list_insert<KL>(L, key);
             }
-            const int pp = tile.pp0 + slot_q;
             uint64_t* out = a.partial + ((size_t)pp * a.max_chunks + tile.chunk) * KL;
 #pragma unroll
             for (int i = 0; i < KL; ++i) out[i] = L[i];
@@ -868,14 +927,14 @@ int launch_scan(const ScanArgs& a, int d_pad, hipStream_t s) {
     return LMI_OK;
 }
 
-template <int KL>
-int launch_scan2(const Scan2Args& b, hipStream_t s) {
+template <int KL, int ABL>
+int launch_scan2_v(const Scan2Args& b, hipStream_t s) {
     constexpr size_t lds = v2::lds_bytes<KL>();
     static_assert(lds <= 160 * 1024, "scan2 LDS budget");
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute((const void*)scan2_kernel<KL>,
+        attr_err = hipFuncSetAttribute((const void*)scan2_kernel<KL, ABL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     LMI_HIP_TRY(attr_err);
@@ -885,10 +944,22 @@ int launch_scan2(const Scan2Args& b, hipStream_t s) {
         const int rc = timing_record(s, true, ev);
         if (rc != LMI_OK) return rc;
     }
-    hipLaunchKernelGGL(scan2_kernel<KL>, dim3(num_cus()), dim3(kThreads), lds, s, b);
+    hipLaunchKernelGGL((scan2_kernel<KL, ABL>), dim3(num_cus()), dim3(kThreads), lds, s, b);
     LMI_LAUNCH_CHECK("scan2_kernel");
     if (timed) return timing_record(s, false, ev);
     return LMI_OK;
+}
+
+template <int KL>
+int launch_scan2(const Scan2Args& b, hipStream_t s) {
+#ifdef LMI_ABLATION
+    const char* e = getenv("LMI_SCAN_ABL");
+    const int abl = e ? atoi(e) : 0;
+    if (abl == 1) return launch_scan2_v<KL, 1>(b, s);
+    if (abl == 2) return launch_scan2_v<KL, 2>(b, s);
+    if (abl == 3) return launch_scan2_v<KL, 3>(b, s);
+#endif
+    return launch_scan2_v<KL, 0>(b, s);
 }
 
 }  // namespace

@@ -17,7 +17,7 @@ import threading
 
 import torch  # noqa: F401  (must precede the dlopen: one HIP runtime per process)
 
-LIB_NAME = "liblmi_hip.so"
+LIB_NAME = os.environ.get("LMI_LIB_NAME", "liblmi_hip.so")  # diagnostic builds only
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 LMI_OK = 0

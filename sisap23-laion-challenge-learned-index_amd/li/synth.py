@@ -132,3 +132,32 @@ def train_router(x_nav: torch.Tensor, labels: torch.Tensor, arch, n_classes: int
         loss.backward()
         opt.step()
     return model.eval()
+
+
+def build_lmi_workload(n: int, nq: int, n_buckets: int, arch: str, device, *, d: int = 768,
+                       centres: int = 400, train_steps: int = 200, seed: int = 2023):
+    """The benchmark workload, deterministic for a given seed.
+
+    Corpus + queries on `device` (torch_mixture), pca96 navigation vectors, a
+    router fitted on the CPU (k-means on a 100K subsample + short Adam fit of
+    the reference architecture: CPU so the fit is reproducible run to run),
+    object labels = router argmax on the GPU (LearnedIndex.py:240).
+    Returns (x f16 [n,d], q f32 [nq,d], qn f32 [nq,96], layers, labels int32 [n])."""
+    x, cen = torch_mixture(n, d, centres, seed=seed, device=device)
+    q, _ = torch_mixture(nq, d, centres, seed=seed + 2219, device=device, centres=cen,
+                         out_dtype=torch.float32)
+    g = torch.Generator(device="cpu")
+    g.manual_seed(96)
+    P = (torch.randn((d, 96), generator=g) / math.sqrt(d)).to(device)
+    xn = torch_nav(x, P)
+    qn = torch_nav(q, P)
+    sub_idx = torch.randperm(n, generator=g)[: min(n, 100_000)]
+    sub = xn[sub_idx.to(device)].cpu()
+    with torch.random.fork_rng(devices=[]):
+        cent = kmeans(sub, n_buckets, iters=20, seed=7)
+        d2 = (sub * sub).sum(1, keepdim=True) - 2 * sub @ cent.T + (cent * cent).sum(1)[None]
+        model = train_router(sub, d2.argmin(1), ARCHS[arch], n_buckets, steps=train_steps,
+                             batch=2048, seed=seed)
+    layers = [(m.weight.detach().cpu(), m.bias.detach().cpu())
+              for m in model if isinstance(m, torch.nn.Linear)]
+    return x, q, qn, xn, layers

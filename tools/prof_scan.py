@@ -1,0 +1,39 @@
+"""Scan-kernel timing harness: 10M workload, lmi_bucket_topk only, optional
+ablation variants (LMI_LIB_NAME=liblmi_hip_abl.so, LMI_SCAN_ABL=0..3)."""
+import argparse, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
+import numpy as np, torch
+from li import _lib, synth
+from li.index import DeviceIndex, DeviceRouter, bucket_topk
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--n", type=int, default=10_000_000)
+ap.add_argument("--nq", type=int, default=10_000)
+ap.add_argument("--R", type=int, default=4)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--chunk-rows", type=int, default=8192)
+ap.add_argument("--abl", default="0")
+a = ap.parse_args()
+dev = torch.device("cuda")
+x, q, qn, xn, layers = synth.build_lmi_workload(a.n, a.nq, 122, "MLP-5", dev)
+router = DeviceRouter(layers)
+labels = router.argmax(xn); del xn
+ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows)
+classes, _ = router.topr(qn, a.R)
+lib = _lib.load()
+for abl in a.abl.split(","):
+    os.environ["LMI_SCAN_ABL"] = abl
+    for _ in range(2):
+        bucket_topk(ix, q, classes, 10)
+    torch.cuda.synchronize()
+    lib.lmi_timing_read(None, 0)
+    lib.lmi_timing_enable(1)
+    for _ in range(a.reps):
+        bucket_topk(ix, q, classes, 10)
+    torch.cuda.synchronize()
+    lib.lmi_timing_enable(0)
+    ms = (_lib.C.c_float * a.reps)()
+    n = lib.lmi_timing_read(ms, a.reps)
+    v = sorted(list(ms)[:n])
+    print(f"abl={abl} scan ms: median {v[len(v)//2]:.3f} min {v[0]:.3f}", flush=True)
