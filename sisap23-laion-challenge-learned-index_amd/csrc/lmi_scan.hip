@@ -70,8 +70,8 @@ struct ScanArgs {
     const int32_t* pair_q;  // [P] pair id p = q*R + r, grouped by bucket
     int32_t R;
     const Tile* tiles;
-    const int32_t* ntiles;
-    int32_t* work;          // dequeue counter
+    const int32_t* meta;    // tile groups (plan_fill_kernel)
+    int32_t* work;          // dequeue counters
     uint64_t* partial;      // [P][max_chunks][KL]
 };
 
@@ -147,33 +147,77 @@ __global__ __launch_bounds__(kThreads) void plan_count_kernel(const int32_t* __r
     if (threadIdx.x == 0) counts[c] = n;
 }
 
+// Tile list layout (a permutation of all tiles):
+//   8 groups, group x = tiles whose global chunk index (chunk_first[c] + j)
+//   is = x mod 8; inside a group, every bucket's chunk-0 tiles first, then
+//   the other chunks, bucket-major, chunk-major, query-block-minor.
+// The persistent scan dequeues from group (blockIdx.x mod 8) — the blocks that
+// share an XCD under the observed round-robin placement — and steals from the
+// other groups when its own is empty; the query blocks of one chunk therefore
+// run back to back on one XCD and re-read the chunk from its L2.  Placement
+// only affects speed.  Chunk-0 tiles first: they publish each pair's k-th key
+// early, so later chunks start with a tight bound.
+//   meta[0..7] group offsets, meta[8..15] group sizes, meta[16] total
+//   work[0..7] group dequeue counters, work[8] the single counter of v1
+constexpr int kGroups = 8;
+
+__device__ inline int count_mod(int a, int n, int x, int ng) {
+    // #{t in [0, n) : (a + t) mod ng == x}, ng a power of two
+    if (n <= 0) return 0;
+    const int first = (x - a) & (ng - 1);
+    return n / ng + ((first < (n & (ng - 1))) ? 1 : 0);
+}
+
 __global__ __launch_bounds__(kThreads) void plan_fill_kernel(
     const int32_t* __restrict__ classes, int32_t P, int32_t C, const int32_t* __restrict__ counts,
     const int32_t* __restrict__ chunk_first, int32_t QB, int32_t* __restrict__ pair_q,
-    int32_t* __restrict__ pair_bucket, Tile* __restrict__ tiles, int32_t* __restrict__ ntiles,
-    int32_t* __restrict__ work) {
+    int32_t* __restrict__ pair_bucket, Tile* __restrict__ tiles, int32_t* __restrict__ meta,
+    int32_t* __restrict__ work, int32_t ng) {
     __shared__ int sh[kThreads / 64];
     __shared__ int wcnt[kThreads / 64];
+    __shared__ int g0_all[kGroups], gr_all[kGroups], g0_lt[kGroups], gr_lt[kGroups];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    auto tiles_of = [&](int b) {
+    if (tid < kGroups) g0_all[tid] = gr_all[tid] = g0_lt[tid] = gr_lt[tid] = 0;
+    __syncthreads();
+    int off = 0;
+    for (int b = tid; b < C; b += kThreads) {
         const int nch = chunk_first[b + 1] - chunk_first[b];
-        return nch * ((counts[b] + QB - 1) / QB);
-    };
-    int off = 0, toff = 0;
-    for (int b = tid; b < c; b += kThreads) {
-        off += counts[b];
-        toff += tiles_of(b);
+        const int nqb = nch > 0 ? (counts[b] + QB - 1) / QB : 0;
+        if (b < c) off += counts[b];
+        if (nqb == 0) continue;
+        const int cf = chunk_first[b];
+        atomicAdd(&g0_all[cf & (ng - 1)], nqb);
+        if (b < c) atomicAdd(&g0_lt[cf & (ng - 1)], nqb);
+        for (int x = 0; x < ng; ++x) {
+            const int r = nqb * count_mod(cf + 1, nch - 1, x, ng);
+            if (r) {
+                atomicAdd(&gr_all[x], r);
+                if (b < c) atomicAdd(&gr_lt[x], r);
+            }
+        }
     }
-    off = block_sum(off, sh);
-    toff = block_sum(toff, sh);
+    off = block_sum(off, sh);  // (contains the __syncthreads the atomics need)
+    int goff[kGroups];
+    {
+        int acc = 0;
+        for (int x = 0; x < kGroups; ++x) {
+            goff[x] = acc;
+            acc += g0_all[x] + gr_all[x];
+        }
+        if (c == C - 1 && tid == 0) {
+            for (int x = 0; x < kGroups; ++x) {
+                meta[x] = goff[x];
+                meta[kGroups + x] = g0_all[x] + gr_all[x];
+                work[x] = 0;
+            }
+            meta[2 * kGroups] = acc;
+            work[kGroups] = 0;
+        }
+    }
     const int cnt = counts[c];
     const int nch = chunk_first[c + 1] - chunk_first[c];
     const int nqb = (cnt + QB - 1) / QB;
-    if (c == C - 1 && tid == 0) {
-        *ntiles = toff + nch * nqb;
-        *work = 0;
-    }
     if (cnt == 0) return;
     // ordered fill of this bucket's pairs (ascending pair id = ascending q)
     const int lane = tid & 63, w = tid >> 6;
@@ -197,15 +241,36 @@ __global__ __launch_bounds__(kThreads) void plan_fill_kernel(
         }
         run += tot;
     }
+    const int cf = chunk_first[c];
     for (int i = tid; i < nch * nqb; i += kThreads) {
         const int j = i / nqb, b = i - j * nqb;
+        const int x = (cf + j) & (ng - 1);
         Tile t;
         t.c = c;
         t.pp0 = off + b * QB;
         t.np = min(QB, cnt - b * QB);
         t.chunk = j;
-        tiles[toff + i] = t;
+        int pos;
+        if (j == 0) {
+            pos = goff[x] + g0_lt[x] + b;
+        } else {
+            // chunks 1 .. j-1 of this bucket that fall in group x, before this one
+            pos = goff[x] + g0_all[x] + gr_lt[x] + nqb * count_mod(cf + 1, j - 1, x, ng) + b;
+        }
+        tiles[pos] = t;
     }
+}
+
+// The next tile for a workgroup of group `gx`: its own group first, then steal.
+__device__ inline int dequeue_tile(const int32_t* meta, int32_t* work, int gx, int ng) {
+    for (int k = 0; k < ng; ++k) {
+        const int g = (gx + k) & (ng - 1);
+        const int sz = meta[kGroups + g];
+        if (__hip_atomic_load(&work[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= sz) continue;
+        const int v = atomicAdd(&work[g], 1);
+        if (v < sz) return meta[g] + v;
+    }
+    return -1;
 }
 
 // ---------------------------------------------------------------------------
@@ -295,10 +360,10 @@ __global__ __launch_bounds__(kThreads, 1) void scan_kernel(ScanArgs a) {
 
     const TC* __restrict__ corpus = reinterpret_cast<const TC*>(a.corpus);
     const QT* __restrict__ qbuf = reinterpret_cast<const QT*>(a.qbuf);
-    const int ntiles = *a.ntiles;
+    const int ntiles = a.meta[2 * kGroups];
 
     for (;;) {
-        if (tid == 0) s_tile = atomicAdd(a.work, 1);
+        if (tid == 0) s_tile = atomicAdd(&a.work[kGroups], 1);
         __syncthreads();
         const int t = s_tile;
         if (t >= ntiles) break;
@@ -486,7 +551,7 @@ constexpr int NQF = D / 16;            // B fragments per lane
 
 template <int KL>
 constexpr size_t lds_bytes() {
-    return (size_t)NSLOT * STAGE + (size_t)kWaves * 64 * 16 * 8 + QB * (8 + 4) + 16;
+    return (size_t)NSLOT * STAGE + (size_t)kWaves * 64 * 16 * 8 + 16;
 }
 }  // namespace v2
 
@@ -501,20 +566,29 @@ struct Scan2Args {
     const int32_t* pair_q;
     int32_t R;
     const Tile* tiles;
-    const int32_t* ntiles;
+    const int32_t* meta;
     int32_t* work;
     uint64_t* partial;
     unsigned long long* thr_g;  // [P] per-pair bound, EMPTY at start
+    int32_t ng;                 // tile groups (power of two <= kGroups)
+    int32_t lag;                // extra ring stages waited for (tuning knob, 0)
 };
 
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
+// expcnt [6:4], lgkmcnt [11:8]); other counters left at their maximum.
+// The builtin (not inline asm) keeps hipcc's wait-count scoreboard in sync,
+// so it does not add its own conservative vmcnt waits later in the loop.
+constexpr int waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
 __device__ inline void vm_wait(int n_stages_after) {
-    // wait until at most n*GLDS of this wave's DMA are outstanding
+    // wait until at most 5 * n of this wave's DMA pieces are outstanding
     switch (n_stages_after) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+        case 0: __builtin_amdgcn_s_waitcnt(waitcnt_vm(0)); break;
+        case 1: __builtin_amdgcn_s_waitcnt(waitcnt_vm(5)); break;
+        case 2: __builtin_amdgcn_s_waitcnt(waitcnt_vm(10)); break;
+        case 3: __builtin_amdgcn_s_waitcnt(waitcnt_vm(15)); break;
+        case 4: __builtin_amdgcn_s_waitcnt(waitcnt_vm(20)); break;
+        default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(25)); break;
     }
 }
 
@@ -548,20 +622,56 @@ __device__ __forceinline__ float cand_dist(float dot, float invq, float invy, in
     return (i < valid_rows) ? d : __builtin_nanf("");
 }
 
-// Insert the block's surviving candidates into the lane's register list.
-// Branches are on wave-uniform ballots, one per accumulator register, so a
-// register nobody passes costs a compare and a scalar branch; a passing one
-// costs one unrolled list insertion for the lanes holding it.
+// The same value from the partner lane (lane ^ 32): both halves of a 32x32
+// accumulator column hold one query.  v_permlane32_swap is a VALU op, so no
+// LDS write happens inside the DMA ring (hipcc would drain the LDS-DMA with a
+// vmcnt(0) before any LDS write it cannot prove disjoint from the ring).
+__device__ __forceinline__ uint32_t partner_u32(uint32_t x, int h) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return h ? r[0] : r[1];
+}
+__device__ __forceinline__ uint64_t partner_u64(uint64_t x, int h) {
+    const uint32_t lo = partner_u32((uint32_t)x, h);
+    const uint32_t hi = partner_u32((uint32_t)(x >> 32), h);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Survivors of a block: appended to the lane's private LDS queue, then
+// inserted into the lane's register list in lockstep (iterations = the
+// largest per-lane count, not one per register).  The queue accesses are
+// inline asm on purpose: hipcc drains every in-flight LDS-DMA (vmcnt(0))
+// before an LDS write it cannot prove disjoint from the DMA targets, which
+// would empty the ring; the queue never aliases the ring.  The same wave's
+// LDS operations complete in order, and each read carries its own wait.
+__device__ __forceinline__ void lds_put_u64(uint32_t addr, uint64_t v) {
+    asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint64_t lds_get_u64(uint32_t addr) {
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+}
+
 template <int KL>
-__device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bound,
-                                                 uint32_t row_base, int h, uint64_t (&L)[KL]) {
+__device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bound, uint64_t thr,
+                                                 uint32_t row_base, int h, uint32_t qaddr,
+                                                 uint64_t (&L)[KL]) {
+    int cnt = 0;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-        const bool pass = dv[reg] <= bound;
-        if (__any(pass)) {
+        if (dv[reg] <= bound) {
             const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
             const uint64_t key = make_key(dv[reg], row_base + (uint32_t)i);
-            if (pass && key < L[KL - 1]) list_insert<KL>(L, key);
+            if (key < thr) {
+                lds_put_u64(qaddr + cnt * 512, key);
+                ++cnt;
+            }
+        }
+    }
+    for (int i = 0; __any(i < cnt); ++i) {
+        if (i < cnt) {
+            const uint64_t key = lds_get_u64(qaddr + i * 512);
+            if (key < L[KL - 1]) list_insert<KL>(L, key);
         }
     }
 }
@@ -572,20 +682,20 @@ __device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bo
 template <int KL, int ABL = 0>
 __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
     using namespace v2;
-    constexpr int XCH = 32;  // blocks between global threshold exchanges
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
+    // [wave][16][64] u64: the candidate queues, and after the ring loop the
+    // buffer of the end-of-tile list merge
     uint64_t* merge_all = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
-    uint64_t* thr_s = merge_all + kWaves * 64 * 16;
-    float* invq_s = reinterpret_cast<float*>(thr_s + QB);
-    int& s_tile = *reinterpret_cast<int*>(invq_s + QB);
+    int& s_tile = *reinterpret_cast<int*>(merge_all + kWaves * 64 * 16);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int h = lane >> 5;
     const int col = lane & 31;
-    const int ntiles = *a.ntiles;
+    const int ng = a.ng;
+    const int gx = blockIdx.x & (ng - 1);
 
     // per-lane constant DMA offsets: this wave stages rows 8w..8w+7 of every
     // stage; lane writes LDS chunk `col` of row (8w + 2i + h) and reads the
@@ -597,12 +707,14 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
         voff[i] = (uint32_t)(row * (D * 2) + ((col ^ (row & 15)) << 4));
     }
     const uint32_t voff_n = (uint32_t)(col * 4);
+    // this lane's queue: entry e at qaddr + e * 512 (64 lanes x 8 B per entry)
+    const uint32_t qaddr = (uint32_t)(uintptr_t)(merge_all + wave * 64 * 16 + lane);
 
     for (;;) {
-        if (tid == 0) s_tile = atomicAdd(a.work, 1);
+        if (tid == 0) s_tile = dequeue_tile(a.meta, a.work, gx, ng);
         __syncthreads();
         const int t = s_tile;
-        if (t >= ntiles) break;
+        if (t < 0) break;
         const Tile tile = a.tiles[t];
         const int64_t bstart = a.bucket_off[tile.c];
         const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
@@ -624,15 +736,15 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
 #pragma unroll
             for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
         }
-        if (h == 0) {
-            invq_s[slot_q] = live ? a.invq[a.pair_q[pp] / a.R] : 0.0f;
-            thr_s[slot_q] = live ? (uint64_t)a.thr_g[pp] : 0ull;
-        }
+        // the query's bound: min over the k-th keys of its partial lists and of
+        // the other chunks' tiles of the same pair; dead slots reject all
+        uint64_t thr = live ? (uint64_t)a.thr_g[pp] : 0ull;
+        const float my_invq = live ? a.invq[a.pair_q[pp] / a.R] : 0.0f;
         uint64_t L[KL];
         list_clear<KL>(L);
+        // retire the fragment loads where hipcc can see it (see waitcnt_vm)
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         __syncthreads();
-        const float my_invq = invq_s[slot_q];
-        uint64_t* thr_slot = &thr_s[slot_q];
 
         // buffer descriptors over this chunk (<= chunk_rows rows: far below the
         // 4 GiB record limit); the range check zero-fills rows past the end
@@ -672,8 +784,9 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
                 const int s = blk * NST + j;
+                // stage s must have landed; stages s+1 .. s+5 stay in flight
                 const int issued = std::min(T - 1, s + NSLOT - 2);
-                if (ABL != 3) vm_wait(issued - std::min(s + 1, T - 1));
+                if (ABL != 3) vm_wait(issued - std::min(s + a.lag, issued));
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
                 const int nx = s + NSLOT - 1;  // stage whose DMA rides in this stage
                 if (ABL == 2 || !wave_live) {
@@ -690,7 +803,6 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
                     // shadow of this block's first 16 MFMAs, with the DMA
                     float dv[16];
                     bool anyp = false;
-                    const uint64_t thr = *thr_slot;
                     const float bound = key_dist_bound(thr);
 #pragma unroll
                     for (int tt = 0; tt < 16; ++tt) {
@@ -703,10 +815,10 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
                         anyp |= dv[reg] <= bound;
                     }
                     if (ABL != 1 && __any(anyp)) {
-                        insert_survivors<KL>(dv, bound, rbp, h, L);
-                        if (L[KL - 1] < thr)
-                            atomicMin(reinterpret_cast<unsigned long long*>(thr_slot),
-                                      (unsigned long long)L[KL - 1]);
+                        insert_survivors<KL>(dv, bound, thr, rbp, h, qaddr, L);
+                        const uint64_t kth = L[KL - 1];
+                        const uint64_t pk = partner_u64(kth, h);
+                        thr = std::min(thr, std::min(kth, pk));
                     }
                 } else {
 #pragma unroll
@@ -720,7 +832,10 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
             }
             if (ABL != 2 && wave_live) {
                 // park this block: its accumulator, norms, row range
-                accp = mfma_drain(acc);
+                // wait states on the MFMA's own registers first: a copy taken
+                // before them would read the accumulator mid-write
+                acc = mfma_drain(acc);
+                accp = acc;
                 const int s = blk * NST + NST - 1;
                 const float* nrm = reinterpret_cast<const float*>(ring + (s % NSLOT) * STAGE +
                                                                   32 * ROWB + wave * 256);
@@ -729,25 +844,17 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
                 rbp = (uint32_t)(row0u + blk * 32);
                 vrp = nrows - blk * 32;
             }
-            if (ABL == 0 && live && h == 0 && (blk % XCH) == XCH - 1) {
-                // share the query's bound with the concurrent tiles of the same
-                // pair (other chunks of its bucket): publish ours, adopt theirs
-                const unsigned long long mine = *thr_slot;
-                const unsigned long long g = atomicMin(&a.thr_g[pp], mine);
-                if (g < mine) atomicMin(reinterpret_cast<unsigned long long*>(thr_slot), g);
-            }
         }
         if (ABL == 0 && wave_live && vrp > 0) {
             // the last block's epilogue (nothing left to hide it behind)
             float dv[16];
-            const uint64_t thr = *thr_slot;
             const float bound = key_dist_bound(thr);
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
                 const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
                 dv[reg] = cand_dist(accp[reg], my_invq, nrmp[reg >> 2][reg & 3], i, vrp);
             }
-            insert_survivors<KL>(dv, bound, rbp, h, L);
+            insert_survivors<KL>(dv, bound, thr, rbp, h, qaddr, L);
         }
         __syncthreads();  // ring drained: every DMA was waited for above
 
@@ -850,8 +957,8 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     const size_t mt = (P / QB + 1) * (size_t)std::max(idx->max_chunks, 1) + (size_t)idx->n_chunks;
     w.max_tiles = (int32_t)std::min<size_t>(mt, (size_t)INT32_MAX);
     w.tiles = take((size_t)w.max_tiles * sizeof(Tile));
-    w.ntiles = take(4);
-    w.work = take(4);
+    w.ntiles = take(4 * (2 * kGroups + 1));
+    w.work = take(4 * (kGroups + 1));
     w.partial = take(P * (size_t)std::max(idx->max_chunks, 1) * KL * sizeof(uint64_t));
     w.thr_g = take(P * sizeof(uint64_t));
     w.total = off;
@@ -995,6 +1102,15 @@ extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq
     return lmi::ws_layout(idx, nq, R, k, qmode).total;
 }
 
+namespace {
+// tuning knobs (defaults are the tuned values; results do not depend on them)
+int env_int(const char* name, int dflt, int lo, int hi) {
+    const char* v = getenv(name);
+    if (!v || !*v) return dflt;
+    return std::max(lo, std::min(hi, atoi(v)));
+}
+}  // namespace
+
 extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                                const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
                                float* out_d, int32_t* out_pos, int32_t* status, void* workspace,
@@ -1043,16 +1159,18 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     int32_t* pair_q = (int32_t*)(ws + w.pair_q);
     int32_t* pair_bucket = (int32_t*)(ws + w.pair_bucket);
     Tile* tiles = (Tile*)(ws + w.tiles);
-    int32_t* ntiles = (int32_t*)(ws + w.ntiles);
+    int32_t* meta = (int32_t*)(ws + w.ntiles);
     int32_t* work = (int32_t*)(ws + w.work);
     const int C = idx->n_buckets;
+    int ng = env_int("LMI_SCAN_GROUPS", kGroups, 1, kGroups);
+    while (ng & (ng - 1)) ng &= ng - 1;
 
     // pair_bucket = -1 marks pairs whose class is out of range (never filled)
     LMI_HIP_TRY(hipMemsetAsync(pair_bucket, 0xff, (size_t)P * 4, s));
     hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kThreads), 0, s, classes, P, counts);
     LMI_LAUNCH_CHECK("plan_count_kernel");
     hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kThreads), 0, s, classes, P, C, counts,
-                       idx->chunk_first, QB, pair_q, pair_bucket, tiles, ntiles, work);
+                       idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
 
     ScanArgs a{};
@@ -1067,7 +1185,7 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     a.pair_q = pair_q;
     a.R = R;
     a.tiles = tiles;
-    a.ntiles = ntiles;
+    a.meta = meta;
     a.work = work;
     a.partial = (uint64_t*)(ws + w.partial);
 
@@ -1084,10 +1202,12 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
         b.pair_q = pair_q;
         b.R = R;
         b.tiles = tiles;
-        b.ntiles = ntiles;
+        b.meta = meta;
         b.work = work;
         b.partial = a.partial;
         b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
+        b.ng = ng;
+        b.lag = env_int("LMI_SCAN_LAG", 0, 0, 3);
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
         rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
     } else if (f16math) {

@@ -14,6 +14,8 @@ ap.add_argument("--R", type=int, default=4)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--chunk-rows", type=int, default=8192)
 ap.add_argument("--abl", default="0")
+ap.add_argument("--variants", default="",
+                help="'|'-separated env settings, e.g. 'LMI_SCAN_GROUPS=1,LMI_SCAN_LAG=1|LMI_SCAN_GROUPS=8'")
 a = ap.parse_args()
 dev = torch.device("cuda")
 x, q, qn, xn, layers = synth.build_lmi_workload(a.n, a.nq, 122, "MLP-5", dev)
@@ -22,8 +24,14 @@ labels = router.argmax(xn); del xn
 ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows)
 classes, _ = router.topr(qn, a.R)
 lib = _lib.load()
-for abl in a.abl.split(","):
+runs = [(abl, "") for abl in a.abl.split(",")]
+if a.variants:
+    runs = [(abl, v) for v in a.variants.split("|") for abl in a.abl.split(",")]
+for abl, var in runs:
     os.environ["LMI_SCAN_ABL"] = abl
+    for kv in filter(None, var.split(",")):
+        kk, vv = kv.split("=")
+        os.environ[kk] = vv
     for _ in range(2):
         bucket_topk(ix, q, classes, 10)
     torch.cuda.synchronize()
@@ -36,4 +44,4 @@ for abl in a.abl.split(","):
     ms = (_lib.C.c_float * a.reps)()
     n = lib.lmi_timing_read(ms, a.reps)
     v = sorted(list(ms)[:n])
-    print(f"abl={abl} scan ms: median {v[len(v)//2]:.3f} min {v[0]:.3f}", flush=True)
+    print(f"[{var}] abl={abl} scan ms: median {v[len(v)//2]:.3f} min {v[0]:.3f}", flush=True)
