@@ -23,7 +23,10 @@
 // (utils.py:35-42, `U \ B_q`) is unspecified in the reference (introsort
 // over ties); here they are taken in ascending position.  They can reach the
 // output only when k_final > k_round.
+#include <omp.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdint>
 #include <cstring>
@@ -144,15 +147,21 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
     int wF = 0;
     std::vector<int> order(nq), start(n_buckets + 1);
     std::vector<double> thr(nq);
-    std::vector<Entry> tmp, cat;
+    // Rounds are sequential; inside a round, queries (threshold, merge,
+    // output) and bucket groups (each writes only its own queries' D_r rows)
+    // are independent and split over OpenMP threads.  Results do not depend
+    // on the thread count.
+    std::atomic<int> err{0};
+    std::vector<int> fillp(n_buckets);
 
     for (int r = 0; r < R; ++r) {
         const bool thresholded = ((r > 0) && use_threshold) || (r == 0 && thr_round0);
-        for (auto& e : Dr) e = Entry{kFill, -1};
-        if (r == 0 && thr_round0) {
-            for (int q = 0; q < nq; ++q) thr[q] = thr_round0[q];
-        } else if (thresholded) {
-            for (int q = 0; q < nq; ++q) {
+#pragma omp parallel for schedule(static)
+        for (int q = 0; q < nq; ++q) {
+            for (int j = 0; j < kr; ++j) Dr[(size_t)q * kr + j] = Entry{kFill, -1};
+            if (r == 0 && thr_round0) {
+                thr[q] = thr_round0[q];
+            } else if (thresholded) {
                 double m = F[(size_t)q * fs].d;
                 for (int j = 1; j < wF; ++j) m = std::max(m, F[(size_t)q * fs + j].d);
                 thr[q] = m;
@@ -165,19 +174,19 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
             if (c >= 0 && c < n_buckets) ++start[c + 1];
         }
         for (int c = 0; c < n_buckets; ++c) start[c + 1] += start[c];
-        {
-            std::vector<int> fillp(start.begin(), start.end() - 1);
-            for (int q = 0; q < nq; ++q) {
-                const int c = classes[(size_t)q * R + r];
-                if (c >= 0 && c < n_buckets) order[fillp[c]++] = q;
-            }
+        std::copy(start.begin(), start.end() - 1, fillp.begin());
+        for (int q = 0; q < nq; ++q) {
+            const int c = classes[(size_t)q * R + r];
+            if (c >= 0 && c < n_buckets) order[fillp[c]++] = q;
         }
         auto list_at = [&](int q, int j, double& d, int64_t& pos) {
             const size_t o = ((size_t)q * R + r) * k_list + j;
             pos = lists_pos[o];
             d = (double)lists_d[o];
         };
+#pragma omp parallel for schedule(dynamic, 1)
         for (int c = 0; c < n_buckets; ++c) {
+            std::vector<Entry> tmp;
             const int g0 = start[c], g1 = start[c + 1];
             if (g0 == g1 || bucket_size[c] <= 0) continue;  // groupby visits non-empty categories only
             if (thresholded) {
@@ -201,20 +210,20 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
                         const int q = order[gi];
                         Entry* out = &Dr[(size_t)q * kr];
                         int n = 0;
-                        std::vector<int64_t> mine;
                         for (int j = 0; j < kl_use && n < kr; ++j) {
                             double d;
                             int64_t pos;
                             list_at(q, j, d, pos);
                             if (pos < 0 || !(d < thr[q])) break;
                             out[n++] = Entry{d, pos};
-                            mine.push_back(pos);
                         }
                         // fillers: objects of U not relevant to q, distance 10000
-                        std::sort(mine.begin(), mine.end());
+                        // (the first n entries of `out` are q's relevant ones)
+                        const int n_rel = n;
                         for (size_t u = 0; u < U.size() && n < kr; ++u) {
-                            if (!std::binary_search(mine.begin(), mine.end(), U[u]))
-                                out[n++] = Entry{kFill, U[u]};
+                            bool mine = false;
+                            for (int j = 0; j < n_rel; ++j) mine |= (out[j].pos == U[u]);
+                            if (!mine) out[n++] = Entry{kFill, U[u]};
                         }
                     }
                 } else {
@@ -258,9 +267,8 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
                         objs.emplace_back(pos, d);
                     }
                     if ((int64_t)objs.size() != n) {
-                        set_error("lmi_replay: list of bucket %d holds %zu of %lld objects", c,
-                                  objs.size(), (long long)n);
-                        return LMI_E_INVALID;
+                        err.store(c + 1);  // reported after the loop
+                        continue;
                     }
                     std::sort(objs.begin(), objs.end());
                     std::vector<double> row;
@@ -284,17 +292,38 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
             wF = kr;
         } else {
             const int wn = std::min(k_final, wF + kr);
-            cat.resize(wF + kr);
-            for (int q = 0; q < nq; ++q) {
-                for (int j = 0; j < wF; ++j) cat[j] = F[(size_t)q * fs + j];
-                for (int j = 0; j < kr; ++j) cat[wF + j] = Dr[(size_t)q * kr + j];
-                std::stable_sort(cat.begin(), cat.end(),
-                                 [](const Entry& a, const Entry& b) { return a.d < b.d; });
-                for (int j = 0; j < wn; ++j) F[(size_t)q * fs + j] = cat[j];
+#pragma omp parallel
+            {
+                std::vector<Entry> cat(wF + kr);
+#pragma omp for schedule(static)
+                for (int q = 0; q < nq; ++q) {
+                    // stable sort of hstack(F, D_r) by distance (argsort(kind='stable')):
+                    // insertion sort, strict > so equal distances keep hstack order.
+                    // (F need not be sorted: quirk rows of round 0 are not.)
+                    int len = 0;
+                    for (int j = 0; j < wF + kr; ++j) {
+                        const Entry e = j < wF ? F[(size_t)q * fs + j] : Dr[(size_t)q * kr + (j - wF)];
+                        int i = len++;
+                        while (i > 0 && cat[i - 1].d > e.d) {
+                            cat[i] = cat[i - 1];
+                            --i;
+                        }
+                        cat[i] = e;
+                    }
+                    for (int j = 0; j < wn; ++j) F[(size_t)q * fs + j] = cat[j];
+                }
             }
             wF = wn;
         }
+        if (err.load()) {
+            const int c = err.load() - 1;
+            set_error("lmi_replay: the list of bucket %d does not hold all its %lld objects", c,
+                      (long long)bucket_size[c]);
+            return LMI_E_INVALID;
+        }
     }
+    std::atomic<int64_t> bad{-1};
+#pragma omp parallel for schedule(static)
     for (int q = 0; q < nq; ++q) {
         for (int j = 0; j < w; ++j) {
             const Entry& e = F[(size_t)q * fs + j];
@@ -302,13 +331,17 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
             int64_t id = 0;
             if (e.pos >= 0) {
                 if (e.pos >= n_total) {
-                    set_error("lmi_replay: position %lld out of range", (long long)e.pos);
-                    return LMI_E_INVALID;
+                    bad.store(e.pos);
+                    continue;
                 }
                 id = pos_to_id[e.pos];
             }
             anns_out[(size_t)q * w + j] = (uint32_t)id;  // numpy int64 -> uint32 assignment
         }
+    }
+    if (bad.load() >= 0) {
+        set_error("lmi_replay: position %lld out of range", (long long)bad.load());
+        return LMI_E_INVALID;
     }
     return LMI_OK;
 }
