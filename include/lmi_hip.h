@@ -42,6 +42,8 @@ extern "C" {
 
 /* bits of the device status word written by lmi_bucket_topk */
 #define LMI_STATUS_QUERY_NOT_F16 1 /* qmode=LMI_Q_F16 but a query is not fp16-exact */
+#define LMI_STATUS_INTERNAL 2      /* a list entry held an out-of-range row (a scan bug): the
+                                      entry was dropped instead of read out of bounds */
 
 /* ---- element types / modes ------------------------------------------ */
 #define LMI_F32 0

@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <utility>
+#include <type_traits>
 #include <vector>
 
 namespace lmi {
@@ -678,7 +679,9 @@ __device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bo
 
 // ABL (diagnostic builds only, -DLMI_ABLATION): 1 = no top-k insertion,
 // 2 = no MFMA / LDS reads (DMA + barriers only), 3 = no DMA (compute on
-// whatever the ring holds).  Results are wrong for ABL != 0: timing only.
+// whatever the ring holds); scan v3 also: 4 = no DMA, no insertion, 5 = no
+// DMA, no epilogue, 6 = 5 without the per-stage barrier.  Results are wrong
+// for ABL != 0: timing only.
 template <int KL, int ABL = 0>
 __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
     using namespace v2;
@@ -880,6 +883,419 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// scan v3 (fp16 corpus, fp16-exact queries, d_pad == 768, k <= 10): the v2
+// ring with 8 waves = two per SIMD.
+//
+//   per wave : 32 queries, B fragments (K = 768) in AGPRs for the whole tile;
+//              the wave serves query group `slot` of the tile, slots being a
+//              SIMD-balanced numbering (groups 0-3 land on four different
+//              SIMDs, whatever the wave -> SIMD placement)
+//   per tile : one chunk of one bucket x up to 256 pairs: every staged
+//              object byte serves 256 queries (v2: 128), halving the
+//              L2 -> LDS traffic, and the two waves of a SIMD hide each
+//              other's filter / insertion VALU behind their MFMAs
+//   ring     : 7 slots of 32 rows x 256 k (16 pieces of two interleaved rows,
+//              see v3::PIECEP) + the block's 32 norms in the slot of its
+//              last stage; DMA 6 stages (2 blocks) ahead; each wave stages
+//              two 1-KiB pieces per stage and its 4 norms once per block;
+//              one s_barrier per stage; slot offsets and DMA offsets are
+//              running values and the steady-state waits immediates (the
+//              scalar unit is shared by the CU's 8 waves)
+//   lists    : each lane's partial top-k list lives in LDS (registers are
+//              taken by the query fragments); the filter bound stays in
+//              registers, so the list is touched only on insertion
+//   epilogue : per 32-row block, right after its last MFMA: a 16-bit
+//              candidate mask from d = 1 - dot/(|q||y|) <= bound, and only
+//              if some lane has a candidate, a per-register ballot-gated
+//              insertion that recomputes d from the accumulator
+// ---------------------------------------------------------------------------
+namespace v3 {
+constexpr int D = 768;
+constexpr int ROWB = 512;              // bytes of one row in one stage (256 k)
+// LDS image of a stage: 16 pieces of two rows each (one 1-KiB DMA), the two
+// rows interleaved at 16-B granularity (row 2p+x, chunk c at 32c + 16x of
+// piece p), pieces at a 1056-B pitch.  Row r chunk c then sits at
+// (r>>1)*1056 + 32c + 16(r&1): affine in c, so a lane's A-fragment reads
+// share one base register + immediate offsets, and the 32-row reads are
+// bank-conflict free (bank start 4r + 8h mod 64).
+constexpr int PIECEP = 2 * ROWB + 32;  // piece pitch
+constexpr int NST = D * 2 / ROWB;      // stages per 32-row block
+constexpr int NORM_OFF = 16 * PIECEP;  // the block's 32 norms (last stage's slot)
+constexpr int STAGE = NORM_OFF + 128;
+constexpr int NSLOT = 7;
+constexpr int LOOK = NSLOT - 1;        // the DMA runs this many stages ahead
+constexpr int NW = 8;
+constexpr int QB = NW * 32;
+constexpr int NQF = D / 16;
+constexpr int KL = 10;
+constexpr size_t lds_bytes = (size_t)NSLOT * STAGE + (size_t)NW * KL * 64 * 8 + 64;
+static_assert(lds_bytes <= 160 * 1024, "LDS budget");
+
+// DMA instructions a wave issues for stages 0..s: two pieces per stage, plus
+// its 4 norms in the last stage of each block
+__host__ __device__ constexpr int pieces_through(int s, bool norms) {
+    return s < 0 ? 0 : 2 * (s + 1) + (norms ? (s + 1) / NST : 0);
+}
+// DMA instructions issued after those of a phase-j stage s once stages up to
+// s + LOOK - 1 are issued (the steady state): the wait immediate of stage s
+constexpr int steady_after(int j) {
+    return pieces_through(j + LOOK - 1, true) - pieces_through(j, true);
+}
+static_assert(NST == 3, "the stage loop spells out three phases");
+}  // namespace v3
+
+
+// VGPR-form MFMAs for scan v3: a kernel that uses no AGPR gets the whole
+// 256-register budget of a two-waves-per-SIMD launch as VGPRs (with AGPRs in
+// use, the compiler splits it 128/128, too few for 192 query registers).
+__device__ __forceinline__ f32x16 mfma_first_v(const half8& a, const half8& b) {
+    f32x16 d;
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ f32x16 mfma_acc_v(const f32x16& c, const half8& a, const half8& b) {
+    f32x16 d = c;
+    asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ f32x16 mfma_drain_v(const f32x16& c) {
+    f32x16 d = c;
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(d));
+    return d;
+}
+
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+#define LMI_VMW(k) \
+    case k: __builtin_amdgcn_s_waitcnt(waitcnt_vm(k)); break;
+    switch (n) {
+        LMI_VMW(1) LMI_VMW(2) LMI_VMW(3) LMI_VMW(4) LMI_VMW(5) LMI_VMW(6) LMI_VMW(7) LMI_VMW(8) LMI_VMW(9) LMI_VMW(10) LMI_VMW(11) LMI_VMW(12) LMI_VMW(13) LMI_VMW(14) LMI_VMW(15) LMI_VMW(16) LMI_VMW(17) LMI_VMW(18) LMI_VMW(19) LMI_VMW(20) LMI_VMW(21) LMI_VMW(22) LMI_VMW(23) LMI_VMW(24) LMI_VMW(25) LMI_VMW(26) LMI_VMW(27) LMI_VMW(28) LMI_VMW(29) LMI_VMW(30) LMI_VMW(31) LMI_VMW(32) LMI_VMW(33) LMI_VMW(34) LMI_VMW(35) LMI_VMW(36) LMI_VMW(37) LMI_VMW(38) LMI_VMW(39) LMI_VMW(40)
+        default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(0)); break;
+    }
+#undef LMI_VMW
+}
+
+// LDS list entries at a base VGPR + immediate offset (one address register
+// for a whole list; plain-C++ addressing would hoist one register per entry)
+template <int OFF>
+__device__ __forceinline__ void lds_put_u64_at(uint32_t addr, uint64_t v) {
+    asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ uint64_t lds_get_u64_at(uint32_t addr) {
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+    return v;
+}
+template <int KL, int OFF = 0>
+__device__ __forceinline__ void list_store(uint32_t addr, const uint64_t (&L)[KL]) {
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+        (lds_put_u64_at<OFF + I * 512>(addr, L[I]), ...);
+    }(std::make_integer_sequence<int, KL>{});
+}
+template <int KL, int OFF = 0>
+__device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
+    static_assert(KL == 10, "one asm block of 10 reads");
+    // all reads in flight, one wait (a wait per read would serialise ~10 LDS
+    // round trips); one asm statement so no use can slip before the wait
+    asm volatile(
+        "ds_read_b64 %0, %10 offset:%11\n\t"
+        "ds_read_b64 %1, %10 offset:%12\n\t"
+        "ds_read_b64 %2, %10 offset:%13\n\t"
+        "ds_read_b64 %3, %10 offset:%14\n\t"
+        "ds_read_b64 %4, %10 offset:%15\n\t"
+        "ds_read_b64 %5, %10 offset:%16\n\t"
+        "ds_read_b64 %6, %10 offset:%17\n\t"
+        "ds_read_b64 %7, %10 offset:%18\n\t"
+        "ds_read_b64 %8, %10 offset:%19\n\t"
+        "ds_read_b64 %9, %10 offset:%20\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
+          "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9])
+        : "v"(addr), "i"(OFF), "i"(OFF + 512), "i"(OFF + 1024), "i"(OFF + 1536), "i"(OFF + 2048),
+          "i"(OFF + 2560), "i"(OFF + 3072), "i"(OFF + 3584), "i"(OFF + 4096), "i"(OFF + 4608)
+        : "memory");
+}
+
+// In-place odd-even transposition sort of a short list (ascending keys).
+template <int KL>
+__device__ __forceinline__ void list_sort(uint64_t (&L)[KL]) {
+#pragma unroll
+    for (int r = 0; r < KL; ++r) {
+#pragma unroll
+        for (int i = r & 1; i + 1 < KL; i += 2) {
+            const uint64_t x = L[i], y = L[i + 1];
+            L[i] = x < y ? x : y;
+            L[i + 1] = x < y ? y : x;
+        }
+    }
+}
+
+extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
+
+// Keeps the compiler from hoisting lane-dependent address arithmetic out of
+// the tile loop (each hoisted value would pin a VGPR for the whole kernel).
+__device__ __forceinline__ int opaque(int x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
+template <int ABL = 0>
+__global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
+    using namespace v3;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* ring = smem;
+    // [wave][KL][64 lanes] u64: every lane's partial top-k list (lane-private
+    // column; registers are all spoken for by the query fragments)
+    uint64_t* lists = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
+    int* wtab = reinterpret_cast<int*>(lists + NW * KL * 64);  // [NW] SIMD ids, [NW] tile
+    int& s_tile = wtab[NW];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ng = a.ng;
+
+    // SIMD-balanced slot of this wave: order waves by (rank on their SIMD, SIMD)
+    int simd, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID, 4, 2)" : "=s"(simd));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    if (lane == 0) wtab[wave] = simd;
+    __syncthreads();
+    int slot = 0;
+    {
+        int key_me = simd;
+        for (int w = 0; w < wave; ++w) key_me += (wtab[w] == simd) ? 4 : 0;  // + rank * 4
+        for (int w = 0; w < NW; ++w) {
+            int kw = wtab[w];
+            for (int v = 0; v < w; ++v) kw += (wtab[v] == wtab[w]) ? 4 : 0;
+            slot += (kw < key_me || (kw == key_me && w < wave)) ? 1 : 0;
+        }
+        slot = __builtin_amdgcn_readfirstlane(slot);
+    }
+    const int gx = xcc & (ng - 1);
+    // this lane's list column: entry i at lbase + i * 512
+    const uint32_t lbase = (uint32_t)(uintptr_t)(lists + wave * KL * 64 + lane);
+
+    for (;;) {
+        if (tid == 0) s_tile = dequeue_tile(a.meta, a.work, gx, ng);
+        __syncthreads();
+        const int t = __builtin_amdgcn_readfirstlane(s_tile);
+        if (t < 0) break;
+        const Tile tile = a.tiles[t];
+        const int64_t bstart = a.bucket_off[tile.c];
+        const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
+        const int nrows = __builtin_amdgcn_readfirstlane(
+            (int)std::min<int64_t>(a.chunk_rows, a.bucket_off[tile.c + 1] - row0));
+        const uint32_t r0lo = __builtin_amdgcn_readfirstlane((uint32_t)row0);
+        const uint32_t r0hi = __builtin_amdgcn_readfirstlane((uint32_t)(row0 >> 32));
+        const int64_t row0u = (int64_t)(((uint64_t)r0hi << 32) | r0lo);
+        const int np = __builtin_amdgcn_readfirstlane(tile.np);
+        const bool wave_live = 32 * slot < np;
+        const int h = opaque(lane) >> 5;
+        const int col = lane & 31;
+        const bool live = 32 * slot + col < np;
+        const int pp = tile.pp0 + 32 * slot + col;
+
+        half8 qf[NQF];
+        uint64_t thr = 0ull;
+        float my_invq = 0.0f;
+        int cnt = 0;  // entries in this lane's list; < KL: an unsorted append buffer
+        if (wave_live) {
+            const int q = live ? a.pair_q[pp] / a.R : 0;
+            const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
+#pragma unroll
+            for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
+            thr = live ? (uint64_t)a.thr_g[pp] : 0ull;  // dead slots reject everything
+            my_invq = live ? a.invq[q] : 0.0f;
+        }
+        {
+            uint64_t E[KL];
+            list_clear<KL>(E);
+            list_store<KL>(opaque_u(lbase), E);
+        }
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+        __syncthreads();
+
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.corpus + row0u * D), (short)0, nrows * D * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.inv_norm + row0u), (short)0, nrows * 4, 0x00020000);
+
+        const int nblk = (nrows + 31) / 32;
+        const int T = nblk * NST;
+        // DMA of one stage (block b, phase j) into the LDS slot at byte offset
+        // `so`: pieces 0, 1 = rows 4w+2i, 4w+2i+1 (lane l: row 4w + 2i + (l&1),
+        // chunk l >> 1; piece 1 is piece 0 + 2 rows through soffset); in the
+        // block's last phase the wave's 4 norms too.
+        // Every wave issues the same count, so the waits below are immediates.
+        const uint32_t vo_row = (uint32_t)((4 * wave + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
+        auto dma_stage = [&](int so, int b, int j) {
+            if (ABL == 3 || ABL >= 4) return;
+            unsigned char* sl = ring + so;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
+                                                     b * (32 * D * 2) + j * ROWB, 0, 0);
+            // (+2 rows through soffset: an instruction offset would move the
+            // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave + 1) * PIECEP), 16,
+                                                     vo_row, b * (32 * D * 2) + j * ROWB + 2 * D * 2,
+                                                     0, 0);
+            if (j == NST - 1 && lane < 4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(sl + NORM_OFF + 16 * wave), 4,
+                                                         (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
+        };
+        // prologue: stages 0 .. LOOK-1 (blocks 0 and 1) into slots 0 .. LOOK-1
+        static_assert(LOOK % NST == 0, "the DMA runs whole blocks ahead");
+        constexpr int AHEAD = LOOK / NST;
+        for (int b = 0; b < std::min(nblk, AHEAD); ++b)
+#pragma unroll
+            for (int j = 0; j < NST; ++j) dma_stage((b * NST + j) * STAGE, b, j);
+        // a lane's A-fragment base inside a slot (row col = lane & 31, half h)
+        const uint32_t lane_off = (uint32_t)(((lane >> 1) & 15) * PIECEP + (lane & 1) * 16 + (lane >> 5) * 32);
+
+        int so = 0;                    // slot of the stage being read
+        int pso = (NSLOT - 1) * STAGE;  // slot of the previous stage = target of this stage's DMA
+        f32x16 acc;
+        for (int blk = 0; blk < nblk; ++blk) {
+            const bool steady = blk + AHEAD < nblk;  // stages s+1 .. s+LOOK-1 all issued
+            int nso = 0;                             // slot holding this block's norms
+#pragma unroll
+            for (int j = 0; j < NST; ++j) {
+                const int s = blk * NST + j;
+                // stage s must have landed: the DMAs issued after it are those of
+                // stages s+1 .. min(T-1, s+LOOK-1), 2 pieces each + 1 in phase 2
+                if (ABL != 3 && ABL < 4) {
+                    if (steady) {
+                        if (j == 0)
+                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(0)));
+                        else if (j == 1)
+                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(1)));
+                        else
+                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(2)));
+                    } else {
+                        vm_wait_dyn(v3::pieces_through(T - 1, true) - v3::pieces_through(s, true));
+                    }
+                }
+                if (ABL != 6) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                const int wso = pso;  // this stage's DMA (stage s + LOOK) goes to stage s-1's slot
+                if (ABL == 2 || !wave_live) {
+                    if (steady) dma_stage(wso, blk + AHEAD, j);
+                } else {
+                    const unsigned char* rp = ring + so + opaque_u(lane_off);
+#define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
+                    half8 af[16];
+#pragma unroll
+                    for (int tt = 0; tt < 3; ++tt) af[tt] = LMI_A3(tt);
+#pragma unroll
+                    for (int tt = 0; tt < 16; ++tt) {
+                        if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
+                        acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
+                                                  : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
+                        if (tt == 4 && steady) dma_stage(wso, blk + AHEAD, j);
+                        // keep the A-fragment reads 3 MFMAs ahead, no further
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#undef LMI_A3
+                }
+                if (j == NST - 1) nso = so;
+                pso = so;
+                so = (so + STAGE == NSLOT * STAGE) ? 0 : so + STAGE;
+            }
+            if (ABL == 2 || ABL >= 5 || !wave_live) continue;
+            // ---- epilogue of this block ----------------------------------------
+            acc = mfma_drain_v(acc);
+            const int ln = opaque(lane);
+            const int hh = ln >> 5;
+            const unsigned char* nb = ring + nso + NORM_OFF + hh * 16;
+            const int vr = nrows - blk * 32 - 4 * hh;  // valid rows past this lane's offset
+            const float bound = key_dist_bound(thr);
+            uint32_t mask = 0;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const f32x4 n4 = *reinterpret_cast<const f32x4*>(nb + 32 * g);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int reg = 4 * g + e;
+                    const float d = fmaf(-acc[reg], my_invq * n4[e], 1.0f);
+                    mask |= (e + 8 * g < vr && d <= bound) ? (1u << reg) : 0u;
+                }
+            }
+            if (ABL != 1 && ABL != 4 && __any(mask != 0)) {
+                const uint32_t la = opaque_u(lbase);
+                const uint32_t rb = (uint32_t)(row0u + blk * 32 + 4 * hh);
+                // registers with a candidate in some lane (wave-uniform bit set),
+                // one at a time with a uniform register index (v_movrels): no
+                // per-register code copies, few live registers
+                uint32_t wm = __builtin_amdgcn_readfirstlane(__ockl_wfred_or_u32(mask));
+#pragma unroll 1
+                for (; wm != 0; wm &= wm - 1) {
+                    const int rg = __builtin_ctz(wm);
+                    if ((mask >> rg) & 1u) {
+                        const int i = (rg & 3) + 8 * (rg >> 2);
+                        const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
+                        const float d = fmaf(-acc[rg], my_invq * n1, 1.0f);
+                        const uint64_t key = make_key(d, rb + (uint32_t)i);
+                        if (key < thr) {
+                            if (cnt < KL) {
+                                // append mode: the first KL candidates below the
+                                // tile's starting bound are stored unsorted (the
+                                // common case once a seed bound exists: a few
+                                // instructions instead of a sorted insertion)
+                                lds_put_u64(la + (uint32_t)cnt * 512u, key);
+                                if (++cnt == KL) {  // full: sort once, switch to list mode
+                                    uint64_t L[KL];
+                                    list_load<KL>(la, L);
+                                    list_sort<KL>(L);
+                                    list_store<KL>(la, L);
+                                    thr = std::min(thr, L[KL - 1]);
+                                }
+                            } else {
+                                uint64_t L[KL];
+                                list_load<KL>(la, L);
+                                list_insert<KL>(L, key);
+                                list_store<KL>(la, L);
+                                thr = std::min(thr, L[KL - 1]);
+                            }
+                        }
+                    }
+                }
+                // every bound is an upper bound of the pair's k-th key: share it
+                thr = std::min(thr, partner_u64(thr, hh));
+            }
+        }
+        // lanes still in append mode hold an unsorted (EMPTY-padded) buffer
+        if (__any(cnt < KL)) {
+            if (cnt < KL) {
+                uint64_t L[KL];
+                list_load<KL>(lbase, L);
+                list_sort<KL>(L);
+                list_store<KL>(lbase, L);
+            }
+        }
+        __syncthreads();  // every wave's DMA drained (the tail waited vmcnt(0))
+
+        // ---- merge the two partial lists of each query (lanes col, col+32) ----
+        if (h == 0 && live) {
+            uint64_t L[KL], P[KL];
+            list_load<KL>(lbase, L);
+            list_load<KL, 32 * 8>(lbase, P);
+#pragma unroll
+            for (int i = 0; i < KL; ++i) {
+                if (P[i] >= L[KL - 1]) break;
+                list_insert<KL>(L, P[i]);
+            }
+            uint64_t* out = a.partial + ((size_t)pp * a.max_chunks + tile.chunk) * KL;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) out[i] = L[i];
+            if (L[KL - 1] != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)L[KL - 1]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // chunk merge
 // ---------------------------------------------------------------------------
 template <int KL>
@@ -887,7 +1303,8 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ counts_total_src,
     const int32_t* __restrict__ chunk_first, const int32_t* __restrict__ gpos, int32_t P, int32_t k,
-    float* __restrict__ out_d, int32_t* __restrict__ out_pos) {
+    float* __restrict__ out_d, int32_t* __restrict__ out_pos, int64_t n_rows,
+    int32_t* __restrict__ status) {
     const int pp = blockIdx.x * kThreads + threadIdx.x;
     if (pp >= P) return;
     const int c = pair_bucket[pp];
@@ -909,8 +1326,11 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
         if (i < k) {
             const uint64_t key = M[i];
             const bool empty = key == kEmptyKey;
-            out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
-            out_pos[o + i] = empty ? -1 : gpos[(uint32_t)key];
+            const uint32_t lp = (uint32_t)key;
+            const bool bad = !empty && lp >= (uint32_t)n_rows;  // never for a sound scan
+            if (bad) atomicOr(status, LMI_STATUS_INTERNAL);
+            out_d[o + i] = (empty || bad) ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
+            out_pos[o + i] = (empty || bad) ? -1 : gpos[lp];
         }
     }
     (void)counts_total_src;
@@ -924,6 +1344,7 @@ struct WsLayout {
     int32_t max_tiles;
     int32_t qb;      // queries per tile
     bool use_v2;     // scan2_kernel
+    bool use_v3;     // scan3_kernel
 };
 
 bool v2_eligible(const lmi_index_desc* idx, int qmode) {
@@ -933,12 +1354,18 @@ bool v2_eligible(const lmi_index_desc* idx, int qmode) {
 
 int pick_kl(int k) { return k <= 10 ? 10 : 16; }
 
+bool v3_eligible(const lmi_index_desc* idx, int qmode, int k) {
+    if (getenv("LMI_SCAN_V2")) return false;  // diagnostic switch: force the 4-wave ring
+    return v2_eligible(idx, qmode) && pick_kl(k) == v3::KL;
+}
+
 WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     WsLayout w{};
     const int KL = pick_kl(k);
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
-    w.use_v2 = v2_eligible(idx, qmode);
-    const int QB = w.use_v2 ? v2::QB : (f16math ? 64 : 32);
+    w.use_v3 = v3_eligible(idx, qmode, k);
+    w.use_v2 = !w.use_v3 && v2_eligible(idx, qmode);
+    const int QB = w.use_v3 ? v3::QB : w.use_v2 ? v2::QB : (f16math ? 64 : 32);
     w.qb = QB;
     const size_t P = (size_t)nq * R;
     const size_t esz = f16math ? 2 : 4;
@@ -1055,6 +1482,42 @@ int launch_scan2_v(const Scan2Args& b, hipStream_t s) {
     LMI_LAUNCH_CHECK("scan2_kernel");
     if (timed) return timing_record(s, false, ev);
     return LMI_OK;
+}
+
+template <int ABL>
+int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
+    constexpr size_t lds = v3::lds_bytes;
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<ABL>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    LMI_HIP_TRY(attr_err);
+    const bool timed = timing().on;
+    std::pair<hipEvent_t, hipEvent_t> ev{};
+    if (timed) {
+        const int rc = timing_record(s, true, ev);
+        if (rc != LMI_OK) return rc;
+    }
+    hipLaunchKernelGGL((scan3_kernel<ABL>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
+    LMI_LAUNCH_CHECK("scan3_kernel");
+    if (timed) return timing_record(s, false, ev);
+    return LMI_OK;
+}
+
+int launch_scan3(const Scan2Args& b, hipStream_t s) {
+#ifdef LMI_ABLATION
+    const char* e = getenv("LMI_SCAN_ABL");
+    const int abl = e ? atoi(e) : 0;
+    if (abl == 1) return launch_scan3_v<1>(b, s);
+    if (abl == 2) return launch_scan3_v<2>(b, s);
+    if (abl == 3) return launch_scan3_v<3>(b, s);
+    if (abl == 4) return launch_scan3_v<4>(b, s);
+    if (abl == 5) return launch_scan3_v<5>(b, s);
+    if (abl == 6) return launch_scan3_v<6>(b, s);
+#endif
+    return launch_scan3_v<0>(b, s);
 }
 
 template <int KL>
@@ -1190,7 +1653,7 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     a.partial = (uint64_t*)(ws + w.partial);
 
     int rc;
-    if (w.use_v2) {
+    if (w.use_v2 || w.use_v3) {
         Scan2Args b{};
         b.corpus = reinterpret_cast<const _Float16*>(idx->corpus);
         b.inv_norm = idx->inv_norm;
@@ -1209,7 +1672,10 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
         b.ng = ng;
         b.lag = env_int("LMI_SCAN_LAG", 0, 0, 3);
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
-        rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
+        if (w.use_v3)
+            rc = launch_scan3(b, s);
+        else
+            rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
     } else if (f16math) {
         rc = (KL == 10) ? launch_scan<10, true, _Float16>(a, idx->d_pad, s)
                         : launch_scan<16, true, _Float16>(a, idx->d_pad, s);
@@ -1226,11 +1692,11 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     if (KL == 10) {
         hipLaunchKernelGGL(chunk_merge_kernel<10>, dim3(grid), dim3(kThreads), 0, s, a.partial,
                            a.max_chunks, pair_q, pair_bucket, nullptr, idx->chunk_first, idx->gpos, P,
-                           k, out_d, out_pos);
+                           k, out_d, out_pos, idx->n_rows, status);
     } else {
         hipLaunchKernelGGL(chunk_merge_kernel<16>, dim3(grid), dim3(kThreads), 0, s, a.partial,
                            a.max_chunks, pair_q, pair_bucket, nullptr, idx->chunk_first, idx->gpos, P,
-                           k, out_d, out_pos);
+                           k, out_d, out_pos, idx->n_rows, status);
     }
     LMI_LAUNCH_CHECK("chunk_merge_kernel");
     return LMI_OK;

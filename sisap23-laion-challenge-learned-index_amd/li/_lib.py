@@ -26,6 +26,7 @@ LMI_E_UNSUPPORTED = 1002
 LMI_E_WORKSPACE = 1003
 LMI_E_HIP = 1004
 LMI_STATUS_QUERY_NOT_F16 = 1
+LMI_STATUS_INTERNAL = 2
 
 LMI_F32 = 0
 LMI_F16 = 1

@@ -409,6 +409,8 @@ class Searcher:
             t1 = time.perf_counter()
             timings["d2h"] = timings.get("d2h", 0.0) + (t1 - t0) * 1e3
             t0 = t1
+        if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL:
+            raise RuntimeError("lmi_bucket_topk: a list held an out-of-range row (internal error)")
         if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
             # queries are not fp16-exact: redo the scan with exact fp32 MFMA
             d, pos, _ = bucket_topk(self.index, q_search, classes, k_list, qmode=_lib.LMI_Q_F32)

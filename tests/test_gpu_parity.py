@@ -99,3 +99,23 @@ def test_full_search_matches_direct_oracle(use_threshold, R):
                                    use_threshold=use_threshold)
     assert dists.shape == ref_d.shape and anns.dtype == np.uint32
     assert O.compare_lists(ref_d, ref_a, dists, anns) == 0
+
+
+@pytest.mark.parametrize("label_mode", ["router", "dup"])
+def test_scan_tiles_of_many_pairs_match_oracle_and_4wave_ring(label_mode, monkeypatch):
+    """Buckets probed by > 256 pairs (several 8-wave tiles per chunk), exact
+    duplicate vectors (tied distances): the 8-wave scan equals the oracle and,
+    bitwise, the 4-wave ring (same MFMA accumulation order)."""
+    w = workloads.clustered(n=20000, nq=1500, C=8, seed=13, label_mode=label_mode)
+    R, k = 2, 10
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    ix = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=2048)
+    q = torch.from_numpy(w["q"]).cuda()
+    ct = torch.from_numpy(classes.astype(np.int32)).cuda()
+    d3, p3, st = bucket_topk(ix, q, ct, k)
+    assert int(st.item()) == 0
+    monkeypatch.setenv("LMI_SCAN_V2", "1")
+    d2, p2, _ = bucket_topk(ix, q, ct, k)
+    assert torch.equal(d3, d2) and torch.equal(p3, p2)
+    ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, w["C"])
+    assert O.compare_lists(ref_d, ref_p, d3.cpu().numpy(), p3.cpu().numpy()) == 0
