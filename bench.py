@@ -103,44 +103,56 @@ def algorithmic_bytes(index, classes, nq):
     return byts, flops, rows
 
 
-def cpu_baseline(index, q, qn_classes, args, budget_s=15.0):
-    """Oracle port (oracle/lmi_oracle.py) on a bounded query sample of the same
-    workload: per-(query, probe) lists by the reference's per-group
-    normalize + GEMM (utils.py:10-11) and the replay (LearnedIndex.py:22-195)."""
+def cpu_baseline(index, q, classes, args, budget_s=15.0):
+    """The oracle port (oracle/lmi_oracle.py) on a bounded sample of the same
+    batch, shaped like the reference's own loop (LearnedIndex.py:143-172):
+    whole (round, bucket) groups, each one sklearn-normalize + fp32 GEMM of the
+    group's queries against the whole bucket (utils.py:10-11) and a full-row
+    argsort.  Groups are taken in batch order until `budget_s` is spent; the
+    rate is (query, probe) pairs / R per second, i.e. queries/s."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import lmi_oracle as O
     off = index.layout.bucket_off
-    corpus = index.corpus
     qh = q.cpu().numpy()
-    R, k = args.R, args.k
+    R = args.R
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    t0 = time.time()
-    done = 0
-    cache = {}
-    while done < min(args.nq, 512) and (time.time() - t0 < budget_s or done < 4):
-        qq = done
-        lists_d = np.full((1, R, k), np.inf, np.float32)
-        lists_p = np.full((1, R, k), -1, np.int32)
-        for r in range(R):
-            c = int(qn_classes[qq, r])
-            a, b = int(off[c]), int(off[c + 1])
-            if a == b:
-                continue
-            if c not in cache:
-                if len(cache) > 16:
-                    cache.pop(next(iter(cache)))
-                cache[c] = corpus[a:b, : index.d].float().cpu().numpy()
-            D = O.pairwise_cosine(qh[qq:qq + 1], cache[c])[0]
-            pos = np.arange(a, b)
-            o = np.lexsort((pos, D))[:k]
-            lists_d[0, r, : o.size] = D[o]
-            lists_p[0, r, : o.size] = pos[o]
-        done += 1
-    t = time.time() - t0
-    return {"value": round(done / t, 3), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{done} of the {args.nq} queries of the same {args.scale} workload, R={R}, "
-                      f"k={k}: per-probe 1-cos (sklearn normalize + fp32 GEMM) and top-k "
-                      f"in numpy, {threads} BLAS threads"}
+    groups = [(r, int(c)) for r in range(R) for c in np.unique(classes[:, r])]
+    pairs = rows = ngroups = 0
+    el = 0.0
+    for r, c in groups:
+        a, b = int(off[c]), int(off[c + 1])
+        G = np.nonzero(classes[:, r] == c)[0]
+        if a == b or G.size == 0:
+            continue
+        y = index.corpus[a:b, : index.d].float().cpu().numpy()  # bucket rows (HBM -> host, untimed)
+        t1 = time.time()
+        D = O.pairwise_cosine(qh[G], y)
+        np.argsort(D, axis=1, kind="quicksort")[:, : args.k]
+        el += time.time() - t1
+        ngroups += 1
+        pairs += G.size
+        rows += b - a
+        if el > budget_s:
+            break
+    return {"value": round(pairs / R / el, 3), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"{ngroups} of the {len(groups)} (round, bucket) groups of the same {args.scale} "
+                      f"batch ({pairs} (query, probe) pairs over {rows} bucket rows, R={R}, k={args.k}): "
+                      f"per group sklearn-normalize + fp32 GEMM + full-row argsort as "
+                      f"LearnedIndex.py:143-172; rate = pairs / R / s; {threads} BLAS threads"}
+
+
+def pmc_traffic(kernel_ms):
+    """HBM-side bytes per scan launch from the committed rocprofv3 PMC passes
+    (tools/gpu_profile.sh -> profiles/*pmc_traffic.json): FETCH_SIZE x 2 (gfx950
+    reports half of wide streaming reads, MI355X_MICROARCH.md HBM section) +
+    WRITE_SIZE, in bytes; None when no summary is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    byts = (2.0 * d["FETCH_SIZE"]["mean_kb"] + d["WRITE_SIZE"]["mean_kb"]) * 1024.0
+    return byts, os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -212,9 +224,12 @@ def main():
             torch.distributed.barrier()
         return
     achieved = byts / (scan_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(scan_ms)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "scan_kernel (lmi_bucket_topk)", "kernel_ms": round(scan_ms, 4),
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None if traffic is None else int(traffic),
+            "traffic_source": traffic_src,
+            "kernel": "scan3_kernel (lmi_bucket_topk)", "kernel_ms": round(scan_ms, 4),
             "algorithmic_bytes": int(byts), "flops": flops,
             "mfma_tflops": round(flops / (scan_ms * 1e-3) / 1e12, 1),
             "mfma_frac": round(flops / (scan_ms * 1e-3) / 1e12 / F16_PEAK_TFLOPS, 4)}

@@ -1031,6 +1031,14 @@ __device__ __forceinline__ void list_sort(uint64_t (&L)[KL]) {
 }
 
 extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
+
+#ifdef LMI_ABLATION
+// ABL == 7 (diagnostic build): the full kernel plus event counters
+// [0] blocks with a candidate in some lane (wave events), [1] candidates,
+// [2] appends, [3] sorted insertions, [4] buffer fills (sorts), [5] blocks
+__device__ unsigned long long lmi_dbg[8];
+#endif
 
 // Keeps the compiler from hoisting lane-dependent address arithmetic out of
 // the tile loop (each hoisted value would pin a VGPR for the whole kernel).
@@ -1046,6 +1054,9 @@ __device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
 template <int ABL = 0>
 __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
+    constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6;
+    constexpr bool kNoEpi = ABL == 2 || ABL == 5 || ABL == 6;
+    constexpr bool kNoIns = ABL == 1 || ABL == 4;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
     // [wave][KL][64 lanes] u64: every lane's partial top-k list (lane-private
@@ -1134,7 +1145,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         // Every wave issues the same count, so the waits below are immediates.
         const uint32_t vo_row = (uint32_t)((4 * wave + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
         auto dma_stage = [&](int so, int b, int j) {
-            if (ABL == 3 || ABL >= 4) return;
+            if (kNoDma) return;
             unsigned char* sl = ring + so;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
                                                      b * (32 * D * 2) + j * ROWB, 0, 0);
@@ -1167,7 +1178,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 const int s = blk * NST + j;
                 // stage s must have landed: the DMAs issued after it are those of
                 // stages s+1 .. min(T-1, s+LOOK-1), 2 pieces each + 1 in phase 2
-                if (ABL != 3 && ABL < 4) {
+                if (!kNoDma) {
                     if (steady) {
                         if (j == 0)
                             __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(0)));
@@ -1204,7 +1215,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 pso = so;
                 so = (so + STAGE == NSLOT * STAGE) ? 0 : so + STAGE;
             }
-            if (ABL == 2 || ABL >= 5 || !wave_live) continue;
+            if (kNoEpi || !wave_live) continue;
             // ---- epilogue of this block ----------------------------------------
             acc = mfma_drain_v(acc);
             const int ln = opaque(lane);
@@ -1223,7 +1234,17 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                     mask |= (e + 8 * g < vr && d <= bound) ? (1u << reg) : 0u;
                 }
             }
-            if (ABL != 1 && ABL != 4 && __any(mask != 0)) {
+#ifdef LMI_ABLATION
+            if (ABL == 7) {
+                const uint32_t nc = __ockl_wfred_add_u32(__builtin_popcount(mask));
+                if (lane == 0) {
+                    atomicAdd(&lmi_dbg[5], 1ull);
+                    if (nc) atomicAdd(&lmi_dbg[0], 1ull);
+                    atomicAdd(&lmi_dbg[1], (unsigned long long)nc);
+                }
+            }
+#endif
+            if (!kNoIns && __any(mask != 0)) {
                 const uint32_t la = opaque_u(lbase);
                 const uint32_t rb = (uint32_t)(row0u + blk * 32 + 4 * hh);
                 // registers with a candidate in some lane (wave-uniform bit set),
@@ -1245,6 +1266,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                                 // common case once a seed bound exists: a few
                                 // instructions instead of a sorted insertion)
                                 lds_put_u64(la + (uint32_t)cnt * 512u, key);
+#ifdef LMI_ABLATION
+                                if (ABL == 7) atomicAdd(&lmi_dbg[2], 1ull);
+                                if (ABL == 7 && cnt + 1 == KL) atomicAdd(&lmi_dbg[4], 1ull);
+#endif
                                 if (++cnt == KL) {  // full: sort once, switch to list mode
                                     uint64_t L[KL];
                                     list_load<KL>(la, L);
@@ -1253,6 +1278,9 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                                     thr = std::min(thr, L[KL - 1]);
                                 }
                             } else {
+#ifdef LMI_ABLATION
+                                if (ABL == 7) atomicAdd(&lmi_dbg[3], 1ull);
+#endif
                                 uint64_t L[KL];
                                 list_load<KL>(la, L);
                                 list_insert<KL>(L, key);
@@ -1516,6 +1544,7 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 4) return launch_scan3_v<4>(b, s);
     if (abl == 5) return launch_scan3_v<5>(b, s);
     if (abl == 6) return launch_scan3_v<6>(b, s);
+    if (abl == 7) return launch_scan3_v<7>(b, s);
 #endif
     return launch_scan3_v<0>(b, s);
 }
@@ -1671,6 +1700,11 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
         b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
         b.ng = ng;
         b.lag = env_int("LMI_SCAN_LAG", 0, 0, 3);
+#ifdef LMI_ABLATION
+        // diagnostic: keep the previous call's per-pair bounds (near-final
+        // seeds when the same batch is repeated) to measure seeding quality
+        if (!getenv("LMI_SCAN_KEEP_THR"))
+#endif
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
         if (w.use_v3)
             rc = launch_scan3(b, s);
@@ -1701,6 +1735,16 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     LMI_LAUNCH_CHECK("chunk_merge_kernel");
     return LMI_OK;
 }
+
+#ifdef LMI_ABLATION
+// diagnostic builds: read and clear the scan's event counters (ABL == 7)
+extern "C" int lmi_debug_counters(unsigned long long* out8) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(lmi::lmi_dbg), sizeof(z)) != hipSuccess) return LMI_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lmi::lmi_dbg), z, sizeof(z)) != hipSuccess) return LMI_E_HIP;
+    return LMI_OK;
+}
+#endif
 
 extern "C" int lmi_timing_enable(int32_t on) {
     lmi::Timing& t = lmi::timing();

@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round artefacts: default bench line (with cpu_baseline), rocprofv3 kernel
+# stats of the same command, and the PMC traffic passes of the scan kernel
+# (FETCH_SIZE and WRITE_SIZE each in its own run).  Outputs under gpurun_out/prof/.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/prof
+export TMPDIR=/tmp
+KRE=${KRE:-scan3_kernel}
+timeout -k 10 500 python bench.py > gpurun_out/prof/bench.json 2> gpurun_out/prof/bench.err
+rc=$?; echo "bench rc=$rc"; cat gpurun_out/prof/bench.json | cut -c1-400; tail -2 gpurun_out/prof/bench.err
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run \
+   -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --recall-sample 20 > gpurun_out/prof/trace.json 2> gpurun_out/prof/trace.err
+rc=$?; echo "kernel-trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv \
+     -d gpurun_out/prof/pmc_$c -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --recall-sample 20 \
+     > gpurun_out/prof/pmc_$c.json 2> gpurun_out/prof/pmc_$c.err
+  rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
+done
+python3 - <<'PY'
+import csv, glob, json
+out = {}
+for c in ("FETCH_SIZE", "WRITE_SIZE"):
+    vals = []
+    for f in glob.glob(f"gpurun_out/prof/pmc_{c}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == c:
+                vals.append(float(r["Counter_Value"]))
+    out[c] = {"launches": len(vals), "mean_kb": sum(vals) / max(len(vals), 1)}
+print(json.dumps(out))
+json.dump(out, open("gpurun_out/prof/pmc_traffic.json", "w"))
+PY

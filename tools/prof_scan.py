@@ -45,3 +45,10 @@ for abl, var in runs:
     n = lib.lmi_timing_read(ms, a.reps)
     v = sorted(list(ms)[:n])
     print(f"[{var}] abl={abl} scan ms: median {v[len(v)//2]:.3f} min {v[0]:.3f}", flush=True)
+    if abl == "7" and hasattr(lib, "lmi_debug_counters"):
+        cnt = (_lib.C.c_ulonglong * 8)()
+        lib.lmi_debug_counters(cnt)
+        runs_ = a.reps + 2
+        names = ["wave-events", "candidates", "appends", "sorted-inserts", "fills", "wave-blocks"]
+        print("   per launch: " + ", ".join(f"{nm}={cnt[i] / runs_:.4g}" for i, nm in enumerate(names)),
+              flush=True)
