@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 1
+#define LMI_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -89,7 +89,8 @@ int lmi_router(const float* x, int32_t nq, int32_t ldx, const lmi_mlp_desc* mlp,
  * (LearnedIndex.py:143-145).  A shard of a G-GPU index holds a contiguous
  * slice of every bucket; `gpos` maps a local row to its global position in
  * the unsharded order (the tie-break key; within a bucket it is monotone in
- * the reference's g.index order). */
+ * the reference's g.index order).  Inside a bucket the rows may be grouped by
+ * sub-cluster as long as the rows of each chunk are in ascending gpos. */
 typedef struct lmi_index_desc {
     const void* corpus;        /* device, [n_rows][d_pad] of dtype, zero-padded past d */
     int32_t dtype;             /* LMI_F16 (values fp16-exact) or LMI_F32 */
@@ -104,6 +105,13 @@ typedef struct lmi_index_desc {
     const int32_t* chunk_first;/* device [C+1]: prefix of ceil(n_c/chunk_rows) (lmi_plan_chunks) */
     int32_t n_chunks;          /* chunk_first[C] */
     int32_t max_chunks;        /* max_c ceil(n_c/chunk_rows) */
+    /* ABI 2: optional (NULL = none) device [n_chunks][d_pad] f32, the unit
+     * centroid of each chunk.  When a bucket's rows are laid out by
+     * sub-cluster (every chunk one sub-cluster; rows inside a chunk still in
+     * ascending gpos), the scan visits each (query, probe)'s nearest chunk
+     * first, so its pruning bound starts near the final k-th distance.
+     * Results do not depend on it. */
+    const float* chunk_centroid;
 } lmi_index_desc;
 
 /* Host helper: fills chunk_first_out[C+1] from host bucket offsets and returns

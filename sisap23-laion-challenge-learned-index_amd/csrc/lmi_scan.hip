@@ -262,6 +262,158 @@ __global__ __launch_bounds__(kThreads) void plan_fill_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// nearest-chunk-first plan (scan v3, index with chunk centroids)
+//
+// Each (query, probe) pair scans every chunk of its bucket; the order only
+// decides how early its pruning bound gets tight.  With the bucket's rows
+// laid out by sub-cluster (one sub-cluster per chunk), a pair's nearest
+// neighbours sit mostly in the chunk whose centroid is nearest, so:
+//   pref_kernel       pair -> its nearest chunk (max cosine to the centroid)
+//   pref_sort_kernel  the bucket's pairs re-ordered by (nearest chunk, pair),
+//                     so a 256-pair tile group shares few nearest chunks
+//   tile3_fill_kernel the tile list: one "seed" tile per group first (the
+//                     nearest chunk of the group's median pair; they publish
+//                     each pair's bound through thr_g), then the rest
+//                     chunk-major
+// ---------------------------------------------------------------------------
+__device__ inline int bucket_pair_off(const int32_t* counts, int c, int* sh) {
+    int off = 0;
+    for (int b = threadIdx.x; b < c; b += kThreads) off += counts[b];
+    return block_sum(off, sh);
+}
+
+__global__ __launch_bounds__(kThreads) void pref_kernel(
+    const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
+    const float* __restrict__ centroid, int32_t d_pad, const _Float16* __restrict__ qbuf,
+    const int32_t* __restrict__ pair_q, int32_t R, int32_t P, int32_t* __restrict__ pref) {
+    // one wave per pair (thousands of waves hide the L2 latency of the loads)
+    const int lane = threadIdx.x & 63;
+    const int pp = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (pp >= P) return;
+    const int c = pair_bucket[pp];
+    if (c < 0) return;
+    const int c0 = chunk_first[c], nch = chunk_first[c + 1] - c0;
+    if (nch <= 1) {
+        if (lane == 0) pref[pp] = 0;
+        return;
+    }
+    const _Float16* qr = qbuf + (size_t)(pair_q[pp] / R) * d_pad;
+    float best = -3.0f;
+    int bj = 0;
+    for (int j = 0; j < nch; ++j) {
+        const float* cr = centroid + (size_t)(c0 + j) * d_pad;
+        float s = 0.0f;
+        for (int e = lane; e < d_pad; e += 64) s = fmaf((float)qr[e], cr[e], s);
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (s > best) {  // wave-uniform after the butterfly; ties -> lower chunk
+            best = s;
+            bj = j;
+        }
+    }
+    if (lane == 0) pref[pp] = bj;
+}
+
+__global__ __launch_bounds__(kThreads) void pref_sort_kernel(
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ chunk_first,
+    int32_t* __restrict__ pair_q, int32_t* __restrict__ pref, int32_t* __restrict__ tmp,
+    int32_t* __restrict__ tmp_pref, int32_t QB, int32_t* __restrict__ n_seed) {
+    __shared__ int sh[kThreads / 64];
+    __shared__ int wcnt[kThreads / 64];
+    const int c = blockIdx.x;
+    const int off = bucket_pair_off(counts, c, sh);
+    const int cnt = counts[c];
+    const int nch = chunk_first[c + 1] - chunk_first[c];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (nch <= 1) {  // nothing to order (an empty bucket has no tiles at all)
+        if (tid == 0) n_seed[c] = (nch == 1) ? (cnt + QB - 1) / QB : 0;
+        return;
+    }
+    // stable counting sort by pref: one ordered compaction pass per chunk
+    int run = 0;
+    for (int j = 0; j < nch; ++j) {
+        for (int base = 0; base < cnt; base += kThreads) {
+            const int e = base + tid;
+            const bool pred = (e < cnt) && (pref[off + e] == j);
+            const uint64_t m = __ballot(pred);
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            __syncthreads();
+            if (lane == 0) wcnt[w] = __popcll(m);
+            __syncthreads();
+            int wpre = 0, tot = 0;
+            for (int i = 0; i < kThreads / 64; ++i) {
+                wpre += (i < w) ? wcnt[i] : 0;
+                tot += wcnt[i];
+            }
+            if (pred) {
+                tmp[off + run + wpre + rank] = pair_q[off + e];
+                tmp_pref[off + run + wpre + rank] = j;
+            }
+            run += tot;
+        }
+    }
+    __syncthreads();
+    for (int e = tid; e < cnt; e += kThreads) {
+        pair_q[off + e] = tmp[off + e];
+        pref[off + e] = tmp_pref[off + e];
+    }
+    // one seed tile per group of QB pairs (see tile3_fill_kernel)
+    if (tid == 0) n_seed[c] = (cnt + QB - 1) / QB;
+}
+
+__global__ __launch_bounds__(kThreads) void tile3_fill_kernel(
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ chunk_first,
+    const int32_t* __restrict__ pref, const int32_t* __restrict__ n_seed, int32_t C, int32_t QB,
+    Tile* __restrict__ tiles, int32_t* __restrict__ meta, int32_t* __restrict__ work) {
+    __shared__ int sh[kThreads / 64];
+    const int c = blockIdx.x;
+    const int tid = threadIdx.x;
+    int s_lt = 0, r_lt = 0, s_all = 0, r_all = 0, off = 0;
+    for (int b = tid; b < C; b += kThreads) {
+        const int nch = chunk_first[b + 1] - chunk_first[b];
+        const int ng = nch > 0 ? (counts[b] + QB - 1) / QB : 0;
+        const int rest = ng * nch - n_seed[b];
+        s_all += n_seed[b];
+        r_all += rest;
+        if (b < c) {
+            s_lt += n_seed[b];
+            r_lt += rest;
+            off += counts[b];
+        }
+    }
+    s_lt = block_sum(s_lt, sh);
+    r_lt = block_sum(r_lt, sh);
+    s_all = block_sum(s_all, sh);
+    r_all = block_sum(r_all, sh);
+    off = block_sum(off, sh);
+    if (c == 0 && tid == 0) {
+        for (int x = 0; x < kGroups; ++x) {
+            meta[x] = 0;
+            meta[kGroups + x] = (x == 0) ? s_all + r_all : 0;
+            work[x] = 0;
+        }
+        meta[2 * kGroups] = s_all + r_all;
+        work[kGroups] = 0;
+    }
+    if (tid != 0) return;  // per-bucket tile lists are short: one thread writes them
+    const int cnt = counts[c];
+    const int nch = chunk_first[c + 1] - chunk_first[c];
+    if (cnt == 0 || nch == 0) return;
+    // the seed chunk of group g: the nearest chunk of its median pair (the
+    // group's pairs are sorted by nearest chunk, so it is the most common one)
+    const int ngr = (cnt + QB - 1) / QB;
+    int ps = s_lt, pr = s_all + r_lt;
+    for (int g = 0; g < ngr; ++g) {
+        const int n = min(QB, cnt - g * QB);
+        tiles[ps++] = Tile{c, off + g * QB, n, pref[off + g * QB + n / 2]};
+    }
+    for (int j = 0; j < nch; ++j)
+        for (int g = 0; g < ngr; ++g) {
+            const int n = min(QB, cnt - g * QB);
+            if (j != pref[off + g * QB + n / 2]) tiles[pr++] = Tile{c, off + g * QB, n, j};
+        }
+}
+
 // The next tile for a workgroup of group `gx`: its own group first, then steal.
 __device__ inline int dequeue_tile(const int32_t* meta, int32_t* work, int gx, int ng) {
     for (int k = 0; k < ng; ++k) {
@@ -662,11 +814,12 @@ __device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bo
     for (int reg = 0; reg < 16; ++reg) {
         if (dv[reg] <= bound) {
             const int i = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            // dv <= bound (the distance part of a bound that may come from
+            // another chunk, whose rows are ordered differently): no key test
             const uint64_t key = make_key(dv[reg], row_base + (uint32_t)i);
-            if (key < thr) {
-                lds_put_u64(qaddr + cnt * 512, key);
-                ++cnt;
-            }
+            lds_put_u64(qaddr + cnt * 512, key);
+            ++cnt;
+            (void)thr;
         }
     }
     for (int i = 0; __any(i < cnt); ++i) {
@@ -938,8 +1091,8 @@ __host__ __device__ constexpr int pieces_through(int s, bool norms) {
 }
 // DMA instructions issued after those of a phase-j stage s once stages up to
 // s + LOOK - 1 are issued (the steady state): the wait immediate of stage s
-constexpr int steady_after(int j) {
-    return pieces_through(j + LOOK - 1, true) - pieces_through(j, true);
+constexpr int steady_after(int j, int look = LOOK) {
+    return pieces_through(j + look - 1, true) - pieces_through(j, true);
 }
 static_assert(NST == 3, "the stage loop spells out three phases");
 }  // namespace v3
@@ -1040,6 +1193,29 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 __device__ unsigned long long lmi_dbg[8];
 #endif
 
+// Per-lane pick of acc[rg] (rg differs by lane): a 4-level select tree on
+// lane masks (inline asm: written as C++ ternaries the compiler turns the
+// tree back into a dynamically indexed array on scratch).
+__device__ __forceinline__ float sel_mask(float a, float b, uint64_t m) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+__device__ __forceinline__ float select16(const f32x16& acc, int rg) {
+    const uint64_t b3 = __builtin_amdgcn_ballot_w64((rg & 8) != 0);
+    const uint64_t b2 = __builtin_amdgcn_ballot_w64((rg & 4) != 0);
+    const uint64_t b1 = __builtin_amdgcn_ballot_w64((rg & 2) != 0);
+    const uint64_t b0 = __builtin_amdgcn_ballot_w64((rg & 1) != 0);
+    float v8[8], v4[4], v2[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v8[e] = sel_mask(acc[e], acc[e + 8], b3);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v4[e] = sel_mask(v8[e], v8[e + 4], b2);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) v2[e] = sel_mask(v4[e], v4[e + 2], b1);
+    return sel_mask(v2[0], v2[1], b0);
+}
+
 // Keeps the compiler from hoisting lane-dependent address arithmetic out of
 // the tile loop (each hoisted value would pin a VGPR for the whole kernel).
 __device__ __forceinline__ int opaque(int x) {
@@ -1056,7 +1232,16 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
     constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6;
     constexpr bool kNoEpi = ABL == 2 || ABL == 5 || ABL == 6;
-    constexpr bool kNoIns = ABL == 1 || ABL == 4;
+    constexpr bool kNoIns = ABL == 1 || ABL == 4 || ABL == 18 || ABL == 19;
+    // placement of the stage's DMA issue in the MFMA stream (tuning, diagnostic
+    // builds): -1 = before the A-fragment prefetch, else after MFMA #kDmaTT
+    // stages the DMA runs ahead (tuning, diagnostic builds: 12 = one block)
+    constexpr int LK = ABL == 12 ? NST : LOOK;
+    // An LDS-DMA issue holds its wave for ~45-60 cycles; the two waves of a
+    // SIMD run in lockstep between barriers, so they issue at different MFMAs
+    // (slots 0-3 early, 4-7 late) and the partner keeps the matrix pipe fed.
+    constexpr int kDmaTT = ABL == 8 ? -1 : ABL == 9 ? 8 : ABL == 10 ? 15 : 2;
+    constexpr int kDmaLate = (ABL == 13) ? kDmaTT : 10;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
     // [wave][KL][64 lanes] u64: every lane's partial top-k list (lane-private
@@ -1088,6 +1273,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         slot = __builtin_amdgcn_readfirstlane(slot);
     }
     const int gx = xcc & (ng - 1);
+    const bool late = slot >= NW / 2;
+    if (ABL == 11 && slot >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half
     // this lane's list column: entry i at lbase + i * 512
     const uint32_t lbase = (uint32_t)(uintptr_t)(lists + wave * KL * 64 + lane);
 
@@ -1147,8 +1334,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         auto dma_stage = [&](int so, int b, int j) {
             if (kNoDma) return;
             unsigned char* sl = ring + so;
+            if (ABL == 17 || ABL == 19) b = 0, j = 0;  // diagnostic: every DMA re-reads the chunk's first stage
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
                                                      b * (32 * D * 2) + j * ROWB, 0, 0);
+            if (ABL == 16 || ABL == 18) return;  // diagnostic: one piece per stage
             // (+2 rows through soffset: an instruction offset would move the
             // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave + 1) * PIECEP), 16,
@@ -1159,8 +1348,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                                                          (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
         };
         // prologue: stages 0 .. LOOK-1 (blocks 0 and 1) into slots 0 .. LOOK-1
-        static_assert(LOOK % NST == 0, "the DMA runs whole blocks ahead");
-        constexpr int AHEAD = LOOK / NST;
+        static_assert(LK % NST == 0 && LK < NSLOT, "the DMA runs whole blocks ahead");
+        constexpr int AHEAD = LK / NST;
         for (int b = 0; b < std::min(nblk, AHEAD); ++b)
 #pragma unroll
             for (int j = 0; j < NST; ++j) dma_stage((b * NST + j) * STAGE, b, j);
@@ -1178,23 +1367,28 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 const int s = blk * NST + j;
                 // stage s must have landed: the DMAs issued after it are those of
                 // stages s+1 .. min(T-1, s+LOOK-1), 2 pieces each + 1 in phase 2
-                if (!kNoDma) {
+                if (!kNoDma && ABL != 14) {
                     if (steady) {
                         if (j == 0)
-                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(0)));
+                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(0, LK)));
                         else if (j == 1)
-                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(1)));
+                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(1, LK)));
                         else
-                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(2)));
+                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(2, LK)));
                     } else {
                         vm_wait_dyn(v3::pieces_through(T - 1, true) - v3::pieces_through(s, true));
                     }
                 }
-                if (ABL != 6) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                const int wso = pso;  // this stage's DMA (stage s + LOOK) goes to stage s-1's slot
+                if (ABL != 6 && ABL != 15) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                // this stage's DMA (stage s + LK) goes to stage s-1's slot when
+                // LK = NSLOT - 1 (the default)
+                const int wso = (LK == NSLOT - 1) ? pso
+                              : (so + LK * STAGE >= NSLOT * STAGE ? so + LK * STAGE - NSLOT * STAGE
+                                                                 : so + LK * STAGE);
                 if (ABL == 2 || !wave_live) {
                     if (steady) dma_stage(wso, blk + AHEAD, j);
                 } else {
+                    if (kDmaTT < 0 && steady) dma_stage(wso, blk + AHEAD, j);
                     const unsigned char* rp = ring + so + opaque_u(lane_off);
 #define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
                     half8 af[16];
@@ -1205,7 +1399,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                         if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
                         acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
                                                   : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
-                        if (tt == 4 && steady) dma_stage(wso, blk + AHEAD, j);
+                        if (tt == (late ? kDmaLate : kDmaTT) && steady) dma_stage(wso, blk + AHEAD, j);
                         // keep the A-fragment reads 3 MFMAs ahead, no further
                         __builtin_amdgcn_sched_barrier(0);
                     }
@@ -1247,46 +1441,52 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             if (!kNoIns && __any(mask != 0)) {
                 const uint32_t la = opaque_u(lbase);
                 const uint32_t rb = (uint32_t)(row0u + blk * 32 + 4 * hh);
-                // registers with a candidate in some lane (wave-uniform bit set),
-                // one at a time with a uniform register index (v_movrels): no
-                // per-register code copies, few live registers
-                uint32_t wm = __builtin_amdgcn_readfirstlane(__ockl_wfred_or_u32(mask));
+                // every lane walks its own candidates, lowest register first:
+                // iterations = the largest per-lane count (usually 1-2), the
+                // accumulator picked by a select tree.  Candidates: d <= the
+                // distance part of thr, a bound that may come from another
+                // chunk (rows ordered differently there), so no key test
+                // against it; ties at the bound are resolved by the chunk merge.
+                uint32_t m = mask;
 #pragma unroll 1
-                for (; wm != 0; wm &= wm - 1) {
-                    const int rg = __builtin_ctz(wm);
-                    if ((mask >> rg) & 1u) {
+                while (__any(m != 0)) {
+                    if (m != 0) {
+                        const int rg = __builtin_ctz(m);
+                        m &= m - 1;
+                        const float dot = select16(acc, rg);
                         const int i = (rg & 3) + 8 * (rg >> 2);
                         const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
-                        const float d = fmaf(-acc[rg], my_invq * n1, 1.0f);
+                        const float d = fmaf(-dot, my_invq * n1, 1.0f);
                         const uint64_t key = make_key(d, rb + (uint32_t)i);
-                        if (key < thr) {
-                            if (cnt < KL) {
-                                // append mode: the first KL candidates below the
-                                // tile's starting bound are stored unsorted (the
-                                // common case once a seed bound exists: a few
-                                // instructions instead of a sorted insertion)
-                                lds_put_u64(la + (uint32_t)cnt * 512u, key);
+                        if (cnt < KL) {
+                            // append mode: the first KL candidates are stored
+                            // unsorted (a few instructions); a full buffer is
+                            // sorted once and the lane switches to list mode
+                            lds_put_u64(la + (uint32_t)cnt * 512u, key);
 #ifdef LMI_ABLATION
-                                if (ABL == 7) atomicAdd(&lmi_dbg[2], 1ull);
-                                if (ABL == 7 && cnt + 1 == KL) atomicAdd(&lmi_dbg[4], 1ull);
+                            if (ABL == 7) atomicAdd(&lmi_dbg[2], 1ull);
+                            if (ABL == 7 && cnt + 1 == KL) atomicAdd(&lmi_dbg[4], 1ull);
 #endif
-                                if (++cnt == KL) {  // full: sort once, switch to list mode
-                                    uint64_t L[KL];
-                                    list_load<KL>(la, L);
-                                    list_sort<KL>(L);
-                                    list_store<KL>(la, L);
-                                    thr = std::min(thr, L[KL - 1]);
-                                }
-                            } else {
-#ifdef LMI_ABLATION
-                                if (ABL == 7) atomicAdd(&lmi_dbg[3], 1ull);
-#endif
+                            if (++cnt == KL) {
                                 uint64_t L[KL];
                                 list_load<KL>(la, L);
-                                list_insert<KL>(L, key);
+                                list_sort<KL>(L);
                                 list_store<KL>(la, L);
                                 thr = std::min(thr, L[KL - 1]);
                             }
+                        } else {
+                            // (the list lives in LDS: registers are taken by
+                            // the query fragments)
+                            uint64_t L[KL];
+                            list_load<KL>(la, L);
+                            if (key < L[KL - 1]) {
+#ifdef LMI_ABLATION
+                                if (ABL == 7) atomicAdd(&lmi_dbg[3], 1ull);
+#endif
+                                list_insert<KL>(L, key);
+                                list_store<KL>(la, L);
+                            }
+                            thr = std::min(thr, L[KL - 1]);
                         }
                     }
                 }
@@ -1340,10 +1540,21 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
     const int nch = chunk_first[c + 1] - chunk_first[c];
     uint64_t M[KL];
     list_clear<KL>(M);
+    // A chunk list is ordered by (distance, row); rows inside a chunk are in
+    // ascending global position (the index layout guarantees it), so mapping
+    // each key to (distance, global position) keeps the list ordered, and the
+    // merge across chunks is by the reference's (distance, g.index) order.
     for (int j = 0; j < nch; ++j) {
         const uint64_t* src = partial + ((size_t)pp * max_chunks + j) * KL;
         for (int i = 0; i < KL; ++i) {
-            const uint64_t key = src[i];
+            uint64_t key = src[i];
+            if (key == kEmptyKey) break;
+            const uint32_t lp = (uint32_t)key;
+            if (lp >= (uint32_t)n_rows) {  // never for a sound scan: drop, flag
+                atomicOr(status, LMI_STATUS_INTERNAL);
+                break;
+            }
+            key = (key & 0xffffffff00000000ull) | (uint32_t)gpos[lp];
             if (key >= M[KL - 1]) break;
             list_insert<KL>(M, key);
         }
@@ -1354,11 +1565,8 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
         if (i < k) {
             const uint64_t key = M[i];
             const bool empty = key == kEmptyKey;
-            const uint32_t lp = (uint32_t)key;
-            const bool bad = !empty && lp >= (uint32_t)n_rows;  // never for a sound scan
-            if (bad) atomicOr(status, LMI_STATUS_INTERNAL);
-            out_d[o + i] = (empty || bad) ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
-            out_pos[o + i] = (empty || bad) ? -1 : gpos[lp];
+            out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
+            out_pos[o + i] = empty ? -1 : (int32_t)(uint32_t)key;
         }
     }
     (void)counts_total_src;
@@ -1368,7 +1576,8 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
 // host side
 // ---------------------------------------------------------------------------
 struct WsLayout {
-    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, ntiles, work, partial, thr_g, total;
+    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, ntiles, work, partial, thr_g, pref,
+        pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
     int32_t qb;      // queries per tile
     bool use_v2;     // scan2_kernel
@@ -1416,6 +1625,10 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     w.work = take(4 * (kGroups + 1));
     w.partial = take(P * (size_t)std::max(idx->max_chunks, 1) * KL * sizeof(uint64_t));
     w.thr_g = take(P * sizeof(uint64_t));
+    w.pref = take(P * 4);
+    w.pref_tmp = take(P * 4);
+    w.pref_tmp2 = take(P * 4);
+    w.n_seed = take((size_t)idx->n_buckets * 4);
     w.total = off;
     return w;
 }
@@ -1545,6 +1758,18 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 5) return launch_scan3_v<5>(b, s);
     if (abl == 6) return launch_scan3_v<6>(b, s);
     if (abl == 7) return launch_scan3_v<7>(b, s);
+    if (abl == 12) return launch_scan3_v<12>(b, s);
+    if (abl == 13) return launch_scan3_v<13>(b, s);
+    if (abl == 14) return launch_scan3_v<14>(b, s);
+    if (abl == 15) return launch_scan3_v<15>(b, s);
+    if (abl == 16) return launch_scan3_v<16>(b, s);
+    if (abl == 17) return launch_scan3_v<17>(b, s);
+    if (abl == 18) return launch_scan3_v<18>(b, s);
+    if (abl == 19) return launch_scan3_v<19>(b, s);
+    if (abl == 11) return launch_scan3_v<11>(b, s);
+    if (abl == 10) return launch_scan3_v<10>(b, s);
+    if (abl == 9) return launch_scan3_v<9>(b, s);
+    if (abl == 8) return launch_scan3_v<8>(b, s);
 #endif
     return launch_scan3_v<0>(b, s);
 }
@@ -1664,6 +1889,23 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kThreads), 0, s, classes, P, C, counts,
                        idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
+    const bool nearest_first = w.use_v3 && idx->chunk_centroid && !getenv("LMI_SCAN_NO_PREF");
+    if (nearest_first) {
+        int32_t* pref = (int32_t*)(ws + w.pref);
+        int32_t* n_seed = (int32_t*)(ws + w.n_seed);
+        hipLaunchKernelGGL(pref_kernel, dim3((P + kThreads / 64 - 1) / (kThreads / 64)), dim3(kThreads),
+                           0, s, pair_bucket, idx->chunk_first, idx->chunk_centroid, idx->d_pad,
+                           (const _Float16*)(ws + w.qbuf), pair_q, R, P, pref);
+        LMI_LAUNCH_CHECK("pref_kernel");
+        hipLaunchKernelGGL(pref_sort_kernel, dim3(C), dim3(kThreads), 0, s, counts, idx->chunk_first,
+                           pair_q, pref, (int32_t*)(ws + w.pref_tmp), (int32_t*)(ws + w.pref_tmp2), QB,
+                           n_seed);
+        LMI_LAUNCH_CHECK("pref_sort_kernel");
+        hipLaunchKernelGGL(tile3_fill_kernel, dim3(C), dim3(kThreads), 0, s, counts, idx->chunk_first,
+                           pref, n_seed, C, QB, tiles, meta, work);
+        LMI_LAUNCH_CHECK("tile3_fill_kernel");
+        ng = 1;  // one queue: seed tiles strictly first
+    }
 
     ScanArgs a{};
     a.corpus = idx->corpus;

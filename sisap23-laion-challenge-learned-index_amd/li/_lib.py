@@ -71,6 +71,9 @@ class MlpDesc(C.Structure):
     ]
 
 
+ABI_VERSION = 2
+
+
 class IndexDesc(C.Structure):
     _fields_ = [
         ("corpus", C.c_void_p),
@@ -86,6 +89,7 @@ class IndexDesc(C.Structure):
         ("chunk_first", C.c_void_p),
         ("n_chunks", C.c_int32),
         ("max_chunks", C.c_int32),
+        ("chunk_centroid", C.c_void_p),  # ABI 2
     ]
 
 
@@ -130,7 +134,7 @@ def load() -> C.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.lmi_abi_version() != 1:
+        if lib.lmi_abi_version() != ABI_VERSION:
             raise LmiUnavailable("liblmi_hip.so ABI version mismatch")
         _lib = lib
         return lib

@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == 1
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
@@ -88,3 +88,34 @@ def test_bucket_stripes_partition_every_bucket(world):
     for c in range(7):
         rows = L.order[L.bucket_off[c]:L.bucket_off[c + 1]]
         assert np.all(np.diff(rows) > 0) and np.all(lab[rows] == c)
+
+
+def test_subcluster_layout_keeps_rows_and_chunk_order():
+    """Host-side index layout (no GPU compute): every bucket is re-ordered by
+    sub-cluster, each chunk stays in ascending global position, every row keeps
+    its vector / 1/||y|| / global position, and the chunk centroids are unit."""
+    import numpy as np
+    import torch
+    import workloads
+    from li.index import DeviceIndex
+    w = workloads.clustered(n=3000, nq=8, C=8, seed=2, label_mode="skewed")
+    ix = DeviceIndex(w["x"], w["labels"], w["C"], device="cpu", chunk_rows=64, subcluster=True)
+    base = DeviceIndex(w["x"], w["labels"], w["C"], device="cpu", chunk_rows=64, subcluster=False)
+    off = ix.bucket_off_local.numpy()
+    cf = ix.chunk_first.numpy()
+    gp, gp0 = ix.gpos.numpy(), base.gpos.numpy()
+    moved = 0
+    for c in range(w["C"]):
+        a, b = off[c], off[c + 1]
+        assert sorted(gp[a:b]) == list(gp0[a:b])           # same rows per bucket
+        moved += int((gp[a:b] != gp0[a:b]).sum())
+        for j in range(cf[c + 1] - cf[c]):
+            seg = gp[a + 64 * j: min(b, a + 64 * (j + 1))]
+            assert np.all(np.diff(seg) > 0)                  # ascending inside a chunk
+    assert moved > 0                                          # the layout did change
+    row_of = {int(g): i for i, g in enumerate(gp0)}
+    idx = torch.tensor([row_of[int(g)] for g in gp])
+    assert torch.equal(ix.corpus, base.corpus[idx])
+    assert torch.equal(ix.inv_norm, base.inv_norm[idx])
+    nrm = ix.chunk_centroid[:, : ix.d].norm(dim=1)
+    assert torch.allclose(nrm, torch.ones_like(nrm), atol=1e-5)

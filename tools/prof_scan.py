@@ -14,6 +14,7 @@ ap.add_argument("--R", type=int, default=4)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--chunk-rows", type=int, default=8192)
 ap.add_argument("--abl", default="0")
+ap.add_argument("--no-subcluster", action="store_true")
 ap.add_argument("--variants", default="",
                 help="'|'-separated env settings, e.g. 'LMI_SCAN_GROUPS=1,LMI_SCAN_LAG=1|LMI_SCAN_GROUPS=8'")
 a = ap.parse_args()
@@ -21,7 +22,7 @@ dev = torch.device("cuda")
 x, q, qn, xn, layers = synth.build_lmi_workload(a.n, a.nq, 122, "MLP-5", dev)
 router = DeviceRouter(layers)
 labels = router.argmax(xn); del xn
-ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows)
+ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows, subcluster=not a.no_subcluster)
 classes, _ = router.topr(qn, a.R)
 lib = _lib.load()
 runs = [(abl, "") for abl in a.abl.split(",")]
