@@ -1039,7 +1039,8 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
 // scan v3 (fp16 corpus, fp16-exact queries, d_pad == 768, k <= 10): the v2
 // ring with 8 waves = two per SIMD.
 //
-//   per wave : 32 queries, B fragments (K = 768) in AGPRs for the whole tile;
+//   per wave : 32 queries, B fragments (K = 768) in VGPRs for the whole tile
+//              (VGPR-form MFMAs: a kernel with no AGPR gets all 256 registers);
 //              the wave serves query group `slot` of the tile, slots being a
 //              SIMD-balanced numbering (groups 0-3 land on four different
 //              SIMDs, whatever the wave -> SIMD placement)
@@ -1047,20 +1048,20 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
 //              object byte serves 256 queries (v2: 128), halving the
 //              L2 -> LDS traffic, and the two waves of a SIMD hide each
 //              other's filter / insertion VALU behind their MFMAs
-//   ring     : 7 slots of 32 rows x 256 k (16 pieces of two interleaved rows,
-//              see v3::PIECEP) + the block's 32 norms in the slot of its
-//              last stage; DMA 6 stages (2 blocks) ahead; each wave stages
-//              two 1-KiB pieces per stage and its 4 norms once per block;
-//              one s_barrier per stage; slot offsets and DMA offsets are
-//              running values and the steady-state waits immediates (the
-//              scalar unit is shared by the CU's 8 waves)
+//   ring     : 6 slots = two 32-row blocks of 3 stages (32 rows x 256 k,
+//              16 pieces of two interleaved rows, see v3::PIECEP) + each
+//              block's 32 norms in its last stage's slot; block b+1's DMA
+//              rides in block b (each wave two 1-KiB pieces per stage and its
+//              4 norms per block, at different MFMAs for the two waves of a
+//              SIMD); one s_barrier per block
 //   lists    : each lane's partial top-k list lives in LDS (registers are
 //              taken by the query fragments); the filter bound stays in
 //              registers, so the list is touched only on insertion
 //   epilogue : per 32-row block, right after its last MFMA: a 16-bit
-//              candidate mask from d = 1 - dot/(|q||y|) <= bound, and only
-//              if some lane has a candidate, a per-register ballot-gated
-//              insertion that recomputes d from the accumulator
+//              candidate mask from d = 1 - dot/(|q||y|) <= bound; only if
+//              some lane has a candidate, every lane walks its own candidates
+//              (accumulator picked by a select tree): the first KL are
+//              appended unsorted, later ones inserted into the sorted list
 // ---------------------------------------------------------------------------
 namespace v3 {
 constexpr int D = 768;
@@ -1075,26 +1076,13 @@ constexpr int PIECEP = 2 * ROWB + 32;  // piece pitch
 constexpr int NST = D * 2 / ROWB;      // stages per 32-row block
 constexpr int NORM_OFF = 16 * PIECEP;  // the block's 32 norms (last stage's slot)
 constexpr int STAGE = NORM_OFF + 128;
-constexpr int NSLOT = 7;
-constexpr int LOOK = NSLOT - 1;        // the DMA runs this many stages ahead
+constexpr int NSLOT = 2 * NST;         // two blocks: one read, the next in flight
 constexpr int NW = 8;
 constexpr int QB = NW * 32;
 constexpr int NQF = D / 16;
 constexpr int KL = 10;
 constexpr size_t lds_bytes = (size_t)NSLOT * STAGE + (size_t)NW * KL * 64 * 8 + 64;
 static_assert(lds_bytes <= 160 * 1024, "LDS budget");
-
-// DMA instructions a wave issues for stages 0..s: two pieces per stage, plus
-// its 4 norms in the last stage of each block
-__host__ __device__ constexpr int pieces_through(int s, bool norms) {
-    return s < 0 ? 0 : 2 * (s + 1) + (norms ? (s + 1) / NST : 0);
-}
-// DMA instructions issued after those of a phase-j stage s once stages up to
-// s + LOOK - 1 are issued (the steady state): the wait immediate of stage s
-constexpr int steady_after(int j, int look = LOOK) {
-    return pieces_through(j + look - 1, true) - pieces_through(j, true);
-}
-static_assert(NST == 3, "the stage loop spells out three phases");
 }  // namespace v3
 
 
@@ -1117,15 +1105,6 @@ __device__ __forceinline__ f32x16 mfma_drain_v(const f32x16& c) {
     return d;
 }
 
-__device__ __forceinline__ void vm_wait_dyn(int n) {
-#define LMI_VMW(k) \
-    case k: __builtin_amdgcn_s_waitcnt(waitcnt_vm(k)); break;
-    switch (n) {
-        LMI_VMW(1) LMI_VMW(2) LMI_VMW(3) LMI_VMW(4) LMI_VMW(5) LMI_VMW(6) LMI_VMW(7) LMI_VMW(8) LMI_VMW(9) LMI_VMW(10) LMI_VMW(11) LMI_VMW(12) LMI_VMW(13) LMI_VMW(14) LMI_VMW(15) LMI_VMW(16) LMI_VMW(17) LMI_VMW(18) LMI_VMW(19) LMI_VMW(20) LMI_VMW(21) LMI_VMW(22) LMI_VMW(23) LMI_VMW(24) LMI_VMW(25) LMI_VMW(26) LMI_VMW(27) LMI_VMW(28) LMI_VMW(29) LMI_VMW(30) LMI_VMW(31) LMI_VMW(32) LMI_VMW(33) LMI_VMW(34) LMI_VMW(35) LMI_VMW(36) LMI_VMW(37) LMI_VMW(38) LMI_VMW(39) LMI_VMW(40)
-        default: __builtin_amdgcn_s_waitcnt(waitcnt_vm(0)); break;
-    }
-#undef LMI_VMW
-}
 
 // LDS list entries at a base VGPR + immediate offset (one address register
 // for a whole list; plain-C++ addressing would hoist one register per entry)
@@ -1230,18 +1209,17 @@ __device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
 template <int ABL = 0>
 __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
+    // diagnostic builds only (results wrong for ABL != 0): 1 no insertion,
+    // 2 DMA + barriers only, 3 no DMA, 4 no DMA and no insertion, 5 no DMA and
+    // no epilogue, 6 = 5 without barriers, 7 event counters, 14 no DMA wait,
+    // 21 no barrier
     constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6;
     constexpr bool kNoEpi = ABL == 2 || ABL == 5 || ABL == 6;
-    constexpr bool kNoIns = ABL == 1 || ABL == 4 || ABL == 18 || ABL == 19;
-    // placement of the stage's DMA issue in the MFMA stream (tuning, diagnostic
-    // builds): -1 = before the A-fragment prefetch, else after MFMA #kDmaTT
-    // stages the DMA runs ahead (tuning, diagnostic builds: 12 = one block)
-    constexpr int LK = ABL == 12 ? NST : LOOK;
-    // An LDS-DMA issue holds its wave for ~45-60 cycles; the two waves of a
-    // SIMD run in lockstep between barriers, so they issue at different MFMAs
-    // (slots 0-3 early, 4-7 late) and the partner keeps the matrix pipe fed.
-    constexpr int kDmaTT = ABL == 8 ? -1 : ABL == 9 ? 8 : ABL == 10 ? 15 : 2;
-    constexpr int kDmaLate = (ABL == 13) ? kDmaTT : 10;
+    constexpr bool kNoIns = ABL == 1 || ABL == 4;
+    constexpr bool kNoBar = ABL == 6 || ABL == 21;
+    // An LDS-DMA issue holds its wave for ~45-60 cycles: the two waves of a
+    // SIMD issue theirs at different MFMAs (slots 0-3 early, 4-7 late)
+    constexpr int kDmaTT = 2, kDmaLate = 10;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
     // [wave][KL][64 lanes] u64: every lane's partial top-k list (lane-private
@@ -1274,7 +1252,6 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     }
     const int gx = xcc & (ng - 1);
     const bool late = slot >= NW / 2;
-    if (ABL == 11 && slot >= 4) __builtin_amdgcn_s_setprio(1);  // static priority, younger half
     // this lane's list column: entry i at lbase + i * 512
     const uint32_t lbase = (uint32_t)(uintptr_t)(lists + wave * KL * 64 + lane);
 
@@ -1324,20 +1301,16 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             (void*)(a.inv_norm + row0u), (short)0, nrows * 4, 0x00020000);
 
         const int nblk = (nrows + 31) / 32;
-        const int T = nblk * NST;
         // DMA of one stage (block b, phase j) into the LDS slot at byte offset
         // `so`: pieces 0, 1 = rows 4w+2i, 4w+2i+1 (lane l: row 4w + 2i + (l&1),
         // chunk l >> 1; piece 1 is piece 0 + 2 rows through soffset); in the
         // block's last phase the wave's 4 norms too.
-        // Every wave issues the same count, so the waits below are immediates.
         const uint32_t vo_row = (uint32_t)((4 * wave + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
         auto dma_stage = [&](int so, int b, int j) {
             if (kNoDma) return;
             unsigned char* sl = ring + so;
-            if (ABL == 17 || ABL == 19) b = 0, j = 0;  // diagnostic: every DMA re-reads the chunk's first stage
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
                                                      b * (32 * D * 2) + j * ROWB, 0, 0);
-            if (ABL == 16 || ABL == 18) return;  // diagnostic: one piece per stage
             // (+2 rows through soffset: an instruction offset would move the
             // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave + 1) * PIECEP), 16,
@@ -1347,68 +1320,47 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(sl + NORM_OFF + 16 * wave), 4,
                                                          (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
         };
-        // prologue: stages 0 .. LOOK-1 (blocks 0 and 1) into slots 0 .. LOOK-1
-        static_assert(LK % NST == 0 && LK < NSLOT, "the DMA runs whole blocks ahead");
-        constexpr int AHEAD = LK / NST;
-        for (int b = 0; b < std::min(nblk, AHEAD); ++b)
+        // block b lives in slots NST*(b&1) .. +NST-1; block 0 is the prologue,
+        // block b+1's DMA rides in block b
 #pragma unroll
-            for (int j = 0; j < NST; ++j) dma_stage((b * NST + j) * STAGE, b, j);
+        for (int j = 0; j < NST; ++j) dma_stage(j * STAGE, 0, j);
         // a lane's A-fragment base inside a slot (row col = lane & 31, half h)
         const uint32_t lane_off = (uint32_t)(((lane >> 1) & 15) * PIECEP + (lane & 1) * 16 + (lane >> 5) * 32);
 
-        int so = 0;                    // slot of the stage being read
-        int pso = (NSLOT - 1) * STAGE;  // slot of the previous stage = target of this stage's DMA
         f32x16 acc;
         for (int blk = 0; blk < nblk; ++blk) {
-            const bool steady = blk + AHEAD < nblk;  // stages s+1 .. s+LOOK-1 all issued
-            int nso = 0;                             // slot holding this block's norms
+            const bool more = blk + 1 < nblk;
+            const int rs0 = (blk & 1) * NST * STAGE;        // this block's slots
+            const int ws0 = ((blk + 1) & 1) * NST * STAGE;  // the next block's (= block blk-1's)
+            // one barrier per block: this wave's DMA of block blk has landed
+            // (nothing newer is in flight yet) and, past the barrier, every
+            // wave's has, and every wave is done with block blk-1's slots
+            if (ABL != 14) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+            if (!kNoBar) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
-                const int s = blk * NST + j;
-                // stage s must have landed: the DMAs issued after it are those of
-                // stages s+1 .. min(T-1, s+LOOK-1), 2 pieces each + 1 in phase 2
-                if (!kNoDma && ABL != 14) {
-                    if (steady) {
-                        if (j == 0)
-                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(0, LK)));
-                        else if (j == 1)
-                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(1, LK)));
-                        else
-                            __builtin_amdgcn_s_waitcnt(waitcnt_vm(v3::steady_after(2, LK)));
-                    } else {
-                        vm_wait_dyn(v3::pieces_through(T - 1, true) - v3::pieces_through(s, true));
-                    }
-                }
-                if (ABL != 6 && ABL != 15) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                // this stage's DMA (stage s + LK) goes to stage s-1's slot when
-                // LK = NSLOT - 1 (the default)
-                const int wso = (LK == NSLOT - 1) ? pso
-                              : (so + LK * STAGE >= NSLOT * STAGE ? so + LK * STAGE - NSLOT * STAGE
-                                                                 : so + LK * STAGE);
                 if (ABL == 2 || !wave_live) {
-                    if (steady) dma_stage(wso, blk + AHEAD, j);
-                } else {
-                    if (kDmaTT < 0 && steady) dma_stage(wso, blk + AHEAD, j);
-                    const unsigned char* rp = ring + so + opaque_u(lane_off);
-#define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
-                    half8 af[16];
-#pragma unroll
-                    for (int tt = 0; tt < 3; ++tt) af[tt] = LMI_A3(tt);
-#pragma unroll
-                    for (int tt = 0; tt < 16; ++tt) {
-                        if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
-                        acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
-                                                  : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
-                        if (tt == (late ? kDmaLate : kDmaTT) && steady) dma_stage(wso, blk + AHEAD, j);
-                        // keep the A-fragment reads 3 MFMAs ahead, no further
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-#undef LMI_A3
+                    if (more) dma_stage(ws0 + j * STAGE, blk + 1, j);
+                    continue;
                 }
-                if (j == NST - 1) nso = so;
-                pso = so;
-                so = (so + STAGE == NSLOT * STAGE) ? 0 : so + STAGE;
+                const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
+#define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
+                half8 af[16];
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt) af[tt] = LMI_A3(tt);
+#pragma unroll
+                for (int tt = 0; tt < 16; ++tt) {
+                    if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
+                    acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
+                                              : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
+                    if (tt == (late ? kDmaLate : kDmaTT) && more)
+                        dma_stage(ws0 + j * STAGE, blk + 1, j);
+                    // keep the A-fragment reads 3 MFMAs ahead, no further
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#undef LMI_A3
             }
+            const int nso = rs0 + (NST - 1) * STAGE;  // slot holding this block's norms
             if (kNoEpi || !wave_live) continue;
             // ---- epilogue of this block ----------------------------------------
             acc = mfma_drain_v(acc);
@@ -1758,18 +1710,8 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 5) return launch_scan3_v<5>(b, s);
     if (abl == 6) return launch_scan3_v<6>(b, s);
     if (abl == 7) return launch_scan3_v<7>(b, s);
-    if (abl == 12) return launch_scan3_v<12>(b, s);
-    if (abl == 13) return launch_scan3_v<13>(b, s);
     if (abl == 14) return launch_scan3_v<14>(b, s);
-    if (abl == 15) return launch_scan3_v<15>(b, s);
-    if (abl == 16) return launch_scan3_v<16>(b, s);
-    if (abl == 17) return launch_scan3_v<17>(b, s);
-    if (abl == 18) return launch_scan3_v<18>(b, s);
-    if (abl == 19) return launch_scan3_v<19>(b, s);
-    if (abl == 11) return launch_scan3_v<11>(b, s);
-    if (abl == 10) return launch_scan3_v<10>(b, s);
-    if (abl == 9) return launch_scan3_v<9>(b, s);
-    if (abl == 8) return launch_scan3_v<8>(b, s);
+    if (abl == 21) return launch_scan3_v<21>(b, s);
 #endif
     return launch_scan3_v<0>(b, s);
 }

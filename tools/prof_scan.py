@@ -15,6 +15,7 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--chunk-rows", type=int, default=8192)
 ap.add_argument("--abl", default="0")
 ap.add_argument("--no-subcluster", action="store_true")
+ap.add_argument("--check", action="store_true", help="compare every variant's lists to abl=0 (bitwise)")
 ap.add_argument("--variants", default="",
                 help="'|'-separated env settings, e.g. 'LMI_SCAN_GROUPS=1,LMI_SCAN_LAG=1|LMI_SCAN_GROUPS=8'")
 a = ap.parse_args()
@@ -25,6 +26,10 @@ labels = router.argmax(xn); del xn
 ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows, subcluster=not a.no_subcluster)
 classes, _ = router.topr(qn, a.R)
 lib = _lib.load()
+ref = None
+if a.check:
+    os.environ["LMI_SCAN_ABL"] = "0"
+    ref = bucket_topk(ix, q, classes, 10)[:2]
 runs = [(abl, "") for abl in a.abl.split(",")]
 if a.variants:
     runs = [(abl, v) for v in a.variants.split("|") for abl in a.abl.split(",")]
@@ -46,6 +51,10 @@ for abl, var in runs:
     n = lib.lmi_timing_read(ms, a.reps)
     v = sorted(list(ms)[:n])
     print(f"[{var}] abl={abl} scan ms: median {v[len(v)//2]:.3f} min {v[0]:.3f}", flush=True)
+    if ref is not None:
+        d, p_ = bucket_topk(ix, q, classes, 10)[:2]
+        same = bool(torch.equal(d, ref[0]) and torch.equal(p_, ref[1]))
+        print(f"   lists identical to abl=0: {same}", flush=True)
     if abl == "7" and hasattr(lib, "lmi_debug_counters"):
         cnt = (_lib.C.c_ulonglong * 8)()
         lib.lmi_debug_counters(cnt)
