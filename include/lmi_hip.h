@@ -173,6 +173,23 @@ int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
                const double* thr_round0, double* dists_out, uint32_t* anns_out,
                int32_t* w_out);
 
+/* The same replay on the device (ABI 2): identical results to lmi_replay
+ * (checked bit for bit by tests/test_gpu_replay.py), no host round trip.
+ * classes, lists_d, lists_pos, bucket_size, pos_to_id, thr_round0 (nullable),
+ * dists_out, anns_out are device pointers; status (device int32, caller
+ * zeroes it) is OR-ed with nonzero bits on an internal inconsistency (a list
+ * shorter than its bucket, a position out of range).  k_list >= k_round,
+ * k_round <= 32, k_final <= 64.  Asynchronous on `stream`; workspace of
+ * lmi_replay_device_workspace_bytes bytes. */
+size_t lmi_replay_device_workspace_bytes(int32_t nq, int32_t R, int32_t k_list, int32_t k_round,
+                                         int32_t k_final, int32_t n_buckets);
+int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                      const float* lists_d, const int32_t* lists_pos, int32_t k_round,
+                      int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
+                      const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
+                      const double* thr_round0, double* dists_out, uint32_t* anns_out,
+                      int32_t* status, void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- kernel timing (measurement only) -------------------------------------- */
 /* While enabled, lmi_bucket_topk records a HIP event pair on its stream around
  * its scan kernel (the roofline kernel).  lmi_timing_read waits for the pairs

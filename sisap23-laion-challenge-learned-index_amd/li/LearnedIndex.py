@@ -12,9 +12,10 @@ argument meaning, side effects and return types (LearnedIndex.py:22-195):
 
 Work split: the router (K1), the per-(query, probe) exact bucket top-k (K2)
 and its merge run on the GPU through liblmi_hip.so; the reference's
-threshold/grouping/padding procedure is replayed on the host in C++
-(lmi_replay) from the k-lists, which reproduces its output exactly on tie-free
-inputs (tests/test_oracle_golden.py, tests/test_gpu_golden.py).
+threshold/grouping/padding procedure is replayed from the k-lists on the GPU
+(lmi_replay_device; the host C++ lmi_replay is its bit-exact twin), which
+reproduces its output exactly on tie-free inputs (tests/test_oracle_golden.py,
+tests/test_gpu_golden.py, tests/test_gpu_replay.py).
 
 The bucket-sorted corpus is built in HBM on first use and cached while the
 same DataFrames and labels are passed again (the reference re-gathers every
@@ -95,18 +96,26 @@ class LearnedIndex(Logger):
         """One bucket per query (LearnedIndex.py:103-195).  `pred_categories`
         is the per-query bucket; object labels come from
         data_navigation['category'] as in the reference's groupby (:143)."""
-        from .index import bucket_topk, replay
+        from .index import bucket_topk, replay_device
         index = self._device_index(data_navigation, data_search,
                                    np.asarray(data_navigation['category']))
-        q = torch.from_numpy(np.ascontiguousarray(queries_search, dtype=np.float32)).to(index.device)
+        dev = index.device
+        q = torch.from_numpy(np.ascontiguousarray(queries_search, dtype=np.float32)).to(dev)
         cls = np.asarray(pred_categories).astype(np.int32).reshape(-1, 1)
-        classes = torch.from_numpy(cls).to(index.device)
+        classes = torch.from_numpy(cls).to(dev)
         d, pos, st = bucket_topk(index, q, classes, k)
         if int(st.item()) & _lib.LMI_STATUS_QUERY_NOT_F16:
             d, pos, _ = bucket_topk(index, q, classes, k, qmode=_lib.LMI_Q_F32)
-        return replay(cls, d.cpu().numpy(), pos.cpu().numpy(), k_round=k, k_final=k,
-                      bucket_size=index.bucket_size, pos_to_id=index.pos_to_id,
-                      use_threshold=False, thr_round0=threshold_dist)
+        thr = None if threshold_dist is None else torch.from_numpy(
+            np.ascontiguousarray(np.asarray(threshold_dist, dtype=np.float64).ravel())).to(dev)
+        dd, aa, rst = replay_device(
+            classes, d, pos, k_round=k, k_final=k,
+            bucket_size=torch.from_numpy(np.ascontiguousarray(index.bucket_size, dtype=np.int64)).to(dev),
+            pos_to_id=torch.from_numpy(np.ascontiguousarray(index.pos_to_id, dtype=np.int64)).to(dev),
+            use_threshold=False, thr_round0=thr)
+        if int(rst.item()):
+            raise RuntimeError(f"search_single: replay status {int(rst.item())}")
+        return dd.cpu().numpy(), aa.cpu().numpy().view(np.uint32)
 
     # ---- build (outside the hot path) -------------------------------------
     def build(self, data, n_categories=100, epochs=100, lr=0.1, model_type='MLP'):

@@ -45,6 +45,8 @@ EXPORTS = (
     "lmi_bucket_topk",
     "lmi_merge_topk",
     "lmi_replay",
+    "lmi_replay_device_workspace_bytes",
+    "lmi_replay_device",
     "lmi_timing_enable",
     "lmi_timing_read",
     "lmi_last_error",
@@ -106,6 +108,9 @@ _SIGNATURES = {
     "lmi_merge_topk": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),
     "lmi_replay": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _I32,
                              _P, _P, _P, _P]),
+    "lmi_replay_device_workspace_bytes": (C.c_size_t, [_I32, _I32, _I32, _I32, _I32, _I32]),
+    "lmi_replay_device": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64,
+                                    _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_timing_enable": (C.c_int, [_I32]),
     "lmi_timing_read": (C.c_int32, [_P, _I32]),
     "lmi_last_error": (C.c_char_p, []),

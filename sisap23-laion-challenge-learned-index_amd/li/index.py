@@ -391,6 +391,40 @@ def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k
     return dists, anns
 
 
+def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch.Tensor, *,
+                  k_round: int, k_final: int, bucket_size: torch.Tensor, pos_to_id: torch.Tensor,
+                  use_threshold: bool, thr_round0: Optional[torch.Tensor] = None, stream=None):
+    """A5 on the device (lmi_replay_device): same results as `replay`, device
+    tensors in and out: (dists f64 [nq, w], anns uint32-as-int32 [nq, w], status)."""
+    lib = _lib.load()
+    dev = lists_d.device
+    classes = _as_torch(classes, dev, torch.int32)
+    if classes.dim() == 1:
+        classes = classes[:, None].contiguous()
+    nq, R = classes.shape
+    lists_d = _as_torch(lists_d, dev, torch.float32).reshape(nq, R, -1).contiguous()
+    lists_pos = _as_torch(lists_pos, dev, torch.int32).reshape(nq, R, -1).contiguous()
+    k_list = lists_d.shape[2]
+    w = k_round if R == 1 else k_final
+    dists = torch.empty((nq, w), dtype=torch.float64, device=dev)
+    anns = torch.empty((nq, w), dtype=torch.int32, device=dev)  # uint32 bits
+    status = torch.zeros((1,), dtype=torch.int32, device=dev)
+    n_b = int(bucket_size.numel())
+    need = lib.lmi_replay_device_workspace_bytes(nq, R, k_list, k_round, k_final, n_b)
+    ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
+    thr = None
+    if thr_round0 is not None:
+        thr = _as_torch(thr_round0, dev, torch.float64).reshape(-1)
+        if thr.numel() != nq:
+            raise ValueError("threshold_dist must have one value per query")
+    s = stream if stream is not None else _lib.stream_handle(dev)
+    check("lmi_replay_device", lib.lmi_replay_device(
+        ptr(classes), nq, R, k_list, ptr(lists_d), ptr(lists_pos), k_round, k_final,
+        ptr(bucket_size), n_b, ptr(pos_to_id), int(pos_to_id.numel()), int(bool(use_threshold)),
+        ptr(thr), ptr(dists), ptr(anns), ptr(status), ptr(ws), ws.numel(), s))
+    return dists, anns, status
+
+
 class Searcher:
     """Runs the whole hot path for one shard set (one process per GPU).
 
@@ -420,61 +454,99 @@ class Searcher:
             d, pos = gather_merge(d, pos, k_list, self.group)
         return classes, d, pos, status
 
+    def _device_tables(self):
+        """bucket sizes and position -> id map in HBM for the device replay."""
+        t = getattr(self, "_dev_tables", None)
+        if t is None:
+            dev = self.index.device
+            t = (torch.from_numpy(np.ascontiguousarray(self.index.bucket_size, dtype=np.int64)).to(dev),
+                 torch.from_numpy(np.ascontiguousarray(self.index.pos_to_id, dtype=np.int64)).to(dev))
+            self._dev_tables = t
+        return t
+
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
                use_threshold: bool = True, classes: Optional[torch.Tensor] = None,
-               timings: Optional[dict] = None):
+               timings: Optional[dict] = None, replay_on: str = "device"):
         """Whole hot path for one batch -> (dists f64 [nq, w], anns u32 [nq, w]).
 
-        `timings` (measurement only) receives per-stage wall times in ms; the
-        stages are then separated by stream synchronisations."""
+        replay_on="device" (default) runs the reference's round merge on the GPU
+        (lmi_replay_device) and copies back only the result; "host" copies the
+        lists back and runs lmi_replay (same results, the checker of the device
+        replay).  `timings` (measurement only) receives per-stage wall times in
+        ms; the stages are then separated by stream synchronisations."""
         import time
+        if replay_on not in ("device", "host"):
+            raise ValueError("replay_on must be 'device' or 'host'")
         k_list = k_round
         dev = self.index.device
         sync = (lambda: torch.cuda.current_stream(dev).synchronize()) if timings is not None else None
-        t0 = time.perf_counter()
-        if classes is None:
-            classes, _ = self.router.topr(q_nav, R)
-        if sync:
-            sync()
-            t1 = time.perf_counter()
-            timings["router"] = timings.get("router", 0.0) + (t1 - t0) * 1e3
-            t0 = t1
-        d, pos, status = bucket_topk(self.index, q_search, classes, k_list)
-        if self.index.world > 1:
-            from .dist import gather_merge
-            d, pos = gather_merge(d, pos, k_list, self.group)
-        if sync:
-            sync()
-            t1 = time.perf_counter()
-            timings["scan"] = timings.get("scan", 0.0) + (t1 - t0) * 1e3
-            t0 = t1
-        nq = classes.shape[0]
-        h_cls = self._host("cls", (nq, R), torch.int32)
-        h_d = self._host("d", tuple(d.shape), torch.float32)
-        h_pos = self._host("pos", tuple(pos.shape), torch.int32)
-        h_st = self._host("st", (1,), torch.int32)
-        h_cls.copy_(classes, non_blocking=True)
-        h_d.copy_(d, non_blocking=True)
-        h_pos.copy_(pos, non_blocking=True)
-        h_st.copy_(status, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        if timings is not None:
-            t1 = time.perf_counter()
-            timings["d2h"] = timings.get("d2h", 0.0) + (t1 - t0) * 1e3
-            t0 = t1
-        if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL:
-            raise RuntimeError("lmi_bucket_topk: a list held an out-of-range row (internal error)")
-        if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
-            # queries are not fp16-exact: redo the scan with exact fp32 MFMA
-            d, pos, _ = bucket_topk(self.index, q_search, classes, k_list, qmode=_lib.LMI_Q_F32)
+
+        def lap(name, t0):
+            if sync:
+                sync()
+                t1 = time.perf_counter()
+                timings[name] = timings.get(name, 0.0) + (t1 - t0) * 1e3
+                return t1
+            return t0
+
+        def scan(qmode=None):
+            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode)
             if self.index.world > 1:
                 from .dist import gather_merge
                 d, pos = gather_merge(d, pos, k_list, self.group)
+            return d, pos, status
+
+        t0 = time.perf_counter()
+        if classes is None:
+            classes, _ = self.router.topr(q_nav, R)
+        t0 = lap("router", t0)
+        d, pos, status = scan()
+        t0 = lap("scan", t0)
+        nq = classes.shape[0]
+        h_st = self._host("st", (2,), torch.int32)
+        if replay_on == "device":
+            bsz, p2id = self._device_tables()
+
+            def run_replay(d, pos):
+                return replay_device(classes, d, pos, k_round=k_round, k_final=k, bucket_size=bsz,
+                                     pos_to_id=p2id, use_threshold=use_threshold)
+
+            rd, ra, rst = run_replay(d, pos)
+            t0 = lap("replay", t0)
+            h_d = self._host("rd", tuple(rd.shape), torch.float64)
+            h_a = self._host("ra", tuple(ra.shape), torch.int32)
+            h_d.copy_(rd, non_blocking=True)
+            h_a.copy_(ra, non_blocking=True)
+            h_st[0:1].copy_(status, non_blocking=True)
+            h_st[1:2].copy_(rst, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            t0 = lap("d2h", t0)
+            if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL or int(h_st[1]):
+                raise RuntimeError(f"search: internal status {int(h_st[0])}/{int(h_st[1])}")
+            if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
+                # queries are not fp16-exact: redo the scan with exact fp32 MFMA
+                d, pos, _ = scan(qmode=_lib.LMI_Q_F32)
+                rd, ra, rst = run_replay(d, pos)
+                h_d.copy_(rd)
+                h_a.copy_(ra)
+            return h_d.numpy().copy(), h_a.numpy().view(np.uint32).copy()
+        h_cls = self._host("cls", (nq, R), torch.int32)
+        h_d = self._host("d", tuple(d.shape), torch.float32)
+        h_pos = self._host("pos", tuple(pos.shape), torch.int32)
+        h_cls.copy_(classes, non_blocking=True)
+        h_d.copy_(d, non_blocking=True)
+        h_pos.copy_(pos, non_blocking=True)
+        h_st[0:1].copy_(status, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        t0 = lap("d2h", t0)
+        if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL:
+            raise RuntimeError("lmi_bucket_topk: a list held an out-of-range row (internal error)")
+        if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
+            d, pos, _ = scan(qmode=_lib.LMI_Q_F32)
             h_d.copy_(d)
             h_pos.copy_(pos)
         out = replay(h_cls.numpy(), h_d.numpy(), h_pos.numpy(), k_round=k_round, k_final=k,
                      bucket_size=self.index.bucket_size, pos_to_id=self.index.pos_to_id,
                      use_threshold=use_threshold)
-        if timings is not None:
-            timings["replay"] = timings.get("replay", 0.0) + (time.perf_counter() - t0) * 1e3
+        lap("replay", t0) if sync else None
         return out
