@@ -59,57 +59,9 @@ __device__ inline int block_min_i(int v, int* sh) {
     return t;
 }
 
-// counts[r][c] = #{q : classes[q, r] == c}
-__global__ __launch_bounds__(kT) void replay_count_kernel(const int32_t* __restrict__ classes,
-                                                          int32_t nq, int32_t R, int32_t C,
-                                                          int32_t* __restrict__ counts) {
-    __shared__ int sh[kT / 64];
-    const int c = blockIdx.x;
-    for (int r = 0; r < R; ++r) {
-        int n = 0;
-        for (int q = threadIdx.x; q < nq; q += kT) n += (classes[(size_t)q * R + r] == c) ? 1 : 0;
-        n = block_sum_i(n, sh);
-        if (threadIdx.x == 0) counts[r * C + c] = n;
-    }
-}
-
-// groups[r][goff(r, c) + i] = i-th query (ascending) with classes[q, r] == c
-__global__ __launch_bounds__(kT) void replay_group_fill_kernel(const int32_t* __restrict__ classes,
-                                                               int32_t nq, int32_t R, int32_t C,
-                                                               const int32_t* __restrict__ counts,
-                                                               int32_t* __restrict__ goff,
-                                                               int32_t* __restrict__ groups) {
-    __shared__ int sh[kT / 64];
-    __shared__ int wcnt[kT / 64];
-    const int c = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int r = 0; r < R; ++r) {
-        int off = 0;
-        for (int b = tid; b < c; b += kT) off += counts[r * C + b];
-        off = block_sum_i(off, sh);
-        if (tid == 0) {
-            goff[r * (C + 1) + c] = off;
-            if (c == C - 1) goff[r * (C + 1) + C] = off + counts[r * C + c];
-        }
-        int run = 0;
-        for (int base = 0; base < nq; base += kT) {
-            const int q = base + tid;
-            const bool pred = (q < nq) && (classes[(size_t)q * R + r] == c);
-            const uint64_t m = __ballot(pred);
-            const int rank = __popcll(m & ((1ull << lane) - 1ull));
-            __syncthreads();
-            if (lane == 0) wcnt[w] = __popcll(m);
-            __syncthreads();
-            int wpre = 0, tot = 0;
-            for (int i = 0; i < kT / 64; ++i) {
-                wpre += (i < w) ? wcnt[i] : 0;
-                tot += wcnt[i];
-            }
-            if (pred) groups[(size_t)r * nq + off + run + wpre + rank] = q;
-            run += tot;
-        }
-        __syncthreads();
-    }
+__device__ inline int wave_min_i(int v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
+    return v;
 }
 
 struct RoundArgs {
@@ -118,13 +70,13 @@ struct RoundArgs {
     const float* lists_d;    // [nq][R][kl]
     const int32_t* lists_p;  // [nq][R][kl]
     const int64_t* bucket_size;
-    const int32_t* groups;   // [R][nq]
-    const int32_t* goff;     // [R][C+1]
+    int32_t* groups;         // [nq] this round's groups, category c at [g0(c), g1(c))
     int32_t thresholded;
     const double* thr;       // [nq]
     double* dr_d;            // [nq][kr]
     int32_t* dr_p;
-    int32_t* uraw;           // [nq * kl] scratch (positions of relevant entries)
+    int32_t* uraw;           // [nq * kl] scratch (positions of relevant entries),
+                             // category c at [g0 * kl, g1 * kl)
     int32_t* status;
 };
 
@@ -173,54 +125,143 @@ __device__ void stable_argsort_dev(const double* row, int n, int* idx) {
     }
 }
 
+constexpr int kUCap = 8192;  // relevant positions of a group held in LDS
+
 __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
     __shared__ int sh[kT / 64];
     __shared__ int32_t S[2 * kMaxKr + 16];  // smallest members of U, ascending
     __shared__ Ent qrow[kMaxKr];            // the quirk row of the group
+    __shared__ int32_t Ul[kUCap];
+    __shared__ int32_t Sw[kT / 64][2 * kMaxKr];  // per wave: smallest members of its share
+    __shared__ int nsw[kT / 64 + 1];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
-    const int g0 = a.goff[a.r * (a.C + 1) + c], g1 = a.goff[a.r * (a.C + 1) + c + 1];
-    if (g0 == g1 || a.bucket_size[c] <= 0) return;  // groupby visits non-empty categories only
-    const int32_t* G = a.groups + (size_t)a.r * a.nq;
+    if (a.bucket_size[c] <= 0) return;  // groupby visits non-empty categories only
+    // the group: queries with classes[q, r] == c in ascending q, placed at
+    // [g0, g1) with g0 = #{q : classes[q, r] < c} (disjoint across categories)
+    int g0, g1;
+    {
+        // every wave takes a contiguous segment of the queries, read
+        // coalesced, matches ranked by ballot
+        __shared__ int wc[2][kT / 64];
+        const int lane = tid & 63, w = tid >> 6;
+        const int seg = ((a.nq + kT / 64 - 1) / (kT / 64) + 63) & ~63;
+        const int qa = min(a.nq, w * seg), qb = min(a.nq, qa + seg);
+        constexpr int kU = 8;  // loads in flight per lane (each pass is latency-bound)
+        int n_eq = 0, n_lt = 0;
+        for (int q0 = qa; q0 < qb; q0 += kU * 64) {
+            int v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int q = q0 + 64 * u + lane;
+                v[u] = q < qb ? a.classes[(size_t)q * a.R + a.r] : INT32_MAX;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                n_eq += __popcll(__ballot(v[u] == c));
+                n_lt += __popcll(__ballot(v[u] < c));
+            }
+        }
+        if (lane == 0) {
+            wc[0][w] = n_eq;
+            wc[1][w] = n_lt;
+        }
+        __syncthreads();
+        int before = 0, n_g = 0, lt = 0;
+        for (int i = 0; i < kT / 64; ++i) {
+            before += (i < w) ? wc[0][i] : 0;
+            n_g += wc[0][i];
+            lt += wc[1][i];
+        }
+        if (n_g == 0) return;
+        g0 = lt;
+        g1 = lt + n_g;
+        int o = g0 + before;
+        const uint64_t lanes_lt = (1ull << lane) - 1ull;
+        for (int q0 = qa; q0 < qb; q0 += kU * 64) {
+            int v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int q = q0 + 64 * u + lane;
+                v[u] = q < qb ? a.classes[(size_t)q * a.R + a.r] : INT32_MAX;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t m = __ballot(v[u] == c);
+                if (v[u] == c) a.groups[o + __popcll(m & lanes_lt)] = q0 + 64 * u + lane;
+                o += __popcll(m);
+            }
+        }
+        __syncthreads();
+    }
+    const int32_t* G = a.groups;
     const int kr = a.kr;
     const int kl_use = min(kr, a.kl);
     if (a.thresholded) {
         // B_q = leading list entries with d < thr[q] (utils.py:22-23, strict);
         // U = unique positions over the group; only its smallest members matter
+        const int nU = (g1 - g0) * kl_use;
+        int32_t* U = nU <= kUCap ? Ul : a.uraw + (size_t)g0 * kl_use;
         int nb_tot = 0;
         for (int gi = g0 + tid; gi < g1; gi += kT) {
             const int q = G[gi];
+            int32_t* u = U + (size_t)(gi - g0) * kl_use;
             int n = 0;
             for (int j = 0; j < kl_use; ++j) {
                 double d;
                 int32_t pos;
                 list_at(a, q, j, d, pos);
                 if (pos < 0 || !(d < a.thr[q])) break;
-                a.uraw[(size_t)q * a.kl + j] = pos;
+                u[j] = pos;
                 ++n;
             }
-            for (int j = n; j < a.kl; ++j) a.uraw[(size_t)q * a.kl + j] = INT32_MAX;
+            for (int j = n; j < kl_use; ++j) u[j] = INT32_MAX;
             nb_tot += n;
         }
-        nb_tot = block_sum_i(nb_tot, sh);
+        nb_tot = block_sum_i(nb_tot, sh);  // (its barriers publish U)
         if (nb_tot == 0) return;  // LearnedIndex.py:157-159
         const int want = kr + kl_use;
-        int ns = 0, prev = -1;
-        for (; ns < want; ++ns) {
+        // the smallest `want` members of U: each wave finds those of its
+        // share (every 4th 64-entry run), then wave 0 merges the four lists
+        // (a global member among the smallest `want` is among its share's)
+        const int lane = tid & 63, wv = tid >> 6;
+        int prev = -1, cnt = 0;
+        for (; cnt < want; ++cnt) {
             int m = INT32_MAX;
-            for (int gi = g0 + tid; gi < g1; gi += kT) {
-                const int q = G[gi];
-                for (int j = 0; j < kl_use; ++j) {
-                    const int32_t p = a.uraw[(size_t)q * a.kl + j];
-                    if (p == INT32_MAX) break;
-                    if (p > prev && p < m) m = p;
-                }
+            for (int e = wv * 64 + lane; e < nU; e += kT) {
+                const int32_t p = U[e];
+                if (p > prev && p < m) m = p;
             }
-            m = block_min_i(m, sh);
+            m = wave_min_i(m);
             if (m == INT32_MAX) break;
-            if (tid == 0) S[ns] = m;
+            if (lane == 0) Sw[wv][cnt] = m;
             prev = m;
         }
+        if (lane == 0) nsw[wv] = cnt;
+        __syncthreads();
+        if (wv == 0) {
+            int v[4 * (2 * kMaxKr) / 64];
+            constexpr int NV = 4 * (2 * kMaxKr) / 64;
+#pragma unroll
+            for (int t = 0; t < NV; ++t) {
+                const int e = lane + 64 * t, w = e / (2 * kMaxKr), i = e % (2 * kMaxKr);
+                v[t] = (i < nsw[w]) ? Sw[w][i] : INT32_MAX;
+            }
+            int pv = -1, n = 0;
+            for (; n < want; ++n) {
+                int m = INT32_MAX;
+#pragma unroll
+                for (int t = 0; t < NV; ++t)
+                    if (v[t] > pv && v[t] < m) m = v[t];
+                m = wave_min_i(m);
+                if (m == INT32_MAX) break;
+                if (lane == 0) S[n] = m;
+                pv = m;
+            }
+            if (lane == 0) nsw[4] = n;
+        }
+        __syncthreads();
+        const int ns = nsw[4];
         __syncthreads();
         if (ns >= kr) {
             // normal case: B_q then the smallest members of U not in B_q
@@ -354,37 +395,42 @@ __global__ __launch_bounds__(kT) void replay_thr_kernel(int32_t nq, int32_t kr, 
     }
 }
 
+// LearnedIndex.py:82-97: the first wn of argsort(hstack(F, D_r), kind='stable'),
+// one thread per element of the concatenation: its stable rank is
+// #{i : d_i < d_j} + #{i < j : d_i == d_j}.  F is read from one buffer and the
+// merged row written to the other (ping-pong across rounds).
 __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr, int32_t fs,
                                                           int32_t wF, int32_t wn, int32_t first,
-                                                          double* __restrict__ Fd,
-                                                          int32_t* __restrict__ Fp,
+                                                          const double* __restrict__ Fd,
+                                                          const int32_t* __restrict__ Fp,
+                                                          double* __restrict__ Fd_out,
+                                                          int32_t* __restrict__ Fp_out,
                                                           const double* __restrict__ dr_d,
                                                           const int32_t* __restrict__ dr_p) {
-    const int q = blockIdx.x * kT + threadIdx.x;
-    if (q >= nq) return;
+    const int n = first ? kr : wF + kr;
+    const int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (t >= (int64_t)nq * n) return;
+    const int q = (int)(t / n), j = (int)(t - (int64_t)q * n);
+    const double* fd = Fd + (size_t)q * fs;
+    const double* dd = dr_d + (size_t)q * kr;
     if (first) {
-        for (int j = 0; j < kr; ++j) {
-            Fd[(size_t)q * fs + j] = dr_d[(size_t)q * kr + j];
-            Fp[(size_t)q * fs + j] = dr_p[(size_t)q * kr + j];
-        }
+        Fd_out[(size_t)q * fs + j] = dd[j];
+        Fp_out[(size_t)q * fs + j] = dr_p[(size_t)q * kr + j];
         return;
     }
-    // stable sort of hstack(F, D_r) by distance (argsort(kind='stable')), first wn
-    Ent cat[kMaxW + kMaxKr];
-    int len = 0;
-    for (int j = 0; j < wF + kr; ++j) {
-        const Ent e = j < wF ? Ent{Fd[(size_t)q * fs + j], Fp[(size_t)q * fs + j]}
-                             : Ent{dr_d[(size_t)q * kr + (j - wF)], dr_p[(size_t)q * kr + (j - wF)]};
-        int i = len++;
-        while (i > 0 && cat[i - 1].d > e.d) {
-            cat[i] = cat[i - 1];
-            --i;
-        }
-        cat[i] = e;
+    const double dj = j < wF ? fd[j] : dd[j - wF];
+    int rank = 0;
+    for (int i = 0; i < wF; ++i) {
+        const double di = fd[i];
+        rank += (di < dj || (di == dj && i < j)) ? 1 : 0;
     }
-    for (int j = 0; j < wn; ++j) {
-        Fd[(size_t)q * fs + j] = cat[j].d;
-        Fp[(size_t)q * fs + j] = cat[j].pos;
+    for (int i = 0; i < kr; ++i) {
+        const double di = dd[i];
+        rank += (di < dj || (di == dj && wF + i < j)) ? 1 : 0;
+    }
+    if (rank < wn) {
+        Fd_out[(size_t)q * fs + rank] = dj;
+        Fp_out[(size_t)q * fs + rank] = j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF];
     }
 }
 
@@ -412,7 +458,7 @@ __global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, i
 }
 
 struct ReplayWs {
-    size_t counts, goff, groups, Fd, Fp, drd, drp, thr, uraw, total;
+    size_t groups, Fd[2], Fp[2], drd, drp, thr, uraw, total;
 };
 
 ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
@@ -424,11 +470,11 @@ ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
         return at;
     };
     const int fs = std::max(kr, w);
-    s.counts = take((size_t)R * C * 4);
-    s.goff = take((size_t)R * (C + 1) * 4);
-    s.groups = take((size_t)R * nq * 4);
-    s.Fd = take((size_t)nq * fs * 8);
-    s.Fp = take((size_t)nq * fs * 4);
+    s.groups = take((size_t)nq * 4);
+    for (int b = 0; b < 2; ++b) {
+        s.Fd[b] = take((size_t)nq * fs * 8);
+        s.Fp[b] = take((size_t)nq * fs * 4);
+    }
     s.drd = take((size_t)nq * kr * 8);
     s.drp = take((size_t)nq * kr * 4);
     s.thr = take((size_t)nq * 8);
@@ -481,19 +527,13 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
     auto* ws = reinterpret_cast<unsigned char*>(workspace);
     const int C = n_buckets;
     const int fs = std::max(k_round, w);
-    int32_t* counts = (int32_t*)(ws + s.counts);
-    int32_t* goff = (int32_t*)(ws + s.goff);
     int32_t* groups = (int32_t*)(ws + s.groups);
-    double* Fd = (double*)(ws + s.Fd);
-    int32_t* Fp = (int32_t*)(ws + s.Fp);
     const dim3 qgrid((unsigned)((nq + kT - 1) / kT));
-    hipLaunchKernelGGL(replay_count_kernel, dim3(C), dim3(kT), 0, st, classes, nq, R, C, counts);
-    LMI_LAUNCH_CHECK("replay_count_kernel");
-    hipLaunchKernelGGL(replay_group_fill_kernel, dim3(C), dim3(kT), 0, st, classes, nq, R, C, counts,
-                       goff, groups);
-    LMI_LAUNCH_CHECK("replay_group_fill_kernel");
+    int cur = 0;  // F lives in buffer cur; the merge writes the other one
     int wF = 0;
     for (int r = 0; r < R; ++r) {
+        double* Fd = (double*)(ws + s.Fd[cur]);
+        int32_t* Fp = (int32_t*)(ws + s.Fp[cur]);
         const bool thresholded = ((r > 0) && use_threshold) || (r == 0 && thr_round0);
         const int mode = (r == 0 && thr_round0) ? 1 : (thresholded ? 2 : 0);
         hipLaunchKernelGGL(replay_thr_kernel, qgrid, dim3(kT), 0, st, nq, k_round, fs, wF, mode, Fd,
@@ -512,7 +552,6 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
         a.lists_p = lists_pos;
         a.bucket_size = bucket_size;
         a.groups = groups;
-        a.goff = goff;
         a.thresholded = thresholded ? 1 : 0;
         a.thr = (const double*)(ws + s.thr);
         a.dr_d = (double*)(ws + s.drd);
@@ -522,12 +561,18 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
         hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kT), 0, st, a);
         LMI_LAUNCH_CHECK("replay_group_kernel");
         const int wn = (r == 0) ? k_round : std::min(k_final, wF + k_round);
-        hipLaunchKernelGGL(replay_merge_kernel, qgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
-                           r == 0 ? 1 : 0, Fd, Fp, (const double*)(ws + s.drd),
+        const int n = (r == 0) ? k_round : wF + k_round;
+        const dim3 mgrid((unsigned)(((int64_t)nq * n + kT - 1) / kT));
+        hipLaunchKernelGGL(replay_merge_kernel, mgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
+                           r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
+                           (int32_t*)(ws + s.Fp[cur ^ 1]), (const double*)(ws + s.drd),
                            (const int32_t*)(ws + s.drp));
         LMI_LAUNCH_CHECK("replay_merge_kernel");
+        cur ^= 1;
         wF = wn;
     }
+    const double* Fd = (const double*)(ws + s.Fd[cur]);
+    const int32_t* Fp = (const int32_t*)(ws + s.Fp[cur]);
     hipLaunchKernelGGL(replay_out_kernel, qgrid, dim3(kT), 0, st, nq, w, fs, Fd, Fp, pos_to_id, n_total,
                        dists_out, anns_out, status);
     LMI_LAUNCH_CHECK("replay_out_kernel");

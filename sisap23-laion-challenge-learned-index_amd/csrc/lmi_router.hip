@@ -6,15 +6,16 @@
 // object labels at LearnedIndex.py:240).
 //
 // One workgroup (4 waves) owns a tile of TQ query rows.  The activations of
-// the tile live in LDS (two ping-pong buffers, one row per query, padded to an
-// odd-ish stride so per-lane row reads are conflict-free); every lane owns one
-// query and a group of output neurons; weight rows are read straight from
-// global memory (they are tiny: 112 KB for 'MLP', 294 KB for 'MLP-5', and are
-// shared by all workgroups through L2).  Each output is the fp32 FMA chain
-// b[o] + sum_i h[i] * W[o][i] in ascending i, i.e. torch's Linear up to
-// summation order.  The last layer's logits stay in LDS and are reduced to the
-// top-R classes (descending logit, ties to the lower class index) and their
-// softmax probabilities, or to the argmax.
+// the tile live in LDS (two ping-pong buffers, one row per query, rows 16-B
+// aligned at a pitch of 4 mod 64 floats so per-lane float4 reads are
+// conflict-free); every lane owns one query and kOB output neurons.  A layer is
+// computed in passes of NG * kOB outputs whose weight rows are first staged in
+// LDS (one coalesced copy per pass, shared by the whole tile) and then read as
+// broadcasts.  Each output is the fp32 FMA chain b[o] + sum_i h[i] * W[o][i] in
+// ascending i, i.e. torch's Linear up to summation order.  The last layer's
+// logits stay in LDS and are reduced to the top-R classes (descending logit,
+// ties to the lower class index) and their softmax probabilities, or to the
+// argmax.
 #include "lmi_common.hpp"
 
 namespace lmi {
@@ -28,17 +29,31 @@ struct RouterArgs {
     const float* W[LMI_MAX_LAYERS];
     const float* b[LMI_MAX_LAYERS];
     int32_t stride;  // LDS row stride in floats
+    int32_t w_vec4;  // every weight matrix 16-B aligned with din % 4 == 0 rows
+    int32_t wpitch;  // LDS pitch of a staged weight row, floats
     int32_t R, mode;
     int32_t* classes;
     float* probs;
 };
 
 constexpr int kThreads = 256;
-constexpr int kOB = 4;  // outputs per lane per pass (register blocking)
+constexpr int kOB = 8;  // outputs per lane per pass (register blocking)
 
 // (logit a, class ia) ranks before (logit b, class ib)?
 __device__ inline bool better(float a, int ia, float b, int ib) {
     return a > b || (a == b && ia < ib);
+}
+
+// wave-wide best (logit, class) under `better`; every lane gets the result
+__device__ inline void wave_best(float& v, int& i) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const float v2 = __shfl_xor(v, o);
+        const int i2 = __shfl_xor(i, o);
+        if (better(v2, i2, v, i)) {
+            v = v2;
+            i = i2;
+        }
+    }
 }
 
 template <int TQ>
@@ -47,8 +62,9 @@ __global__ __launch_bounds__(kThreads) void router_kernel(RouterArgs a) {
     constexpr int G = 64 / TQ;    // query groups per wave
     constexpr int NG = 4 * G;     // output groups per workgroup
     const int S = a.stride;
-    float* H[2] = {smem, smem + TQ * S};
-    float* stat = smem + 2 * TQ * S;  // [TQ][2]: max, sum
+    const int WP = a.wpitch;                    // staged weight row pitch (floats)
+    float* wt = smem + 2 * TQ * S;              // [NG * kOB][WP] weights of one pass
+    float* stat = wt + NG * kOB * WP;           // [TQ][2]: max, sum
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -59,10 +75,22 @@ __global__ __launch_bounds__(kThreads) void router_kernel(RouterArgs a) {
 
     // Stage the query tile.
     const int din0 = a.dims[0];
-    for (int e = tid; e < TQ * din0; e += kThreads) {
-        const int r = e / din0, c = e - r * din0;
-        const int q = q0 + r;
-        H[0][r * S + c] = (q < a.nq) ? a.x[(size_t)q * a.ldx + c] : 0.0f;
+    {
+        constexpr int kU = 8;
+        for (int e0 = tid; e0 < TQ * din0; e0 += kU * kThreads) {
+            float v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int e = e0 + u * kThreads;
+                const int r = e / din0, c = e - r * din0;
+                v[u] = (e < TQ * din0 && q0 + r < a.nq) ? a.x[(size_t)(q0 + r) * a.ldx + c] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int e = e0 + u * kThreads;
+                if (e < TQ * din0) smem[(e / din0) * S + e % din0] = v[u];
+            }
+        }
     }
     __syncthreads();
 
@@ -71,26 +99,76 @@ __global__ __launch_bounds__(kThreads) void router_kernel(RouterArgs a) {
         const int din = a.dims[l], dout = a.dims[l + 1];
         const float* __restrict__ W = a.W[l];
         const float* __restrict__ bias = a.b[l];
-        const float* hin = H[cur] + ql * S;
-        float* hout = H[cur ^ 1] + ql * S;
+        // (LDS pointers computed from smem directly: through an array of
+        // pointers the compiler loses the address space and emits flat loads)
+        const float* hin = smem + cur * TQ * S + ql * S;
+        float* hout = smem + (cur ^ 1) * TQ * S + ql * S;
         const bool relu = (l + 1 < a.n_layers);
-        for (int o0 = grp * kOB; o0 < dout; o0 += NG * kOB) {
+        const int din4 = din & ~3;
+        for (int ob = 0; ob < dout; ob += NG * kOB) {
+            // stage rows ob .. ob + NG*kOB - 1 (clamped) of W: contiguous in HBM
+            const int nrow = min(NG * kOB, dout - ob);
+            __syncthreads();  // the previous pass's readers are done with wt
+            if (a.w_vec4) {
+                // all of a thread's loads in flight before its LDS stores (a
+                // load-store loop would pay one L2 round trip per element)
+                constexpr int kU = 8;
+                const int n4 = din >> 2, tot = nrow * n4;
+                const float4* src = reinterpret_cast<const float4*>(W + (size_t)ob * din);
+                for (int e0 = tid; e0 < tot; e0 += kU * kThreads) {
+                    float4 v[kU];
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) {
+                        const int e = e0 + u * kThreads;
+                        if (e < tot) v[u] = src[e];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kU; ++u) {
+                        const int e = e0 + u * kThreads;
+                        if (e < tot) {
+                            const int r = e / n4, c4 = e - r * n4;
+                            *reinterpret_cast<float4*>(wt + r * WP + 4 * c4) = v[u];
+                        }
+                    }
+                }
+            } else {
+                for (int e = tid; e < nrow * din; e += kThreads) {
+                    const int r = e / din, c = e - r * din;
+                    wt[r * WP + c] = W[(size_t)ob * din + e];
+                }
+            }
+            __syncthreads();
             float acc[kOB];
             const float* wr[kOB];
 #pragma unroll
             for (int j = 0; j < kOB; ++j) {
-                const int o = min(o0 + j, dout - 1);
-                acc[j] = bias[o];
-                wr[j] = W + (size_t)o * din;
+                const int r = min(grp * kOB + j, nrow - 1);
+                acc[j] = bias[ob + r];
+                wr[j] = wt + r * WP;
             }
-            for (int i = 0; i < din; ++i) {
+            // ascending i, one fmaf per term: the same chain as a scalar loop
+            int i = 0;
+#pragma unroll 2
+            for (; i < din4; i += 4) {
+                const float4 h4 = *reinterpret_cast<const float4*>(hin + i);
+#pragma unroll
+                for (int j = 0; j < kOB; ++j) {
+                    const float4 w4 = *reinterpret_cast<const float4*>(wr[j] + i);
+                    acc[j] = fmaf(h4.x, w4.x, acc[j]);
+                    acc[j] = fmaf(h4.y, w4.y, acc[j]);
+                    acc[j] = fmaf(h4.z, w4.z, acc[j]);
+                    acc[j] = fmaf(h4.w, w4.w, acc[j]);
+                }
+            }
+            for (; i < din; ++i) {
                 const float h = hin[i];
 #pragma unroll
                 for (int j = 0; j < kOB; ++j) acc[j] = fmaf(h, wr[j][i], acc[j]);
             }
 #pragma unroll
             for (int j = 0; j < kOB; ++j) {
-                if (o0 + j < dout) hout[o0 + j] = relu ? fmaxf(acc[j], 0.0f) : acc[j];
+                const int o = ob + grp * kOB + j;
+                if (o < dout) hout[o] = relu ? fmaxf(acc[j], 0.0f) : acc[j];
             }
         }
         __syncthreads();
@@ -98,52 +176,66 @@ __global__ __launch_bounds__(kThreads) void router_kernel(RouterArgs a) {
     }
 
     const int C = a.dims[a.n_layers];
-    const float* logit = H[cur];
+    const float* logit = smem + cur * TQ * S;
 
+    // One wave per query from here on (the logits of a query across the 64
+    // lanes): argmax, softmax statistics and the top-R picks are wave
+    // reductions.  The picks compare logits exactly, so they do not depend on
+    // the reduction order; only the softmax sum's rounding does.
+    constexpr int NW = kThreads / 64;
     if (a.mode == LMI_ROUTER_ARGMAX) {
-        if (tid < TQ && q0 + tid < a.nq) {
-            const float* lr = logit + tid * S;
-            float best = lr[0];
-            int bi = 0;
-            for (int i = 1; i < C; ++i)
-                if (lr[i] > best) { best = lr[i]; bi = i; }
-            a.classes[q0 + tid] = bi;
+        for (int qq = wave; qq < TQ && q0 + qq < a.nq; qq += NW) {
+            const float* lr = logit + qq * S;
+            float bv = -__builtin_inff();
+            int bi = INT32_MAX;
+            for (int i = lane; i < C; i += 64) {
+                const float v = lr[i];
+                if (better(v, i, bv, bi)) { bv = v; bi = i; }
+            }
+            wave_best(bv, bi);
+            if (lane == 0) a.classes[q0 + qq] = bi;
         }
         return;
     }
 
     // softmax statistics (torch: exp(x - max) / sum)
-    if (tid < TQ) {
-        const float* lr = logit + tid * S;
-        float m = lr[0];
-        for (int i = 1; i < C; ++i) m = fmaxf(m, lr[i]);
-        float s = 0.0f;
-        for (int i = 0; i < C; ++i) s += expf(lr[i] - m);
-        stat[2 * tid] = m;
-        stat[2 * tid + 1] = s;
+    for (int qq = wave; qq < TQ; qq += NW) {
+        const float* lr = logit + qq * S;
+        float m = -__builtin_inff();
+        for (int i = lane; i < C; i += 64) m = fmaxf(m, lr[i]);
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        float sum = 0.0f;
+        for (int i = lane; i < C; i += 64) sum += expf(lr[i] - m);
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == 0) {
+            stat[2 * qq] = m;
+            stat[2 * qq + 1] = sum;
+        }
     }
     __syncthreads();
 
     const int R = a.R;
     if (R <= 8) {
-        // R selection passes, one lane per query.
-        if (tid < TQ && q0 + tid < a.nq) {
-            const float* lr = logit + tid * S;
-            const float m = stat[2 * tid], s = stat[2 * tid + 1];
+        // R selection rounds per query, each a wave-wide best over the
+        // classes strictly after the previous pick in (desc logit, asc index)
+        for (int qq = wave; qq < TQ && q0 + qq < a.nq; qq += NW) {
+            const float* lr = logit + qq * S;
+            const float m = stat[2 * qq], sum = stat[2 * qq + 1];
             float pl = __builtin_inff();
             int pi = -1;
             for (int r = 0; r < R; ++r) {
                 float bl = -__builtin_inff();
-                int bi = -1;
-                for (int i = 0; i < C; ++i) {
+                int bi = INT32_MAX;
+                for (int i = lane; i < C; i += 64) {
                     const float v = lr[i];
-                    // strictly after the previous pick in (desc logit, asc index) order
-                    const bool after = better(pl, pi, v, i);
-                    if (after && (bi < 0 || better(v, i, bl, bi))) { bl = v; bi = i; }
+                    if (better(pl, pi, v, i) && better(v, i, bl, bi)) { bl = v; bi = i; }
                 }
-                const size_t o = (size_t)(q0 + tid) * R + r;
-                a.classes[o] = bi;
-                if (a.probs) a.probs[o] = expf(bl - m) / s;
+                wave_best(bl, bi);
+                if (lane == 0) {
+                    const size_t o = (size_t)(q0 + qq) * R + r;
+                    a.classes[o] = bi;
+                    if (a.probs) a.probs[o] = expf(bl - m) / sum;
+                }
                 pl = bl;
                 pi = bi;
             }
@@ -214,20 +306,25 @@ extern "C" int lmi_router(const float* x, int32_t nq, int32_t ldx, const lmi_mlp
         a.W[l] = mlp->W[l];
         a.b[l] = mlp->b[l];
     }
-    // stride = maxdim rounded up to a multiple of 4, plus 1: odd => lanes that
-    // read the same column of different rows hit different banks.
-    a.stride = ((maxdim + 3) / 4) * 4 + 1;
+    // stride = maxdim rounded up to a multiple of 64, plus 4: 16-B aligned
+    // rows whose float4 reads by 16 lanes cover all 64 banks once
+    a.stride = ((maxdim + 63) / 64) * 64 + 4;
+    a.w_vec4 = 1;
+    for (int l = 0; l < mlp->n_layers; ++l)
+        if ((mlp->dims[l] & 3) || ((uintptr_t)mlp->W[l] & 15)) a.w_vec4 = 0;
     a.R = R;
     a.mode = mode;
     a.classes = classes_out;
     a.probs = probs_out;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    a.wpitch = ((maxdim + 3) / 4) * 4 + 4;  // two rows read together sit 4 banks apart
     const size_t lds_limit = 160 * 1024;
-    for (int tq : {64, 32, 16, 8}) {
-        const size_t lds = (size_t)(2 * tq * a.stride + 2 * tq) * sizeof(float);
+    for (int tq : {32, 16, 8}) {
+        const int ng = 4 * (64 / tq);
+        const size_t lds =
+            (size_t)(2 * tq * a.stride + ng * kOB * a.wpitch + 2 * tq) * sizeof(float);
         if (lds > lds_limit) continue;
         switch (tq) {
-            case 64: return launch_router<64>(a, lds, s);
             case 32: return launch_router<32>(a, lds, s);
             case 16: return launch_router<16>(a, lds, s);
             default: return launch_router<8>(a, lds, s);

@@ -143,7 +143,13 @@ __global__ __launch_bounds__(kThreads) void plan_count_kernel(const int32_t* __r
     __shared__ int sh[kThreads / 64];
     const int c = blockIdx.x;
     int n = 0;
-    for (int e = threadIdx.x; e < P; e += kThreads) n += (classes[e] == c) ? 1 : 0;
+    for (int e0 = threadIdx.x; e0 < P; e0 += 8 * kThreads) {  // eight loads in flight
+        int v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = (e0 + u * kThreads < P) ? classes[e0 + u * kThreads] : -1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) n += (v[u] == c) ? 1 : 0;
+    }
     n = block_sum(n, sh);
     if (threadIdx.x == 0) counts[c] = n;
 }
@@ -220,27 +226,48 @@ __global__ __launch_bounds__(kThreads) void plan_fill_kernel(
     const int nch = chunk_first[c + 1] - chunk_first[c];
     const int nqb = (cnt + QB - 1) / QB;
     if (cnt == 0) return;
-    // ordered fill of this bucket's pairs (ascending pair id = ascending q)
-    const int lane = tid & 63, w = tid >> 6;
-    int run = 0;
-    for (int base = 0; base < P; base += kThreads) {
-        const int e = base + tid;
-        const bool pred = (e < P) && (classes[e] == c);
-        const uint64_t m = __ballot(pred);
-        const int rank = __popcll(m & ((1ull << lane) - 1ull));
-        __syncthreads();
-        if (lane == 0) wcnt[w] = __popcll(m);
-        __syncthreads();
-        int wpre = 0, tot = 0;
-        for (int i = 0; i < kThreads / 64; ++i) {
-            wpre += (i < w) ? wcnt[i] : 0;
-            tot += wcnt[i];
+    // ordered fill of this bucket's pairs (ascending pair id = ascending q):
+    // every wave takes a contiguous segment, reads it coalesced (64 pairs per
+    // instruction) and ranks its matches by ballot; a wave's base is the
+    // count of the segments before it
+    {
+        const int lane = tid & 63, w = tid >> 6;
+        const int seg = ((P + kThreads / 64 - 1) / (kThreads / 64) + 63) & ~63;
+        const int sa = min(P, w * seg), sb = min(P, sa + seg);
+        constexpr int kU = 8;  // loads in flight per lane (each pass is latency-bound)
+        int n = 0;
+        for (int e0 = sa; e0 < sb; e0 += kU * 64) {
+            int v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int e = e0 + 64 * u + lane;
+                v[u] = e < sb ? classes[e] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) n += __popcll(__ballot(v[u] == c));
         }
-        if (pred) {
-            pair_q[off + run + wpre + rank] = e;
-            pair_bucket[off + run + wpre + rank] = c;
+        if (lane == 0) wcnt[w] = n;
+        __syncthreads();
+        int o = off;
+        for (int i = 0; i < w; ++i) o += wcnt[i];
+        const uint64_t lt = (1ull << lane) - 1ull;
+        for (int e0 = sa; e0 < sb; e0 += kU * 64) {
+            int v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int e = e0 + 64 * u + lane;
+                v[u] = e < sb ? classes[e] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint64_t m = __ballot(v[u] == c);
+                if (v[u] == c) {
+                    pair_q[o + __popcll(m & lt)] = e0 + 64 * u + lane;
+                    pair_bucket[o + __popcll(m & lt)] = c;
+                }
+                o += __popcll(m);
+            }
         }
-        run += tot;
     }
     const int cf = chunk_first[c];
     for (int i = tid; i < nch * nqb; i += kThreads) {
@@ -1168,8 +1195,11 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 #ifdef LMI_ABLATION
 // ABL == 7 (diagnostic build): the full kernel plus event counters
 // [0] blocks with a candidate in some lane (wave events), [1] candidates,
-// [2] appends, [3] sorted insertions, [4] buffer fills (sorts), [5] blocks
-__device__ unsigned long long lmi_dbg[8];
+// [2] appends, [3] sorted insertions, [4] buffer fills (sorts), [5] blocks;
+// every ABL: [8] sum over workgroups of shader-clock cycles (s_memtime) and
+// [9] of 100-MHz ticks (s_memrealtime) between kernel entry and exit,
+// [10] earliest entry tick, [11] latest exit tick, [12] workgroups
+__device__ unsigned long long lmi_dbg[16];
 #endif
 
 // Per-lane pick of acc[rg] (rg differs by lane): a 4-level select tree on
@@ -1212,9 +1242,14 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     // diagnostic builds only (results wrong for ABL != 0): 1 no insertion,
     // 2 DMA + barriers only, 3 no DMA, 4 no DMA and no insertion, 5 no DMA and
     // no epilogue, 6 = 5 without barriers, 7 event counters, 14 no DMA wait,
-    // 21 no barrier
+    // 21 no barrier, 31 every block's DMA re-reads the tile's first 4 blocks
+    // (L2-resident source: the cost of DMA without HBM misses), 32 = 2 with
+    // the source of 31, 33 non-temporal row loads (aux = nt)
+    constexpr int kAux = ABL == 33 ? 2 : 0;
+    constexpr bool kDmaOnly = ABL == 2 || ABL == 32;
+    constexpr bool kL2Src = ABL == 31 || ABL == 32;
     constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6;
-    constexpr bool kNoEpi = ABL == 2 || ABL == 5 || ABL == 6;
+    constexpr bool kNoEpi = kDmaOnly || ABL == 5 || ABL == 6;
     constexpr bool kNoIns = ABL == 1 || ABL == 4;
     constexpr bool kNoBar = ABL == 6 || ABL == 21;
     // An LDS-DMA issue holds its wave for ~45-60 cycles: the two waves of a
@@ -1252,6 +1287,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     }
     const int gx = xcc & (ng - 1);
     const bool late = slot >= NW / 2;
+#ifdef LMI_ABLATION
+    const uint64_t clk0 = __builtin_amdgcn_s_memtime();
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // this lane's list column: entry i at lbase + i * 512
     const uint32_t lbase = (uint32_t)(uintptr_t)(lists + wave * KL * 64 + lane);
 
@@ -1309,13 +1348,14 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         auto dma_stage = [&](int so, int b, int j) {
             if (kNoDma) return;
             unsigned char* sl = ring + so;
+            if (kL2Src) b &= 3;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
-                                                     b * (32 * D * 2) + j * ROWB, 0, 0);
+                                                     b * (32 * D * 2) + j * ROWB, 0, kAux);
             // (+2 rows through soffset: an instruction offset would move the
             // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave + 1) * PIECEP), 16,
                                                      vo_row, b * (32 * D * 2) + j * ROWB + 2 * D * 2,
-                                                     0, 0);
+                                                     0, kAux);
             if (j == NST - 1 && lane < 4)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(sl + NORM_OFF + 16 * wave), 4,
                                                          (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
@@ -1339,7 +1379,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             if (!kNoBar) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
-                if (ABL == 2 || !wave_live) {
+                if (kDmaOnly || !wave_live) {
                     if (more) dma_stage(ws0 + j * STAGE, blk + 1, j);
                     continue;
                 }
@@ -1473,19 +1513,32 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             if (L[KL - 1] != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)L[KL - 1]);
         }
     }
+#ifdef LMI_ABLATION
+    if (tid == 0) {
+        const uint64_t clk1 = __builtin_amdgcn_s_memtime();
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&lmi_dbg[8], (unsigned long long)(clk1 - clk0));
+        atomicAdd(&lmi_dbg[9], (unsigned long long)(rt1 - rt0));
+        atomicMin(&lmi_dbg[10], (unsigned long long)rt0);
+        atomicMax(&lmi_dbg[11], (unsigned long long)rt1);
+        atomicAdd(&lmi_dbg[12], 1ull);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
 // chunk merge
 // ---------------------------------------------------------------------------
 template <int KL>
-__global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
+__global__ __launch_bounds__(64) void chunk_merge_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
-    const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ counts_total_src,
-    const int32_t* __restrict__ chunk_first, const int32_t* __restrict__ gpos, int32_t P, int32_t k,
-    float* __restrict__ out_d, int32_t* __restrict__ out_pos, int64_t n_rows,
-    int32_t* __restrict__ status) {
-    const int pp = blockIdx.x * kThreads + threadIdx.x;
+    const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
+    const int32_t* __restrict__ gpos, int32_t P, int32_t k, float* __restrict__ out_d,
+    int32_t* __restrict__ out_pos, int64_t n_rows, int32_t* __restrict__ status) {
+    // one thread per pair, 64-thread blocks (spread over every CU); each
+    // chunk list is read with all its loads in flight, then its global
+    // positions gathered the same way, then merged into a register list
+    const int pp = blockIdx.x * 64 + threadIdx.x;
     if (pp >= P) return;
     const int c = pair_bucket[pp];
     if (c < 0) return;
@@ -1498,17 +1551,25 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
     // merge across chunks is by the reference's (distance, g.index) order.
     for (int j = 0; j < nch; ++j) {
         const uint64_t* src = partial + ((size_t)pp * max_chunks + j) * KL;
+        uint64_t K[KL];
+#pragma unroll
+        for (int i = 0; i < KL; ++i) K[i] = src[i];
+        int32_t g[KL];
+#pragma unroll
         for (int i = 0; i < KL; ++i) {
-            uint64_t key = src[i];
-            if (key == kEmptyKey) break;
-            const uint32_t lp = (uint32_t)key;
-            if (lp >= (uint32_t)n_rows) {  // never for a sound scan: drop, flag
-                atomicOr(status, LMI_STATUS_INTERNAL);
-                break;
-            }
-            key = (key & 0xffffffff00000000ull) | (uint32_t)gpos[lp];
-            if (key >= M[KL - 1]) break;
-            list_insert<KL>(M, key);
+            const uint32_t lp = (uint32_t)K[i];
+            // (pre-filter on the distance part only: the low halves are rows
+            // here and global positions in M)
+            const bool live = K[i] != kEmptyKey && (K[i] >> 32) <= (M[KL - 1] >> 32);
+            const bool ok = lp < (uint32_t)n_rows;
+            if (live && !ok) atomicOr(status, LMI_STATUS_INTERNAL);  // never for a sound scan
+            g[i] = (live && ok) ? gpos[lp] : -1;
+        }
+#pragma unroll
+        for (int i = 0; i < KL; ++i) {
+            if (g[i] < 0) continue;
+            const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
+            if (key < M[KL - 1]) list_insert<KL>(M, key);
         }
     }
     const size_t o = (size_t)pair_q[pp] * k;
@@ -1521,7 +1582,6 @@ __global__ __launch_bounds__(kThreads) void chunk_merge_kernel(
             out_pos[o + i] = empty ? -1 : (int32_t)(uint32_t)key;
         }
     }
-    (void)counts_total_src;
 }
 
 // ---------------------------------------------------------------------------
@@ -1712,6 +1772,9 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 7) return launch_scan3_v<7>(b, s);
     if (abl == 14) return launch_scan3_v<14>(b, s);
     if (abl == 21) return launch_scan3_v<21>(b, s);
+    if (abl == 31) return launch_scan3_v<31>(b, s);
+    if (abl == 32) return launch_scan3_v<32>(b, s);
+    if (abl == 33) return launch_scan3_v<33>(b, s);
 #endif
     return launch_scan3_v<0>(b, s);
 }
@@ -1906,25 +1969,26 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     }
     if (rc != LMI_OK) return rc;
 
-    const int grid = (P + kThreads - 1) / kThreads;
+    const int grid = (P + 63) / 64;
     if (KL == 10) {
-        hipLaunchKernelGGL(chunk_merge_kernel<10>, dim3(grid), dim3(kThreads), 0, s, a.partial,
-                           a.max_chunks, pair_q, pair_bucket, nullptr, idx->chunk_first, idx->gpos, P,
-                           k, out_d, out_pos, idx->n_rows, status);
+        hipLaunchKernelGGL(chunk_merge_kernel<10>, dim3(grid), dim3(64), 0, s, a.partial,
+                           a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, out_d,
+                           out_pos, idx->n_rows, status);
     } else {
-        hipLaunchKernelGGL(chunk_merge_kernel<16>, dim3(grid), dim3(kThreads), 0, s, a.partial,
-                           a.max_chunks, pair_q, pair_bucket, nullptr, idx->chunk_first, idx->gpos, P,
-                           k, out_d, out_pos, idx->n_rows, status);
+        hipLaunchKernelGGL(chunk_merge_kernel<16>, dim3(grid), dim3(64), 0, s, a.partial,
+                           a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, out_d,
+                           out_pos, idx->n_rows, status);
     }
     LMI_LAUNCH_CHECK("chunk_merge_kernel");
     return LMI_OK;
 }
 
 #ifdef LMI_ABLATION
-// diagnostic builds: read and clear the scan's event counters (ABL == 7)
-extern "C" int lmi_debug_counters(unsigned long long* out8) {
-    unsigned long long z[8] = {};
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(lmi::lmi_dbg), sizeof(z)) != hipSuccess) return LMI_E_HIP;
+// diagnostic builds: read and clear the scan's counters (lmi_dbg above)
+extern "C" int lmi_debug_counters(unsigned long long* out16) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(lmi::lmi_dbg), sizeof(z)) != hipSuccess) return LMI_E_HIP;
+    z[10] = ~0ull;
     if (hipMemcpyToSymbol(HIP_SYMBOL(lmi::lmi_dbg), z, sizeof(z)) != hipSuccess) return LMI_E_HIP;
     return LMI_OK;
 }

@@ -100,3 +100,22 @@ def test_device_replay_on_real_lists_reaches_every_branch(seed):
     assert int(s2.item()) == 0
     np.testing.assert_array_equal(dd.cpu().numpy(), ref_d)
     np.testing.assert_array_equal(aa.cpu().numpy().view(np.uint32), ref_a)
+
+
+@pytest.mark.parametrize("use_threshold", [True, False])
+def test_device_replay_large_groups(use_threshold):
+    """Groups whose relevant positions exceed the kernel's LDS staging
+    (kUCap = 8192 entries) take the global-scratch path; small ones in the
+    same launch stay in LDS."""
+    classes, d, pos, size, ids = _random_lists(21, nq=6000, R=3, C=5, kl=10, tiny=(4,))
+    ref_d, ref_a = replay(classes, d, pos, k_round=10, k_final=10, bucket_size=size,
+                          pos_to_id=ids, use_threshold=use_threshold)
+    assert np.bincount(classes[:, 1], minlength=5).max() * 10 > 8192
+    dev = torch.device("cuda")
+    dd, aa, st = replay_device(torch.from_numpy(classes).to(dev), torch.from_numpy(d).to(dev),
+                               torch.from_numpy(pos).to(dev), k_round=10, k_final=10,
+                               bucket_size=torch.from_numpy(size).to(dev),
+                               pos_to_id=torch.from_numpy(ids).to(dev), use_threshold=use_threshold)
+    assert int(st.item()) == 0
+    np.testing.assert_array_equal(dd.cpu().numpy(), ref_d)
+    np.testing.assert_array_equal(aa.cpu().numpy().view(np.uint32), ref_a)

@@ -41,6 +41,10 @@ for abl, var in runs:
     for _ in range(2):
         bucket_topk(ix, q, classes, 10)
     torch.cuda.synchronize()
+    dbg = hasattr(lib, "lmi_debug_counters")
+    cnt = (_lib.C.c_ulonglong * 16)()
+    if dbg:
+        lib.lmi_debug_counters(cnt)  # clear
     lib.lmi_timing_read(None, 0)
     lib.lmi_timing_enable(1)
     for _ in range(a.reps):
@@ -51,14 +55,20 @@ for abl, var in runs:
     n = lib.lmi_timing_read(ms, a.reps)
     v = sorted(list(ms)[:n])
     print(f"[{var}] abl={abl} scan ms: median {v[len(v)//2]:.3f} min {v[0]:.3f}", flush=True)
+    if dbg:
+        lib.lmi_debug_counters(cnt)
+        if cnt[9] and cnt[12]:
+            # shader clock = cycles / 100-MHz ticks; utilisation = mean
+            # workgroup lifetime / (last exit - first entry) of the reps
+            ghz = cnt[8] / cnt[9] * 0.1
+            life_us = cnt[9] / cnt[12] * 0.01
+            print(f"   clock {ghz:.3f} GHz, workgroup life {life_us:.0f} us avg over {cnt[12] // a.reps} WGs/launch",
+                  flush=True)
+        if abl == "7":
+            names = ["wave-events", "candidates", "appends", "sorted-inserts", "fills", "wave-blocks"]
+            print("   per launch: " + ", ".join(f"{nm}={cnt[i] / a.reps:.4g}" for i, nm in enumerate(names)),
+                  flush=True)
     if ref is not None:
         d, p_ = bucket_topk(ix, q, classes, 10)[:2]
         same = bool(torch.equal(d, ref[0]) and torch.equal(p_, ref[1]))
         print(f"   lists identical to abl=0: {same}", flush=True)
-    if abl == "7" and hasattr(lib, "lmi_debug_counters"):
-        cnt = (_lib.C.c_ulonglong * 8)()
-        lib.lmi_debug_counters(cnt)
-        runs_ = a.reps + 2
-        names = ["wave-events", "candidates", "appends", "sorted-inserts", "fills", "wave-blocks"]
-        print("   per launch: " + ", ".join(f"{nm}={cnt[i] / runs_:.4g}" for i, nm in enumerate(names)),
-              flush=True)
