@@ -168,12 +168,16 @@ def main():
     ap.add_argument("--arch", default="MLP-5")
     ap.add_argument("--centres", type=int, default=400)
     ap.add_argument("--train-steps", type=int, default=200)
-    ap.add_argument("--chunk-rows", type=int, default=8192)
+    ap.add_argument("--chunk-rows", type=int, default=None,
+                    help="scan chunk (rows); default by GPU count: 8192 on 1, 4096 on 2-4, 2048 on "
+                         "more (a shard's tiles must still fill 256 CUs; tools/gpu_shards.sh)")
     ap.add_argument("--recall-sample", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     rank, world, local = init_from_env()
+    if args.chunk_rows is None:
+        args.chunk_rows = 8192 if world == 1 else 4096 if world <= 4 else 2048
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     device = torch.device("cuda", local)

@@ -59,10 +59,10 @@ __device__ inline int block_min_i(int v, int* sh) {
     return t;
 }
 
-__device__ inline int wave_min_i(int v) {
-    for (int off = 32; off > 0; off >>= 1) v = min(v, __shfl_xor(v, off));
-    return v;
-}
+extern "C" __device__ int __ockl_wfred_min_i32(int);
+extern "C" __device__ int __ockl_wfred_add_i32(int);
+// wave-wide minimum (DPP reduction)
+__device__ inline int wave_min_i(int v) { return __ockl_wfred_min_i32(v); }
 
 struct RoundArgs {
     const int32_t* classes;
@@ -78,6 +78,7 @@ struct RoundArgs {
     int32_t* uraw;           // [nq * kl] scratch (positions of relevant entries),
                              // category c at [g0 * kl, g1 * kl)
     int32_t* status;
+    int32_t abl;  // diagnostic builds: 1/2/3 stop after grouping / U / selection
 };
 
 __device__ inline void list_at(const RoundArgs& a, int q, int j, double& d, int32_t& pos) {
@@ -126,14 +127,29 @@ __device__ void stable_argsort_dev(const double* row, int n, int* idx) {
 }
 
 constexpr int kUCap = 8192;  // relevant positions of a group held in LDS
+constexpr int kTG = 1024;    // group kernel: one large workgroup per category
 
-__global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
-    __shared__ int sh[kT / 64];
+template <int NT>
+__device__ inline int block_reduce_g(int v, int* sh, bool is_min) {
+    v = is_min ? wave_min_i(v) : __ockl_wfred_add_i32(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    int t = sh[0];
+    for (int w = 1; w < NT / 64; ++w) t = is_min ? min(t, sh[w]) : t + sh[w];
+    __syncthreads();
+    return t;
+}
+__device__ inline int block_sum_g(int v, int* sh) { return block_reduce_g<kTG>(v, sh, false); }
+__device__ inline int block_min_g(int v, int* sh) { return block_reduce_g<kTG>(v, sh, true); }
+
+__global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
+    __shared__ int sh[kTG / 64];
     __shared__ int32_t S[2 * kMaxKr + 16];  // smallest members of U, ascending
     __shared__ Ent qrow[kMaxKr];            // the quirk row of the group
     __shared__ int32_t Ul[kUCap];
-    __shared__ int32_t Sw[kT / 64][2 * kMaxKr];  // per wave: smallest members of its share
-    __shared__ int nsw[kT / 64 + 1];
+    __shared__ int32_t Sw[kTG / 64][2 * kMaxKr];  // per wave: smallest members of its share
+    __shared__ int nsw[kTG / 64 + 1];
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
     if (a.bucket_size[c] <= 0) return;  // groupby visits non-empty categories only
@@ -143,9 +159,9 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
     {
         // every wave takes a contiguous segment of the queries, read
         // coalesced, matches ranked by ballot
-        __shared__ int wc[2][kT / 64];
+        __shared__ int wc[2][kTG / 64];
         const int lane = tid & 63, w = tid >> 6;
-        const int seg = ((a.nq + kT / 64 - 1) / (kT / 64) + 63) & ~63;
+        const int seg = ((a.nq + kTG / 64 - 1) / (kTG / 64) + 63) & ~63;
         const int qa = min(a.nq, w * seg), qb = min(a.nq, qa + seg);
         constexpr int kU = 8;  // loads in flight per lane (each pass is latency-bound)
         int n_eq = 0, n_lt = 0;
@@ -168,7 +184,7 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
         }
         __syncthreads();
         int before = 0, n_g = 0, lt = 0;
-        for (int i = 0; i < kT / 64; ++i) {
+        for (int i = 0; i < kTG / 64; ++i) {
             before += (i < w) ? wc[0][i] : 0;
             n_g += wc[0][i];
             lt += wc[1][i];
@@ -194,6 +210,9 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
         }
         __syncthreads();
     }
+#ifdef LMI_ABLATION
+    if (a.abl == 1) return;
+#endif
     const int32_t* G = a.groups;
     const int kr = a.kr;
     const int kl_use = min(kr, a.kl);
@@ -202,24 +221,23 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
         // U = unique positions over the group; only its smallest members matter
         const int nU = (g1 - g0) * kl_use;
         int32_t* U = nU <= kUCap ? Ul : a.uraw + (size_t)g0 * kl_use;
+        // entry-parallel: a list is sorted by distance with its empty entries
+        // last, so "leading entries with d < thr" is a per-entry test
         int nb_tot = 0;
-        for (int gi = g0 + tid; gi < g1; gi += kT) {
+        for (int e = tid; e < nU; e += kTG) {
+            const int gi = g0 + e / kl_use, j = e - (e / kl_use) * kl_use;
             const int q = G[gi];
-            int32_t* u = U + (size_t)(gi - g0) * kl_use;
-            int n = 0;
-            for (int j = 0; j < kl_use; ++j) {
-                double d;
-                int32_t pos;
-                list_at(a, q, j, d, pos);
-                if (pos < 0 || !(d < a.thr[q])) break;
-                u[j] = pos;
-                ++n;
-            }
-            for (int j = n; j < kl_use; ++j) u[j] = INT32_MAX;
-            nb_tot += n;
+            const size_t o = ((size_t)q * a.R + a.r) * a.kl + j;
+            const int32_t pos = a.lists_p[o];
+            const bool rel = pos >= 0 && (double)a.lists_d[o] < a.thr[q];
+            U[e] = rel ? pos : INT32_MAX;
+            nb_tot += rel ? 1 : 0;
         }
-        nb_tot = block_sum_i(nb_tot, sh);  // (its barriers publish U)
+        nb_tot = block_sum_g(nb_tot, sh);  // (its barriers publish U)
         if (nb_tot == 0) return;  // LearnedIndex.py:157-159
+#ifdef LMI_ABLATION
+        if (a.abl == 2) return;
+#endif
         const int want = kr + kl_use;
         // the smallest `want` members of U: each wave finds those of its
         // share (every 4th 64-entry run), then wave 0 merges the four lists
@@ -228,7 +246,7 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
         int prev = -1, cnt = 0;
         for (; cnt < want; ++cnt) {
             int m = INT32_MAX;
-            for (int e = wv * 64 + lane; e < nU; e += kT) {
+            for (int e = wv * 64 + lane; e < nU; e += kTG) {
                 const int32_t p = U[e];
                 if (p > prev && p < m) m = p;
             }
@@ -240,8 +258,8 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
         if (lane == 0) nsw[wv] = cnt;
         __syncthreads();
         if (wv == 0) {
-            int v[4 * (2 * kMaxKr) / 64];
-            constexpr int NV = 4 * (2 * kMaxKr) / 64;
+            constexpr int NV = (kTG / 64) * (2 * kMaxKr) / 64;
+            int v[NV];
 #pragma unroll
             for (int t = 0; t < NV; ++t) {
                 const int e = lane + 64 * t, w = e / (2 * kMaxKr), i = e % (2 * kMaxKr);
@@ -258,34 +276,47 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
                 if (lane == 0) S[n] = m;
                 pv = m;
             }
-            if (lane == 0) nsw[4] = n;
+            if (lane == 0) nsw[kTG / 64] = n;
         }
         __syncthreads();
-        const int ns = nsw[4];
+        const int ns = nsw[kTG / 64];
+#ifdef LMI_ABLATION
+        if (a.abl == 3) return;
+#endif
         __syncthreads();
         if (ns >= kr) {
-            // normal case: B_q then the smallest members of U not in B_q
-            for (int gi = g0 + tid; gi < g1; gi += kT) {
+            // normal case: B_q then the smallest members of U not in B_q;
+            // B_q entry-parallel (U holds its positions), then per query the
+            // fillers, membership tested against its U row
+            for (int e = tid; e < nU; e += kTG) {
+                const int32_t p = U[e];
+                if (p == INT32_MAX) continue;
+                const int gi = g0 + e / kl_use, j = e - (e / kl_use) * kl_use;
                 const int q = G[gi];
+                a.dr_d[(size_t)q * kr + j] = (double)a.lists_d[((size_t)q * a.R + a.r) * a.kl + j];
+                a.dr_p[(size_t)q * kr + j] = p;
+            }
+            for (int gi = g0 + tid; gi < g1; gi += kTG) {
+                const int q = G[gi];
+                const int32_t* u = U + (size_t)(gi - g0) * kl_use;
+                int32_t lp[kMaxKr];
+                int n_rel = 0;
+#pragma unroll
+                for (int j = 0; j < kMaxKr; ++j) {
+                    lp[j] = j < kl_use ? u[j] : INT32_MAX;
+                    n_rel += lp[j] != INT32_MAX ? 1 : 0;
+                }
                 double* od = a.dr_d + (size_t)q * kr;
                 int32_t* op = a.dr_p + (size_t)q * kr;
-                int n = 0, n_rel;
-                for (int j = 0; j < kl_use && n < kr; ++j) {
-                    double d;
-                    int32_t pos;
-                    list_at(a, q, j, d, pos);
-                    if (pos < 0 || !(d < a.thr[q])) break;
-                    od[n] = d;
-                    op[n] = pos;
-                    ++n;
-                }
-                n_rel = n;
-                for (int u = 0; u < ns && n < kr; ++u) {
+                int n = n_rel;
+                for (int v = 0; v < ns && n < kr; ++v) {
+                    const int32_t sv = S[v];
                     bool mine = false;
-                    for (int j = 0; j < n_rel; ++j) mine |= (op[j] == S[u]);
+#pragma unroll
+                    for (int j = 0; j < kMaxKr; ++j) mine |= lp[j] == sv;
                     if (!mine) {
                         od[n] = kFill;
-                        op[n] = S[u];
+                        op[n] = sv;
                         ++n;
                     }
                 }
@@ -311,7 +342,7 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
                 quirk_row_dev(row, kr, S, ns, ann, kr, kr, qrow);
             }
             __syncthreads();
-            for (int gi = g0 + tid; gi < g1; gi += kT) {
+            for (int gi = g0 + tid; gi < g1; gi += kTG) {
                 const int q = G[gi];
                 for (int j = 0; j < kr; ++j) {
                     a.dr_d[(size_t)q * kr + j] = qrow[j].d;
@@ -322,7 +353,7 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
     } else {
         const int64_t n = a.bucket_size[c];
         if (n >= kr) {
-            for (int gi = g0 + tid; gi < g1; gi += kT) {
+            for (int gi = g0 + tid; gi < g1; gi += kTG) {
                 const int q = G[gi];
                 for (int j = 0; j < kr; ++j) {
                     double d;
@@ -362,7 +393,7 @@ __global__ __launch_bounds__(kT) void replay_group_kernel(RoundArgs a) {
                 }
             }
             __syncthreads();
-            for (int gi = g0 + tid; gi < g1; gi += kT) {
+            for (int gi = g0 + tid; gi < g1; gi += kTG) {
                 const int q = G[gi];
                 for (int j = 0; j < kr; ++j) {
                     a.dr_d[(size_t)q * kr + j] = qrow[j].d;
@@ -558,7 +589,10 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
         a.dr_p = (int32_t*)(ws + s.drp);
         a.uraw = (int32_t*)(ws + s.uraw);
         a.status = status;
-        hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kT), 0, st, a);
+#ifdef LMI_ABLATION
+        a.abl = getenv("LMI_REPLAY_ABL") ? atoi(getenv("LMI_REPLAY_ABL")) : 0;
+#endif
+        hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, a);
         LMI_LAUNCH_CHECK("replay_group_kernel");
         const int wn = (r == 0) ? k_round : std::min(k_final, wF + k_round);
         const int n = (r == 0) ? k_round : wF + k_round;

@@ -44,16 +44,20 @@ __device__ inline bool better(float a, int ia, float b, int ib) {
     return a > b || (a == b && ia < ib);
 }
 
-// wave-wide best (logit, class) under `better`; every lane gets the result
+extern "C" __device__ uint64_t __ockl_wfred_min_u64(uint64_t);
+extern "C" __device__ float __ockl_wfred_max_f32(float);
+extern "C" __device__ float __ockl_wfred_add_f32(float);
+
+// wave-wide best (logit, class) under `better`: a DPP minimum of the u64 key
+// (~ordered(logit) << 32 | class), i.e. descending logit, then ascending
+// class; every lane gets the winner
 __device__ inline void wave_best(float& v, int& i) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const float v2 = __shfl_xor(v, o);
-        const int i2 = __shfl_xor(i, o);
-        if (better(v2, i2, v, i)) {
-            v = v2;
-            i = i2;
-        }
-    }
+    const uint32_t bits = v == 0.0f ? 0u : __float_as_uint(v);  // -0 ties with +0, as in `better`
+    const uint32_t asc = (bits & 0x80000000u) ? ~bits : (bits | 0x80000000u);
+    const uint64_t key = __ockl_wfred_min_u64(((uint64_t)~asc << 32) | (uint32_t)i);
+    const uint32_t wa = ~(uint32_t)(key >> 32);
+    v = __uint_as_float((wa & 0x80000000u) ? (wa ^ 0x80000000u) : ~wa);
+    i = (int)(uint32_t)key;
 }
 
 template <int TQ>
@@ -203,10 +207,10 @@ __global__ __launch_bounds__(kThreads) void router_kernel(RouterArgs a) {
         const float* lr = logit + qq * S;
         float m = -__builtin_inff();
         for (int i = lane; i < C; i += 64) m = fmaxf(m, lr[i]);
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        m = __ockl_wfred_max_f32(m);
         float sum = 0.0f;
         for (int i = lane; i < C; i += 64) sum += expf(lr[i] - m);
-        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        sum = __ockl_wfred_add_f32(sum);
         if (lane == 0) {
             stat[2 * qq] = m;
             stat[2 * qq + 1] = sum;

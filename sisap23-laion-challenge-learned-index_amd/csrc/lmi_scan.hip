@@ -1252,6 +1252,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     constexpr bool kNoEpi = kDmaOnly || ABL == 5 || ABL == 6;
     constexpr bool kNoIns = ABL == 1 || ABL == 4;
     constexpr bool kNoBar = ABL == 6 || ABL == 21;
+    // bound exchange period in blocks (diagnostic: 40 none, 41 every 4, 42 every 8, 43 every 16)
+    constexpr int kXch = ABL == 40 ? 0 : ABL == 41 ? 4 : ABL == 42 ? 8 : ABL == 43 ? 16 : 32;
     // An LDS-DMA issue holds its wave for ~45-60 cycles: the two waves of a
     // SIMD issue theirs at different MFMAs (slots 0-3 early, 4-7 late)
     constexpr int kDmaTT = 2, kDmaLate = 10;
@@ -1377,6 +1379,13 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             // wave's has, and every wave is done with block blk-1's slots
             if (ABL != 14) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
             if (!kNoBar) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // every kXch blocks: publish this lane's bound to the pair's global
+            // bound and take the global one back (tiles of the same pair on
+            // other chunks run concurrently); the returning atomic is consumed
+            // in this block's epilogue, behind its MFMAs
+            uint64_t xg = kEmptyKey;
+            if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live)
+                xg = atomicMin(&a.thr_g[pp], (unsigned long long)thr);
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
                 if (kDmaOnly || !wave_live) {
@@ -1408,6 +1417,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             const int hh = ln >> 5;
             const unsigned char* nb = ring + nso + NORM_OFF + hh * 16;
             const int vr = nrows - blk * 32 - 4 * hh;  // valid rows past this lane's offset
+            thr = std::min(thr, xg);
             const float bound = key_dist_bound(thr);
             uint32_t mask = 0;
 #pragma unroll
@@ -1775,6 +1785,10 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 31) return launch_scan3_v<31>(b, s);
     if (abl == 32) return launch_scan3_v<32>(b, s);
     if (abl == 33) return launch_scan3_v<33>(b, s);
+    if (abl == 40) return launch_scan3_v<40>(b, s);
+    if (abl == 41) return launch_scan3_v<41>(b, s);
+    if (abl == 42) return launch_scan3_v<42>(b, s);
+    if (abl == 43) return launch_scan3_v<43>(b, s);
 #endif
     return launch_scan3_v<0>(b, s);
 }

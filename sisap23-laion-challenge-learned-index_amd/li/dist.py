@@ -7,9 +7,11 @@ per-shard lists: top-k(union of shards) = top-k(union of per-shard top-k).
 The one exchange step is an all-gather of the lists (nq*R*k*8 bytes per rank,
 ~3.2 MB at 10k queries, R=4: latency-bound on xGMI), over RCCL
 (torch.distributed backend "nccl"), followed by K3 (lmi_merge_topk) on every
-rank.  The router is replicated: every rank computes the same classes
-(deterministic K1), so no broadcast is needed.  Results are bitwise identical
+rank.  Every rank ends up with the same classes.  Results are bitwise identical
 for any G because every list is ordered by (distance, global position).
+The router is sharded by queries (route_sharded): each rank routes nq/G queries
+and the classes are all-gathered (nq*R*4 bytes), so its cost shrinks with G;
+the per-query results are the same as routing the whole batch on one GPU.
 """
 from __future__ import annotations
 
@@ -60,3 +62,22 @@ def gather_merge(d: torch.Tensor, pos: torch.Tensor, k: int, group=None,
         from .index import merge_topk
         return merge_topk(gd, gp, k)
     return merge(gd, gp, k)
+
+
+def route_sharded(router, q_nav: torch.Tensor, R: int, group=None) -> torch.Tensor:
+    """K1 on this rank's contiguous slice of the queries, then an all-gather of
+    the classes: [nq, R] int32 on every rank, equal to router.topr(q_nav, R)
+    (the router is per-query: a query's classes do not depend on its batch)."""
+    G = dist.get_world_size(group)
+    g = dist.get_rank(group)
+    nq = q_nav.shape[0]
+    per = -(-nq // G)
+    lo = min(nq, g * per)
+    hi = min(nq, lo + per)
+    part = torch.zeros((per, R), dtype=torch.int32, device=q_nav.device)
+    if hi > lo:
+        c, _ = router.topr(q_nav[lo:hi], R)
+        part[: hi - lo] = c
+    out = torch.empty((G * per, R), dtype=torch.int32, device=q_nav.device)
+    dist.all_gather_into_tensor(out, part, group=group)
+    return out[:nq]

@@ -447,12 +447,21 @@ class Searcher:
               classes: Optional[torch.Tensor] = None):
         """Device part: router + scan (+ RCCL merge).  Returns device tensors."""
         if classes is None:
-            classes, _ = self.router.topr(q_nav, R)
+            classes = self.route(q_nav, R)
         d, pos, status = bucket_topk(self.index, q_search, classes, k_list)
         if self.index.world > 1:
             from .dist import gather_merge
             d, pos = gather_merge(d, pos, k_list, self.group)
         return classes, d, pos, status
+
+    def route(self, q_nav, R: int) -> torch.Tensor:
+        """K1 classes [nq, R]; with G > 1 ranks each routes nq/G queries and
+        the classes are all-gathered (li.dist.route_sharded)."""
+        if self.index.world > 1:
+            from .dist import route_sharded
+            return route_sharded(self.router, _as_torch(q_nav, self.index.device, torch.float32), R,
+                                 self.group)
+        return self.router.topr(q_nav, R)[0]
 
     def _device_tables(self):
         """bucket sizes and position -> id map in HBM for the device replay."""
@@ -498,7 +507,7 @@ class Searcher:
 
         t0 = time.perf_counter()
         if classes is None:
-            classes, _ = self.router.topr(q_nav, R)
+            classes = self.route(q_nav, R)
         t0 = lap("router", t0)
         d, pos, status = scan()
         t0 = lap("scan", t0)

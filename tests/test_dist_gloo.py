@@ -66,7 +66,7 @@ def _worker(rank, world, port, result_path):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import lmi_oracle as O
     import workloads
-    from li.dist import gather_merge, init_from_env
+    from li.dist import gather_merge, init_from_env, route_sharded
     from li.index import BucketLayout
     init_from_env(backend="gloo")
     w = workloads.clustered(n=2500, nq=80, C=16, seed=31, label_mode="skewed")
@@ -75,20 +75,28 @@ def _worker(rank, world, port, result_path):
     gpos, _ = BucketLayout.from_labels(w["labels"], C).shard(rank, world)
     d, p = _shard_lists(w, classes, R, k, C, gpos)
     md, mp_ = gather_merge(torch.from_numpy(d), torch.from_numpy(p), k, merge=_oracle_merge)
+
+    class _OracleRouter:  # K1's contract on the CPU: per-query top-R classes
+        def topr(self, x, R):
+            c = O.rank_classes(O.mlp_forward(x.numpy(), w["layers"]))[:, :R]
+            return torch.from_numpy(np.ascontiguousarray(c, dtype=np.int32)), None
+
+    routed = route_sharded(_OracleRouter(), torch.from_numpy(w["qn"]), R).numpy()
     if rank == 0:
         fd, fp = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, C)
         # BLAS results depend on the matrix shape at the ulp level, so the
         # oracle is compared with the tie-aware comparator (the GPU scan is
         # shape-independent and is checked bitwise in test_gpu_parity.py)
         ok = O.compare_lists(fd, fp, md.numpy(), mp_.numpy()) == 0 and \
-            np.array_equal(np.isfinite(md.numpy()), np.isfinite(fd))
+            np.array_equal(np.isfinite(md.numpy()), np.isfinite(fd)) and \
+            np.array_equal(routed, classes)
         with open(result_path, "w") as f:
             f.write("ok" if ok else "mismatch")
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_striped_search_equals_single_shard(world, tmp_path):
     res = tmp_path / "result.txt"
     mp.spawn(_worker, args=(world, _free_port(), str(res)), nprocs=world, join=True)

@@ -14,6 +14,8 @@ ap.add_argument("--R", type=int, default=4)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--chunk-rows", type=int, default=8192)
 ap.add_argument("--abl", default="0")
+ap.add_argument("--world", type=int, default=1, help="time the shard of --rank out of --world GPUs")
+ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--no-subcluster", action="store_true")
 ap.add_argument("--check", action="store_true", help="compare every variant's lists to abl=0 (bitwise)")
 ap.add_argument("--variants", default="",
@@ -23,7 +25,8 @@ dev = torch.device("cuda")
 x, q, qn, xn, layers = synth.build_lmi_workload(a.n, a.nq, 122, "MLP-5", dev)
 router = DeviceRouter(layers)
 labels = router.argmax(xn); del xn
-ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows, subcluster=not a.no_subcluster)
+ix = DeviceIndex(x, labels, 122, chunk_rows=a.chunk_rows, subcluster=not a.no_subcluster,
+                 rank=a.rank, world=a.world)
 classes, _ = router.topr(qn, a.R)
 lib = _lib.load()
 ref = None

@@ -1,0 +1,52 @@
+"""Device replay (K4) timing on bench-shaped random lists: 10k queries, R=4,
+122 buckets of skewed popularity, k=10; torch events around lmi_replay_device.
+With LMI_LIB_NAME=liblmi_hip_abl.so, LMI_REPLAY_ABL=1/2/3 stop the group kernel
+after grouping / U / selection (diagnostic: results then wrong)."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
+import numpy as np
+import torch
+from li.index import replay_device
+
+
+def _random_lists(seed, nq, R, C, kl):
+    """sorted per-(query, probe) lists over buckets of 40-400 rows, skewed
+    bucket popularity, ties likely (the shape tests/test_gpu_replay.py uses)"""
+    rng = np.random.default_rng(seed)
+    size = rng.integers(40, 400, C).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(size)])
+    p = rng.dirichlet(np.full(C, 0.5))
+    classes = np.stack([rng.choice(C, R, replace=False, p=p) for _ in range(nq)]).astype(np.int32)
+    d = np.full((nq, R, kl), np.inf, np.float32)
+    pos = np.full((nq, R, kl), -1, np.int32)
+    for q in range(nq):
+        for r in range(R):
+            c = classes[q, r]
+            n = min(kl, size[c])
+            pp = rng.choice(size[c], n, replace=False) + off[c]
+            dd = np.round(rng.random(n) * 0.6 + 0.2, 3).astype(np.float32)
+            o = np.lexsort((pp, dd))
+            d[q, r, :n], pos[q, r, :n] = dd[o], pp[o]
+    ids = rng.permutation(int(off[-1])).astype(np.int64) + 1
+    return classes, d, pos, size, ids
+
+
+classes, d, pos, size, ids = _random_lists(3, nq=10000, R=4, C=122, kl=10)
+dev = torch.device("cuda")
+args = [torch.from_numpy(x).to(dev) for x in (classes, d, pos)]
+bsz, p2id = torch.from_numpy(size).to(dev), torch.from_numpy(ids).to(dev)
+for abl in (os.environ.get("ABLS", "0").split(",")):
+    os.environ["LMI_REPLAY_ABL"] = abl
+    fn = lambda: replay_device(*args, k_round=10, k_final=10, bucket_size=bsz, pos_to_id=p2id,
+                               use_threshold=True)
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"replay abl={abl}: {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us", flush=True)
