@@ -41,14 +41,17 @@ def init_from_env(backend: Optional[str] = None):
 
 
 def all_gather_lists(d: torch.Tensor, pos: torch.Tensor, group=None):
-    """[nq, R, k] per rank -> [G, nq, R, k] on every rank."""
+    """[nq, R, k] per rank -> [G, nq, R, k] on every rank, in ONE collective:
+    the f32 distances travel bit-for-bit as int32 beside the positions."""
     G = dist.get_world_size(group)
+    both = torch.stack((d.contiguous().view(torch.int32), pos.to(torch.int32).contiguous()), dim=-1)
     # concatenated along dim 0 (the form both RCCL and gloo accept), viewed [G, ...]
-    gd = torch.empty((G * d.shape[0],) + tuple(d.shape[1:]), dtype=d.dtype, device=d.device)
-    gp = torch.empty((G * pos.shape[0],) + tuple(pos.shape[1:]), dtype=pos.dtype, device=pos.device)
-    dist.all_gather_into_tensor(gd, d.contiguous(), group=group)
-    dist.all_gather_into_tensor(gp, pos.contiguous(), group=group)
-    return gd.view((G,) + tuple(d.shape)), gp.view((G,) + tuple(pos.shape))
+    out = torch.empty((G * both.shape[0],) + tuple(both.shape[1:]), dtype=both.dtype, device=both.device)
+    dist.all_gather_into_tensor(out, both, group=group)
+    out = out.view((G,) + tuple(both.shape))
+    gd = out[..., 0].contiguous().view(torch.float32)
+    gp = out[..., 1].contiguous().to(pos.dtype)
+    return gd, gp
 
 
 def gather_merge(d: torch.Tensor, pos: torch.Tensor, k: int, group=None,
