@@ -119,3 +119,29 @@ def test_scan_tiles_of_many_pairs_match_oracle_and_4wave_ring(label_mode, monkey
     assert torch.equal(d3, d2) and torch.equal(p3, p2)
     ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, w["C"])
     assert O.compare_lists(ref_d, ref_p, d3.cpu().numpy(), p3.cpu().numpy()) == 0
+
+
+@pytest.mark.parametrize("hidden", [(128,), (256, 128), (100,)])
+def test_router_mfma_matches_fma_path(hidden, monkeypatch):
+    """K1's MFMA form (widths multiples of 16) and its FMA-chain form
+    (LMI_ROUTER_FMA=1, and the automatic fallback for other widths) agree with
+    the oracle and with each other up to near-ties of the logits."""
+    rng = np.random.default_rng(5)
+    dims = (96,) + hidden + (122,)
+    layers = [(rng.standard_normal((o, i)).astype(np.float32) / np.sqrt(i),
+               rng.standard_normal(o).astype(np.float32) * 0.1) for i, o in zip(dims, dims[1:])]
+    x = rng.standard_normal((1000, 96)).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    logits = O.mlp_forward(x, layers)
+    r = DeviceRouter(layers)
+    xt = torch.from_numpy(x).cuda()
+    cls_m, p_m = r.topr(xt, 7, with_probs=True)
+    monkeypatch.setenv("LMI_ROUTER_FMA", "1")
+    cls_f, p_f = r.topr(xt, 7, with_probs=True)
+    am_f = r.argmax(xt).cpu().numpy()
+    monkeypatch.delenv("LMI_ROUTER_FMA")
+    am_m = r.argmax(xt).cpu().numpy()
+    for cls in (cls_m.cpu().numpy(), cls_f.cpu().numpy()):
+        assert _router_mismatch(cls, logits, 7) == 0
+    np.testing.assert_allclose(p_m.cpu().numpy(), p_f.cpu().numpy(), rtol=1e-5, atol=1e-7)
+    assert (am_m != am_f).sum() <= 1

@@ -1,0 +1,40 @@
+"""Per-rank step time of a W-GPU striped index, timed on ONE GPU: rank 0's shard,
+a 1-process RCCL group (the all-gather moves only this rank's lists), full
+Searcher.search (router + scan + K3 merge + device replay + D2H).  Estimates the
+fixed per-step costs that do not shrink with W."""
+import argparse, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
+import numpy as np, torch, torch.distributed as dist
+from li import synth
+from li.index import DeviceIndex, DeviceRouter, Searcher
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--worlds", default="1,8")
+ap.add_argument("--steps", type=int, default=20)
+a = ap.parse_args()
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1"); os.environ.setdefault("MASTER_PORT", "29533")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1)
+dev = torch.device("cuda", 0)
+x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
+router = DeviceRouter(layers)
+labels = router.argmax(xn); del xn
+for W in map(int, a.worlds.split(",")):
+    ck = 8192 if W == 1 else 4096 if W <= 4 else 2048
+    ix = DeviceIndex(x, labels, 122, chunk_rows=ck, rank=0, world=W)
+    s = Searcher(ix, router)
+    for _ in range(3):
+        s.search(qn, q, 4, k=10)
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    for _ in range(a.steps):
+        s.search(qn, q, 4, k=10)
+    torch.cuda.synchronize(); el = (time.perf_counter() - t0) / a.steps * 1e3
+    tm = {}
+    for _ in range(5):
+        s.search(qn, q, 4, k=10, timings=tm)
+    br = {k: round(v / 5, 3) for k, v in tm.items()}
+    print(f"world {W} chunk {ck}: step {el:.3f} ms -> {10000 / el * 1e3 * 1:.0f} q/s per rank-step; "
+          f"breakdown {br}", flush=True)
+    del ix, s; torch.cuda.empty_cache()
+dist.destroy_process_group()
