@@ -44,6 +44,11 @@ def _fingerprint(a: np.ndarray):
 
 class LearnedIndex(Logger):
 
+    # class-level defaults for instances unpickled from the reference's
+    # pickle (li.index_io.load_index), which hold only `model`
+    _cache_key = None
+    _index = None
+
     def __init__(self):
         self.model = None
         self._cache_key = None

@@ -85,6 +85,11 @@ def get_device() -> torch.device:
 class NeuralNetwork(Logger):
     """The router (model.py:114-229); inference runs on K1 (lmi_router)."""
 
+    # class-level defaults: an instance unpickled from the reference's own
+    # pickle (li.index_io.load_index) carries only the reference's attributes
+    _router = None
+    _router_version = None
+
     def __init__(self, input_dim, output_dim, loss=torch.nn.CrossEntropyLoss, lr=0.1,
                  model_type="MLP", class_weight=None):
         self.device = get_device()
