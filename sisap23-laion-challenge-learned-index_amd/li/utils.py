@@ -30,18 +30,8 @@ def prepare(kind, size):
 
 def store_results(dst, algo, kind, dists, anns, buildtime, querytime, params, size):
     """utils.py:85-97: HDF5 with attrs algo/data/buildtime/querytime/size/params
-    and datasets knns (anns dtype, uint32) and dists (float64), read by eval/."""
-    try:
-        import h5py
-    except ImportError as e:
-        raise ImportError("store_results needs h5py (eval/ reads HDF5 result files)") from e
+    and datasets knns (uint32) and dists (float64), read by eval/ — written by
+    the native libhdf5 shim (li.h5, liblmi_h5.so)."""
+    from . import h5
     os.makedirs(Path(dst).parent, exist_ok=True)
-    with h5py.File(dst, "w") as f:
-        f.attrs["algo"] = algo
-        f.attrs["data"] = kind
-        f.attrs["buildtime"] = buildtime
-        f.attrs["querytime"] = querytime
-        f.attrs["size"] = size
-        f.attrs["params"] = params
-        f.create_dataset("knns", anns.shape, dtype=anns.dtype)[:] = anns
-        f.create_dataset("dists", dists.shape, dtype=dists.dtype)[:] = dists
+    h5.write_results(dst, algo, kind, dists, anns, buildtime, querytime, params, size)

@@ -38,9 +38,10 @@ def _normalize(x):
 
 
 def _load(kind, size, key):
-    import h5py
-    data = np.array(h5py.File(os.path.join("data", kind, size, "dataset.h5"), "r")[key])
-    queries = np.array(h5py.File(os.path.join("data", kind, size, "query.h5"), "r")[key])
+    """search.py:48-49 / :79-87 (np.array(h5py.File(...)[key])) on liblmi_h5.so."""
+    from li import h5
+    data = h5.read_dataset(os.path.join("data", kind, size, "dataset.h5"), key)
+    queries = h5.read_dataset(os.path.join("data", kind, size, "query.h5"), key)
     return data, queries
 
 
@@ -108,12 +109,9 @@ def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc
         short_identifier = 'learned-index'
         identifier = (f'{short_identifier}-{kind}-{size}-ep={epochs}-lr={lr}-cat='
                       f'{n_categories}-model={model_type}-buck={bucket}')
-        try:
-            store_results(os.path.join("result/", kind, size, f"{identifier}.h5"),
-                          short_identifier.capitalize(), kind, dists, nns, build_t, search_t,
-                          identifier, size)
-        except ImportError as e:
-            LOG.warning(f'{e}; result file not written')
+        store_results(os.path.join("result/", kind, size, f"{identifier}.h5"),
+                      short_identifier.capitalize(), kind, dists, nns, build_t, search_t,
+                      identifier, size)
 
 
 if __name__ == "__main__":
