@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 2
+#define LMI_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -189,6 +189,28 @@ int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, int32_t k_l
                       const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
                       const double* thr_round0, double* dists_out, uint32_t* anns_out,
                       int32_t* status, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- k-means for the index build (ABI 3) -------------- */
+/* Replaces faiss.Kmeans(d, k, seed=2023).train(X) and
+ * kmeans.index.search(X, 1) (LearnedIndex.py:242-282); the Lloyd loop, the
+ * training subsample and the empty-cluster split run on the host
+ * (li/kmeans.py).  All pointers are device memory; asynchronous on `stream`.
+ *
+ * lmi_kmeans_assign: labels_out[i] = argmin_j Σ_e (x[i][e] - cent[j][e])²
+ *   (squared L2 in fp32, e ascending, no FMA contraction; ties -> lower j);
+ *   dist_out (nullable) receives the minimum.  x [n][d], cent [k][d] f32,
+ *   1 <= d <= LMI_KMEANS_MAX_D.
+ * lmi_kmeans_update: cent_out[c] = mean of the points labelled c (fp64 sums
+ *   in a fixed order, rounded once), counts_out[c] = their number; rows of
+ *   empty clusters are left untouched.  A label outside [0, k) ORs 1 into
+ *   *status (device int32) and is skipped.  Deterministic. */
+#define LMI_KMEANS_MAX_D 128
+int lmi_kmeans_assign(const float* x, int64_t n, int32_t d, const float* cent, int32_t k,
+                      int32_t* labels_out, float* dist_out, void* stream);
+size_t lmi_kmeans_workspace_bytes(int64_t n, int32_t d, int32_t k);
+int lmi_kmeans_update(const float* x, int64_t n, int32_t d, const int32_t* labels, int32_t k,
+                      float* cent_out, int64_t* counts_out, int32_t* status, void* workspace,
+                      size_t ws_bytes, void* stream);
 
 /* ---- kernel timing (measurement only) -------------------------------------- */
 /* While enabled, lmi_bucket_topk records a HIP event pair on its stream around

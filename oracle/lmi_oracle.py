@@ -362,3 +362,116 @@ def compare_lists(d_a, p_a, d_b, p_b, *, atol=1e-5, tie=1e-6):
                 bad += 1
                 break
     return bad
+
+
+# ---------------------------------------------------------------------------
+# k-means for the index build (LearnedIndex.py:242-282)
+#
+# The reference calls faiss.Kmeans(d, k, verbose=True, seed=2023).train(X)
+# and labels with kmeans.index.search(X, 1) (LearnedIndex.py:275-282).  faiss
+# (1.7.x, pinned by the reference's environment, not vendored and not in this
+# image) is restated from its published Clustering::train: subsample to
+# k * max_points_per_centroid points, initialise with k random training
+# points, niter Lloyd iterations (assign, mean update, split of empty
+# clusters).  faiss's own RNG (mt19937 behind faiss::RandomGenerator) is
+# replaced by numpy RandomState streams with the same seeds, so sample, init
+# and split choices are NOT faiss's: "parity unpinned" against faiss itself.
+# The Lloyd arithmetic is pinned against sklearn's KMeans (lloyd, explicit
+# init) in tests/test_kmeans.py, and the GPU kernels (csrc/lmi_kmeans.hip)
+# are checked bit for bit against the functions below.
+# ---------------------------------------------------------------------------
+KMEANS_SLICES = 256
+KMEANS_EPS = np.float32(1.0 / 1024.0)
+
+
+def kmeans_assign(x: np.ndarray, cent: np.ndarray):
+    """argmin_j Σ_e (x_e - c_je)², fp32, e ascending, each op rounded
+    separately (the kernel's exact arithmetic); ties -> lower j (faiss's
+    IndexFlatL2 argmin order)."""
+    x = np.ascontiguousarray(x, np.float32)
+    cent = np.ascontiguousarray(cent, np.float32)
+    acc = np.zeros((x.shape[0], cent.shape[0]), np.float32)
+    for e in range(x.shape[1]):
+        t = x[:, e, None] - cent[None, :, e]
+        acc = acc + t * t
+    lab = acc.argmin(1).astype(np.int32)
+    return lab, acc[np.arange(x.shape[0]), lab]
+
+
+def kmeans_slices(n: int) -> int:
+    return int(max(1, min(KMEANS_SLICES, (n + 1023) // 1024)))
+
+
+def kmeans_update(x: np.ndarray, labels: np.ndarray, cent: np.ndarray):
+    """Mean of every cluster: fp64 sums per slice in point order, slices added
+    in order, rounded once to fp32 (faiss compute_centroids, deterministic
+    order of the kernel).  Empty clusters keep their row."""
+    n, d = x.shape
+    k = cent.shape[0]
+    S = kmeans_slices(n)
+    tot = np.zeros((k, d), np.float64)
+    cnt = np.zeros(k, np.int64)
+    for s in range(S):
+        a, b = s * n // S, (s + 1) * n // S
+        part = np.zeros((k, d), np.float64)
+        np.add.at(part, labels[a:b], x[a:b].astype(np.float64))  # sequential, point order
+        tot += part
+        cnt += np.bincount(labels[a:b], minlength=k)
+    out = cent.astype(np.float32).copy()
+    nz = cnt > 0
+    out[nz] = (tot[nz] / cnt[nz, None]).astype(np.float32)
+    return out, cnt
+
+
+def kmeans_split_empty(cent: np.ndarray, counts: np.ndarray, n: int, rng) -> int:
+    """faiss split_clusters: every empty centroid copies a cluster cj picked
+    with probability (|cj| - 1)/(n - k) (scanning cj cyclically), both are
+    perturbed by ±EPS on alternating dimensions, and cj's count is halved."""
+    k = cent.shape[0]
+    nsplit = 0
+    for ci in range(k):
+        if counts[ci] != 0:
+            continue
+        cj = 0
+        while True:
+            p = np.float32((counts[cj] - 1.0) / float(np.float32(n - k)))
+            r = np.float32(rng.random_sample())
+            if r < p:
+                break
+            cj = (cj + 1) % k
+        cent[ci] = cent[cj]
+        cent[ci, 0::2] *= np.float32(1) + KMEANS_EPS
+        cent[cj, 0::2] *= np.float32(1) - KMEANS_EPS
+        cent[ci, 1::2] *= np.float32(1) - KMEANS_EPS
+        cent[cj, 1::2] *= np.float32(1) + KMEANS_EPS
+        counts[ci] = counts[cj] // 2
+        counts[cj] -= counts[ci]
+        nsplit += 1
+    return nsplit
+
+
+def kmeans_train_sample(n: int, k: int, seed: int, max_points_per_centroid: int = 256):
+    """Rows of X that faiss trains on: all, or a seeded sample of k·mppc."""
+    if n > k * max_points_per_centroid:
+        return np.random.RandomState(seed).permutation(n)[: k * max_points_per_centroid]
+    return np.arange(n)
+
+
+def kmeans_train(x: np.ndarray, k: int, *, niter: int = 25, seed: int = 1234,
+                 max_points_per_centroid: int = 256):
+    """faiss Clustering::train restated (see the block comment above);
+    returns (centroids [k, d] f32, per-iteration objective list)."""
+    x = np.ascontiguousarray(x, np.float32)
+    xt = x[kmeans_train_sample(x.shape[0], k, seed, max_points_per_centroid)]
+    n = xt.shape[0]
+    if n < k:
+        raise ValueError(f"{n} training points for {k} centroids")
+    cent = xt[np.random.RandomState(seed + 1).permutation(n)[:k]].copy()
+    rng = np.random.RandomState(1234)
+    obj = []
+    for _ in range(niter):
+        lab, dist = kmeans_assign(xt, cent)
+        obj.append(float(dist.astype(np.float64).sum()))
+        cent, cnt = kmeans_update(xt, lab, cent)
+        kmeans_split_empty(cent, cnt, n, rng)
+    return cent, obj

@@ -139,16 +139,17 @@ class LearnedIndex(Logger):
         return nn.predict(data_X_to_torch(data)), time.time() - s
 
     def cluster(self, data, n_clusters):
-        """k-means labels (LearnedIndex.py:242-282 uses faiss.Kmeans, seed 2023,
-        25 iterations, which is not available here: Lloyd on the GPU instead)."""
-        from .synth import kmeans
-        X = torch.from_numpy(np.array(data).astype(np.float32))
-        if X.shape[0] < 2:
-            return None, np.zeros_like(X.shape[0])
-        if X.shape[0] < n_clusters:
-            n_clusters = max(X.shape[0] // 5, 2)
-        dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
-        X = X.to(dev)
-        cent = kmeans(X, n_clusters, iters=25, seed=2023)
-        d2 = (X * X).sum(1, keepdim=True) - 2 * X @ cent.T + (cent * cent).sum(1)[None]
-        return cent, d2.argmin(1).cpu().numpy()
+        """LearnedIndex.py:242-282: k-means labels of the navigation data.  The
+        reference's faiss.Kmeans(d, k, seed=2023) is replaced by li.kmeans.Kmeans
+        (same API and defaults, GPU kernels csrc/lmi_kmeans.hip)."""
+        from .kmeans import Kmeans
+        if data.shape[0] < 2:
+            return None, np.zeros_like(data.shape[0])
+        if data.shape[0] < n_clusters:
+            n_clusters = data.shape[0] // 5
+            if n_clusters < 2:
+                n_clusters = 2
+        X = np.array(data).astype(np.float32)
+        kmeans = Kmeans(d=X.shape[1], k=n_clusters, verbose=False, seed=2023)
+        kmeans.train(X)
+        return kmeans, kmeans.index.search(X, 1)[1].T[0]

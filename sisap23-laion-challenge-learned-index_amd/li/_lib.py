@@ -36,6 +36,7 @@ LMI_Q_F16 = 0
 LMI_Q_F32 = 1
 LMI_MAX_LAYERS = 8
 LMI_MAX_K = 16
+LMI_KMEANS_MAX_D = 128
 
 # every symbol include/lmi_hip.h declares (tests check the export table)
 EXPORTS = (
@@ -47,6 +48,9 @@ EXPORTS = (
     "lmi_replay",
     "lmi_replay_device_workspace_bytes",
     "lmi_replay_device",
+    "lmi_kmeans_assign",
+    "lmi_kmeans_workspace_bytes",
+    "lmi_kmeans_update",
     "lmi_timing_enable",
     "lmi_timing_read",
     "lmi_last_error",
@@ -73,7 +77,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class IndexDesc(C.Structure):
@@ -111,6 +115,9 @@ _SIGNATURES = {
     "lmi_replay_device_workspace_bytes": (C.c_size_t, [_I32, _I32, _I32, _I32, _I32, _I32]),
     "lmi_replay_device": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64,
                                     _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
+    "lmi_kmeans_assign": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P]),
+    "lmi_kmeans_workspace_bytes": (C.c_size_t, [_I64, _I32, _I32]),
+    "lmi_kmeans_update": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_timing_enable": (C.c_int, [_I32]),
     "lmi_timing_read": (C.c_int32, [_P, _I32]),
     "lmi_last_error": (C.c_char_p, []),
