@@ -35,14 +35,14 @@ sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd
 
 from li import _lib, synth  # noqa: E402
 from li.dist import init_from_env  # noqa: E402
-from li.index import DeviceIndex, DeviceRouter, Searcher  # noqa: E402
+from li.index import DeviceIndex, DeviceRouter, RowSource, Searcher  # noqa: E402
 
 METRIC = "queries/sec @ recall≥90% on 10M clip768, 10k-query batch; % HBM roofline"
 PUBLISHED_QPS_10M = 19.42  # README:17,30 — 514.91 s for 10k queries, EPYC 7532, 1 core
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 F16_PEAK_TFLOPS = 2500.0   # dense fp16 MFMA
 
-SCALES = {"10M": 10_000_000, "1M": 1_000_000, "300K": 300_000, "100K": 100_000}
+SCALES = {"100M": 100_000_000, "10M": 10_000_000, "1M": 1_000_000, "300K": 300_000, "100K": 100_000}
 
 
 def log(*a):
@@ -55,6 +55,23 @@ def build_workload(args, device, rank, world):
     buckets, object labels = router argmax (LearnedIndex.py:240); deterministic."""
     n, C = SCALES[args.scale], args.n_buckets
     t0 = time.time()
+    if args.scale == "100M":
+        # configs[4]: random vectors, k-means buckets; the corpus is generated
+        # chunk by chunk straight into each rank's shard (never whole in HBM)
+        x, q, qn, layers, labels = synth.build_random_workload(n, args.nq, C, args.arch, device,
+                                                               train_steps=args.train_steps)
+        router = DeviceRouter(layers, device=device)
+        torch.cuda.synchronize()
+        log(f"[bench] workload n={n} (random, generated per chunk) in {time.time() - t0:.1f}s")
+        t0 = time.time()
+        index = DeviceIndex(x, labels, C, device=device, chunk_rows=args.chunk_rows, rank=rank,
+                            world=world)
+        torch.cuda.synchronize()
+        log(f"[bench] index (rank {rank}/{world}, {index.n_rows} rows, {index.storage}) "
+            f"in {time.time() - t0:.1f}s; bucket sizes min/median/max = "
+            f"{index.bucket_size.min()}/{int(np.median(index.bucket_size))}/"
+            f"{index.bucket_size.max()}")
+        return x, q, qn, router, index, labels
     x, q, qn, xn, layers = synth.build_lmi_workload(n, args.nq, C, args.arch, device,
                                                     centres=args.centres,
                                                     train_steps=args.train_steps)
@@ -79,8 +96,10 @@ def exact_knn(x, qs, k, chunk=1 << 20):
     qn = qs / qs.norm(dim=1, keepdim=True)
     best_s = torch.full((qs.shape[0], k), -2.0, device=qs.device)
     best_i = torch.zeros((qs.shape[0], k), dtype=torch.int64, device=qs.device)
-    for a in range(0, x.shape[0], chunk):
-        blk = x[a:a + chunk].float()
+    blocks = x.chunks() if isinstance(x, RowSource) else (
+        (a, None, x[a:a + chunk]) for a in range(0, x.shape[0], chunk))
+    for a, _, blk in blocks:
+        blk = blk.float()
         s = qn @ (blk / blk.norm(dim=1, keepdim=True)).T
         v, i = s.topk(k, dim=1)
         cs = torch.cat([best_s, v], 1)
@@ -228,7 +247,8 @@ def main():
             torch.distributed.barrier()
         return
     achieved = byts / (scan_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(scan_ms)
+    # the committed PMC passes profile the default (10M, 1 GPU) command only
+    traffic, traffic_src = pmc_traffic(scan_ms) if (args.scale == "10M" and world == 1) else (None, None)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": None if traffic is None else int(traffic),
@@ -250,7 +270,7 @@ def main():
         "higher_is_better": True, "scaling": "strong",
         "vs_baseline": round(value / PUBLISHED_QPS_10M, 1) if args.scale == "10M" else None,
         "dtype": "f16", "data": "synthetic",
-        "config": {"workload": f"{args.scale} clip768-like synthetic (fp16-exact), {args.n_buckets} "
+        "config": {"workload": f"{args.scale} {'random unit (configs[4])' if args.scale == '100M' else 'clip768-like'} synthetic (fp16-exact), {args.n_buckets} "
                                f"buckets, R={args.R}, k={args.k}, {args.nq} queries, router "
                                f"{args.arch}", "n": SCALES[args.scale], "d": 768, "nq": args.nq,
                    "R": args.R, "k": args.k, "n_buckets": args.n_buckets, "router": args.arch,

@@ -96,6 +96,22 @@ class BucketLayout:
 # ---------------------------------------------------------------------------
 # device index
 # ---------------------------------------------------------------------------
+class RowSource:
+    """A corpus too large to materialise twice (BASELINE configs[4], 100M x 768):
+    ``fn(a, b)`` returns rows [a, b) as an fp16 device tensor [b - a, d] and is
+    called on whole chunks [i·chunk, (i+1)·chunk).  DeviceIndex scatters every
+    chunk straight into its bucket-sorted slots, so HBM holds the shard once."""
+
+    def __init__(self, n: int, d: int, fn, chunk: int = 1 << 20):
+        self.n, self.d, self.fn, self.chunk = int(n), int(d), fn, int(chunk)
+        self.shape = (self.n, self.d)
+
+    def chunks(self):
+        for a in range(0, self.n, self.chunk):
+            b = min(self.n, a + self.chunk)
+            yield a, b, self.fn(a, b)
+
+
 class DeviceIndex:
     """One shard of the bucket-sorted search corpus, resident in HBM."""
 
@@ -119,6 +135,31 @@ class DeviceIndex:
         self.rank, self.world = rank, world
 
         gpos, loc_off = self.layout.shard(rank, world)
+        if isinstance(data, RowSource):
+            self._fill_from_source(data, gpos)
+        else:
+            self._fill(data, gpos, storage)
+        self.gpos = torch.from_numpy(gpos.astype(np.int32)).to(self.device)
+        self.n_rows = int(gpos.size)
+        self.chunk_rows = int(chunk_rows)
+        cf = np.zeros(n_buckets + 1, np.int32)
+        lib = _lib.load()
+        mx = lib.lmi_plan_chunks(loc_off.ctypes.data, n_buckets, self.chunk_rows, cf.ctypes.data)
+        if mx < 0:
+            check("lmi_plan_chunks", -mx)
+        self.max_chunks = int(mx)
+        self.n_chunks = int(cf[-1])
+        self.bucket_off_local = torch.from_numpy(loc_off).to(self.device)
+        self.chunk_first = torch.from_numpy(cf).to(self.device)
+        self.chunk_centroid = None
+        if subcluster and self.n_chunks > 0:
+            self._subcluster_layout(loc_off, cf)
+        self._desc = IndexDescHolder(self)
+        self._ws = {}
+
+    @torch.no_grad()
+    def _fill(self, data, gpos, storage):
+        n = self.n_total
         rows = torch.from_numpy(self.layout.order[gpos])
         src = data if isinstance(data, torch.Tensor) else torch.from_numpy(
             np.ascontiguousarray(np.asarray(data, dtype=np.float32)))
@@ -151,23 +192,38 @@ class DeviceIndex:
             norm = torch.where(norm < eps10, torch.ones_like(norm), norm)
             self.inv_norm[a:a + step] = 1.0 / norm
             del blk, f
-        self.gpos = torch.from_numpy(gpos.astype(np.int32)).to(self.device)
-        self.n_rows = int(gpos.size)
-        self.chunk_rows = int(chunk_rows)
-        cf = np.zeros(n_buckets + 1, np.int32)
-        lib = _lib.load()
-        mx = lib.lmi_plan_chunks(loc_off.ctypes.data, n_buckets, self.chunk_rows, cf.ctypes.data)
-        if mx < 0:
-            check("lmi_plan_chunks", -mx)
-        self.max_chunks = int(mx)
-        self.n_chunks = int(cf[-1])
-        self.bucket_off_local = torch.from_numpy(loc_off).to(self.device)
-        self.chunk_first = torch.from_numpy(cf).to(self.device)
-        self.chunk_centroid = None
-        if subcluster and self.n_chunks > 0:
-            self._subcluster_layout(loc_off, cf)
-        self._desc = IndexDescHolder(self)
-        self._ws = {}
+
+    @torch.no_grad()
+    def _fill_from_source(self, src: "RowSource", gpos):
+        """Scatter every generated chunk into this shard's bucket-sorted slots
+        (fp16 storage; 1/||y|| as sklearn's normalize, zero norms -> 1)."""
+        n = self.n_total
+        if src.n != n:
+            raise ValueError("RowSource must have one row per label")
+        self.d = src.d
+        self.d_pad = (self.d + 31) // 32 * 32
+        self.storage = "f16"
+        n_rows = int(gpos.size)
+        self.corpus = torch.zeros((n_rows, self.d_pad), dtype=torch.float16, device=self.device)
+        self.inv_norm = torch.empty((n_rows,), dtype=torch.float32, device=self.device)
+        slot = torch.full((n,), -1, dtype=torch.int64, device=self.device)
+        slot[torch.from_numpy(self.layout.order[gpos]).to(self.device)] = torch.arange(
+            n_rows, dtype=torch.int64, device=self.device)
+        eps10 = 10 * float(np.finfo(np.float32).eps)
+        for a, b, blk in src.chunks():
+            if blk.dtype != torch.float16 or blk.shape != (b - a, self.d):
+                raise ValueError("RowSource chunks must be fp16 [b - a, d]")
+            sl = slot[a:b]
+            m = sl >= 0
+            dst = sl[m]
+            x = blk[m]
+            self.corpus[dst, : self.d] = x
+            f = x.float()
+            norm = torch.sqrt((f * f).sum(dim=1))
+            norm = torch.where(norm < eps10, torch.ones_like(norm), norm)
+            self.inv_norm[dst] = 1.0 / norm
+            del blk, x, f
+        del slot
 
     @torch.no_grad()
     def _subcluster_layout(self, loc_off, cf, iters: int = 8, seed: int = 1):

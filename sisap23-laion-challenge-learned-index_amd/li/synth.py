@@ -161,3 +161,58 @@ def build_lmi_workload(n: int, nq: int, n_buckets: int, arch: str, device, *, d:
     layers = [(m.weight.detach().cpu(), m.bias.detach().cpu())
               for m in model if isinstance(m, torch.nn.Linear)]
     return x, q, qn, xn, layers
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs[4]: 100M random clip768-shaped vectors, k-means buckets
+# ---------------------------------------------------------------------------
+def random_rows_fn(d: int, seed: int, device, chunk: int = 1 << 20):
+    """Counter-based rows: chunk i = normalised N(0,1) rows from a generator
+    seeded (seed, i), rounded to fp16, so any rank regenerates any chunk."""
+    def fn(a: int, b: int) -> torch.Tensor:
+        if a % chunk:
+            raise ValueError("rows are generated in whole chunks")
+        g = torch.Generator(device=device)
+        g.manual_seed(seed * 1_000_003 + a // chunk)
+        x = torch.randn((b - a, d), generator=g, device=device)
+        x /= x.norm(dim=1, keepdim=True)
+        return x.half()
+    return fn
+
+
+def build_random_workload(n: int, nq: int, n_buckets: int, arch: str, device, *, d: int = 768,
+                          train_steps: int = 200, seed: int = 2023, chunk: int = 1 << 20):
+    """configs[4]: n random unit vectors (fp16-exact), never materialised whole
+    (li.index.RowSource).  Buckets: k-means (li.kmeans, the K5 kernels, faiss's
+    122·256-row training sample) on the pca96 navigation vectors, a router fitted
+    to them on the CPU (reproducible on every rank), object labels = router
+    argmax (K1) chunk by chunk.  Returns (source, q f32, qn f32, layers, labels)."""
+    from .index import DeviceRouter, RowSource
+    from .kmeans import Kmeans
+    fn = random_rows_fn(d, seed, device, chunk)
+    src = RowSource(n, d, fn, chunk)
+    gq = torch.Generator(device=device)
+    gq.manual_seed(seed + 2219)
+    with torch.no_grad():
+        q = torch.randn((nq, d), generator=gq, device=device)
+        q = (q / q.norm(dim=1, keepdim=True)).half().float()
+    g = torch.Generator(device="cpu")
+    g.manual_seed(96)
+    P = (torch.randn((d, 96), generator=g) / math.sqrt(d)).to(device)
+    qn = torch_nav(q, P)
+    n_train = min(n, n_buckets * 256)
+    sub = torch_nav(fn(0, min(n, chunk))[:n_train], P)
+    km = Kmeans(96, n_buckets, niter=20, seed=seed, device=device)
+    km.train(sub)
+    _, lab = km.index.search(sub, 1)
+    with torch.random.fork_rng(devices=[]):
+        model = train_router(sub.cpu(), torch.from_numpy(lab[:, 0]), ARCHS[arch], n_buckets,
+                             steps=train_steps, batch=2048, seed=seed)
+    layers = [(m.weight.detach().cpu(), m.bias.detach().cpu())
+              for m in model if isinstance(m, torch.nn.Linear)]
+    router = DeviceRouter(layers, device=device)
+    labels = torch.empty(n, dtype=torch.int32, device=device)
+    for a, b, blk in src.chunks():
+        labels[a:b] = router.argmax(torch_nav(blk, P)).to(torch.int32)
+        del blk
+    return src, q, qn, layers, labels

@@ -145,3 +145,22 @@ def test_router_mfma_matches_fma_path(hidden, monkeypatch):
         assert _router_mismatch(cls, logits, 7) == 0
     np.testing.assert_allclose(p_m.cpu().numpy(), p_f.cpu().numpy(), rtol=1e-5, atol=1e-7)
     assert (am_m != am_f).sum() <= 1
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_row_source_index_equals_tensor_index(world):
+    """configs[4]'s generated corpus (li.index.RowSource, chunks scattered into
+    the shard) lays out exactly the index built from the whole tensor."""
+    from li import synth
+    from li.index import RowSource
+    n, d, ch = 5000, 96, 1024
+    fn = synth.random_rows_fn(d, 7, "cuda", chunk=ch)
+    x = torch.cat([fn(a, min(n, a + ch)) for a in range(0, n, ch)])
+    labels = torch.from_numpy(np.random.default_rng(3).integers(0, 9, n).astype(np.int32))
+    for rank in range(world):
+        a = DeviceIndex(x, labels, 9, chunk_rows=512, rank=rank, world=world, device="cuda")
+        b = DeviceIndex(RowSource(n, d, fn, ch), labels, 9, chunk_rows=512, rank=rank, world=world,
+                        device="cuda")
+        assert a.storage == b.storage == "f16" and a.n_rows == b.n_rows
+        assert torch.equal(a.corpus, b.corpus) and torch.equal(a.inv_norm, b.inv_norm)
+        assert torch.equal(a.gpos, b.gpos) and torch.equal(a.chunk_first, b.chunk_first)
