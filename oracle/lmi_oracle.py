@@ -475,3 +475,23 @@ def kmeans_train(x: np.ndarray, k: int, *, niter: int = 25, seed: int = 1234,
         cent, cnt = kmeans_update(xt, lab, cent)
         kmeans_split_empty(cent, cnt, n, rng)
     return cent, obj
+
+
+def search_exact(labels, ids, data_search, queries_search, classes, n_buckets, R, k=10):
+    """The `semantics="exact"` option (not a reference behaviour; SURVEY.md
+    §8(a) asks for it beside the reference semantics): per query, the exact
+    top-k by (distance, bucket-sorted position) over the union of its R probed
+    buckets, ids 1-based as DataFrame.index, padded with (10000, 0)."""
+    order, _ = layout(labels, n_buckets)
+    d, p = bucket_lists(labels, data_search, queries_search, classes, R, k, n_buckets)
+    nq = d.shape[0]
+    out_d = np.full((nq, k), FILL, np.float64)
+    out_a = np.zeros((nq, k), np.uint32)
+    for q in range(nq):
+        dd, pp = d[q].ravel(), p[q].ravel()
+        m = pp >= 0
+        dd, pp = dd[m], pp[m]
+        o = np.lexsort((pp, dd))[:k]
+        out_d[q, : o.size] = dd[o]
+        out_a[q, : o.size] = np.asarray(ids)[order[pp[o]]]
+    return out_d, out_a

@@ -84,8 +84,10 @@ class LearnedIndex(Logger):
 
     # ---- search -------------------------------------------------------------
     def search(self, data_navigation, queries_navigation, data_search, queries_search,
-               pred_categories, n_buckets=1, k=10, use_threshold=False):
-        """Search for k nearest neighbors of each query (LearnedIndex.py:22-101)."""
+               pred_categories, n_buckets=1, k=10, use_threshold=False, semantics="reference"):
+        """Search for k nearest neighbors of each query (LearnedIndex.py:22-101).
+        `semantics="exact"` (an addition; default off) returns the exact top-k of
+        the union of the probed buckets instead of the reference's round merge."""
         from .index import Searcher
         assert self.model is not None, 'Model is not trained, call `build` first.'
         data_navigation['category'] = pred_categories   # :67 (caller-visible side effect)
@@ -94,7 +96,7 @@ class LearnedIndex(Logger):
         q_nav = data_X_to_torch(queries_navigation).to(index.device)
         q_search = torch.from_numpy(np.ascontiguousarray(queries_search, dtype=np.float32)).to(index.device)
         return Searcher(index, router).search(q_nav, q_search, n_buckets, k=k, k_round=10,
-                                              use_threshold=use_threshold)
+                                              use_threshold=use_threshold, semantics=semantics)
 
     def search_single(self, data_navigation, data_search, queries_search, pred_categories,
                       k=10, threshold_dist=None):

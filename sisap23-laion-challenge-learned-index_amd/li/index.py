@@ -531,8 +531,16 @@ class Searcher:
 
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
                use_threshold: bool = True, classes: Optional[torch.Tensor] = None,
-               timings: Optional[dict] = None, replay_on: str = "device"):
+               timings: Optional[dict] = None, replay_on: str = "device",
+               semantics: str = "reference"):
         """Whole hot path for one batch -> (dists f64 [nq, w], anns u32 [nq, w]).
+
+        semantics="reference" (default) reproduces LearnedIndex.search's round
+        merge (thresholds, fillers, the <k quirk).
+        semantics="exact" returns instead the exact top-k, by (distance, id
+        position), of the union of each query's R probed buckets (K3 merge of
+        its R lists on the device; fewer than k objects pad with (10000, 0)),
+        the option SURVEY.md §8(a) asks for beside the reference semantics.
 
         replay_on="device" (default) runs the reference's round merge on the GPU
         (lmi_replay_device) and copies back only the result; "host" copies the
@@ -542,7 +550,11 @@ class Searcher:
         import time
         if replay_on not in ("device", "host"):
             raise ValueError("replay_on must be 'device' or 'host'")
-        k_list = k_round
+        if semantics not in ("reference", "exact"):
+            raise ValueError("semantics must be 'reference' or 'exact'")
+        k_list = k_round if semantics == "reference" else max(k_round, k)
+        if k_list > _lib.LMI_MAX_K:
+            raise ValueError(f"k={k_list} > {_lib.LMI_MAX_K}")
         dev = self.index.device
         sync = (lambda: torch.cuda.current_stream(dev).synchronize()) if timings is not None else None
 
@@ -569,6 +581,35 @@ class Searcher:
         t0 = lap("scan", t0)
         nq = classes.shape[0]
         h_st = self._host("st", (2,), torch.int32)
+        if semantics == "exact":
+            _, p2id = self._device_tables()
+
+            def exact(d, pos):
+                Rr = classes.shape[1]
+                md, mp = merge_topk(d.view(nq, Rr, k_list).transpose(0, 1).contiguous(),
+                                    pos.view(nq, Rr, k_list).transpose(0, 1).contiguous(), k_list)
+                md, mp = md[:, :k], mp[:, :k]
+                none = mp < 0
+                ids = p2id[mp.clamp(min=0).long()]
+                return (torch.where(none, torch.full_like(md, 10000.0), md).double(),
+                        torch.where(none, torch.zeros_like(ids), ids).to(torch.int32))
+
+            rd, ra = exact(d, pos)
+            t0 = lap("replay", t0)
+            h_d = self._host("xd", tuple(rd.shape), torch.float64)
+            h_a = self._host("xa", tuple(ra.shape), torch.int32)
+            h_d.copy_(rd, non_blocking=True)
+            h_a.copy_(ra, non_blocking=True)
+            h_st[0:1].copy_(status, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            t0 = lap("d2h", t0)
+            if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL:
+                raise RuntimeError(f"search: internal status {int(h_st[0])}")
+            if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
+                rd, ra = exact(*scan(qmode=_lib.LMI_Q_F32)[:2])
+                h_d.copy_(rd)
+                h_a.copy_(ra)
+            return h_d.numpy().copy(), h_a.numpy().view(np.uint32).copy()
         if replay_on == "device":
             bsz, p2id = self._device_tables()
 

@@ -55,7 +55,7 @@ def _synthetic(n, nq=10_000):
 
 def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc=None,
         n_categories=None, epochs=100, model_type='MLP', lr=0.1, preprocess=False, save=False,
-        synthetic=0):
+        synthetic=0, semantics='reference'):
     n_buckets_perc = [int((b / 100) * n_categories) for b in n_buckets_perc]   # search.py:37-38
     n_buckets_perc = list(set([b for b in n_buckets_perc if b > 0]))
     LOG.info(f'Running with: kind={kind}, key={key}, size={size}, n_buckets_perc={n_buckets_perc}, '
@@ -97,7 +97,7 @@ def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc
             dists, nns = li.search(data_navigation=data, queries_navigation=queries,
                                    data_search=data_search, queries_search=queries_search,
                                    pred_categories=pred_categories, n_buckets=bucket, k=k,
-                                   use_threshold=True)
+                                   use_threshold=True, semantics=semantics)
         else:
             _, pred_proba_categories = li.model.predict_proba(data_X_to_torch(queries))
             data['category'] = pred_categories
@@ -131,8 +131,11 @@ if __name__ == "__main__":
     parser.add_argument("--save", default=False, type=bool, help='Whether to save the model or not')
     parser.add_argument("--synthetic", default=0, type=int,
                         help='run on N synthetic rows instead of data/ (this build has no network)')
+    parser.add_argument("--semantics", default="reference", choices=["reference", "exact"],
+                        help='reference: LearnedIndex.search round merge (default); exact: exact '
+                             'top-k over the probed buckets')
     args = parser.parse_args()
     assert args.size in ['100K', '300K', '10M', '30M', '100M']
     run(args.dataset, args.emb, args.size, args.k, 'learned-index',
         [int(b) for b in args.buckets_perc], args.n_categories, args.epochs, args.model_type,
-        args.lr, args.preprocess, args.save, synthetic=args.synthetic)
+        args.lr, args.preprocess, args.save, synthetic=args.synthetic, semantics=args.semantics)

@@ -164,3 +164,18 @@ def test_row_source_index_equals_tensor_index(world):
         assert a.storage == b.storage == "f16" and a.n_rows == b.n_rows
         assert torch.equal(a.corpus, b.corpus) and torch.equal(a.inv_norm, b.inv_norm)
         assert torch.equal(a.gpos, b.gpos) and torch.equal(a.chunk_first, b.chunk_first)
+
+
+@pytest.mark.parametrize("label_mode,R,k", [("router", 4, 10), ("skewed", 3, 7), ("dup", 5, 16)])
+def test_exact_semantics_matches_oracle(label_mode, R, k):
+    """semantics="exact": exact top-k over the union of the R probed buckets."""
+    w = workloads.clustered(n=4000, nq=150, C=16, seed=23, label_mode=label_mode)
+    ids = np.arange(1, w["x"].shape[0] + 1)
+    s = Searcher(DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=512, device="cuda"),
+                 DeviceRouter(w["layers"], device="cuda"))
+    d, a = s.search(torch.from_numpy(w["qn"]).cuda(), torch.from_numpy(w["q"]).cuda(), R, k=k,
+                    semantics="exact")
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    rd, ra = O.search_exact(w["labels"], ids, w["x"], w["q"], classes, w["C"], R, k)
+    assert d.shape == (150, k) and a.dtype == np.uint32
+    assert O.compare_lists(rd, ra, d, a) == 0
