@@ -179,3 +179,50 @@ def test_exact_semantics_matches_oracle(label_mode, R, k):
     rd, ra = O.search_exact(w["labels"], ids, w["x"], w["q"], classes, w["C"], R, k)
     assert d.shape == (150, k) and a.dtype == np.uint32
     assert O.compare_lists(rd, ra, d, a) == 0
+
+
+def test_full_size_10m_properties():
+    """BASELINE configs[2] at full size (10M x 768 fp16, 122 buckets, 10k
+    queries, R = 4): K2's per-(query, probe) lists on a sample of queries equal
+    an independent torch fp32 brute force over the same bucket rows, and the
+    whole search output has the reference's shape invariants (ascending rows,
+    ids in range, distances = recomputed 1 - cos of the returned ids)."""
+    from li import synth
+    dev = torch.device("cuda")
+    x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
+    router = DeviceRouter(layers, device=dev)
+    labels = router.argmax(xn)
+    del xn
+    ix = DeviceIndex(x, labels, 122, chunk_rows=8192, device=dev)
+    classes, _ = router.topr(qn, 4)
+    d, pos, st = bucket_topk(ix, q, classes, 10)
+    assert int(st.item()) == 0
+    d, pos = d.cpu().numpy(), pos.cpu().numpy()
+    assert np.all(np.diff(d, axis=2) >= 0)
+    off = ix.bucket_off_local.cpu().numpy()
+    cls = classes.cpu().numpy()
+    rng = np.random.default_rng(0)
+    qs = rng.choice(10_000, 48, replace=False)
+    qh = q[qs].float()
+    qh = qh / qh.norm(dim=1, keepdim=True)
+    for i, qi in enumerate(qs):
+        for r in range(4):
+            c = cls[qi, r]
+            a, b = int(off[c]), int(off[c + 1])
+            assert ((pos[qi, r] >= a) & (pos[qi, r] < b)).all()
+            y = ix.corpus[a:b, :768].float() * ix.inv_norm[a:b, None]
+            dd = (1.0 - y @ qh[i]).double().cpu().numpy()
+            o = np.lexsort((np.arange(b - a), dd))[:10]
+            np.testing.assert_allclose(d[qi, r], dd[o], atol=2e-6)
+            assert O.compare_lists(dd[o][None], o[None] + a, d[qi, r][None], pos[qi, r][None]) == 0
+    s = Searcher(ix, router)
+    dists, anns = s.search(qn, q, 4, k=10)
+    assert dists.shape == (10_000, 10) and anns.dtype == np.uint32
+    assert np.all(np.diff(dists, axis=1) >= 0)
+    assert anns.max() <= 10_000_000
+    ids = torch.from_numpy(anns[qs].astype(np.int64) - 1).to(dev)
+    y = x[ids.clamp(min=0)].float()
+    y = y / y.norm(dim=2, keepdim=True)
+    dd = (1.0 - (y * qh[:, None, :]).sum(2)).double().cpu().numpy()
+    live = anns[qs] > 0
+    np.testing.assert_allclose(dists[qs][live], dd[live], atol=1e-5)
