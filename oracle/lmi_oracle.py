@@ -380,7 +380,7 @@ def compare_lists(d_a, p_a, d_b, p_b, *, atol=1e-5, tie=1e-6):
 # init) in tests/test_kmeans.py, and the GPU kernels (csrc/lmi_kmeans.hip)
 # are checked bit for bit against the functions below.
 # ---------------------------------------------------------------------------
-KMEANS_SLICES = 256
+KMEANS_SLICES = 512
 KMEANS_EPS = np.float32(1.0 / 1024.0)
 
 
@@ -399,7 +399,7 @@ def kmeans_assign(x: np.ndarray, cent: np.ndarray):
 
 
 def kmeans_slices(n: int) -> int:
-    return int(max(1, min(KMEANS_SLICES, (n + 1023) // 1024)))
+    return int(max(1, min(KMEANS_SLICES, (n + 127) // 128)))
 
 
 def kmeans_update(x: np.ndarray, labels: np.ndarray, cent: np.ndarray):

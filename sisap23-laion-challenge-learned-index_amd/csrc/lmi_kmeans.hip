@@ -31,7 +31,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kCentLds = 16384;  // floats of the LDS centroid tile (64 KiB)
-constexpr int kSlices = 256;     // fixed partition of the points for the sums
+constexpr int kSlices = 512;     // fixed partition of the points for the sums (<= 512 slices of >= 128 points)
 
 // #pragma clang fp contract(off) keeps a*b+c as two rounded operations
 template <int DP>
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_reduce_kernel(
 }
 
 int slices_for(int64_t n) {
-    const int64_t s = (n + 1023) / 1024;
+    const int64_t s = (n + 127) / 128;
     return (int)(s < 1 ? 1 : (s > kSlices ? kSlices : s));
 }
 
