@@ -437,16 +437,31 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
                                                           double* __restrict__ Fd_out,
                                                           int32_t* __restrict__ Fp_out,
                                                           const double* __restrict__ dr_d,
-                                                          const int32_t* __restrict__ dr_p) {
+                                                          const int32_t* __restrict__ dr_p,
+                                                          double* __restrict__ thr_next,
+                                                          double* __restrict__ drd_next,
+                                                          int32_t* __restrict__ drp_next) {
+    // fused prologue of the next round (replay_thr_kernel's mode 2): its row
+    // buffers (the other pair) reset to (10000, -1), and its threshold
+    // max(F_q) written by the thread that places F's last element
     const int n = first ? kr : wF + kr;
     const int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x;
     if (t >= (int64_t)nq * n) return;
     const int q = (int)(t / n), j = (int)(t - (int64_t)q * n);
     const double* fd = Fd + (size_t)q * fs;
     const double* dd = dr_d + (size_t)q * kr;
+    if (drd_next && j < kr) {
+        drd_next[(size_t)q * kr + j] = kFill;
+        drp_next[(size_t)q * kr + j] = -1;
+    }
     if (first) {
         Fd_out[(size_t)q * fs + j] = dd[j];
         Fp_out[(size_t)q * fs + j] = dr_p[(size_t)q * kr + j];
+        if (thr_next && j == 0) {  // round 0's row need not be ascending (the <k quirk)
+            double m = dd[0];
+            for (int i = 1; i < kr; ++i) m = fmax(m, dd[i]);
+            thr_next[q] = m;
+        }
         return;
     }
     const double dj = j < wF ? fd[j] : dd[j - wF];
@@ -463,6 +478,7 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
         Fd_out[(size_t)q * fs + rank] = dj;
         Fp_out[(size_t)q * fs + rank] = j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF];
     }
+    if (thr_next && rank == wn - 1) thr_next[q] = dj;  // the merged row is ascending
 }
 
 __global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, int32_t fs,
@@ -489,7 +505,7 @@ __global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, i
 }
 
 struct ReplayWs {
-    size_t groups, Fd[2], Fp[2], drd, drp, thr, uraw, total;
+    size_t groups, Fd[2], Fp[2], drd[2], drp[2], thr, uraw, total;
 };
 
 ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
@@ -506,8 +522,10 @@ ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
         s.Fd[b] = take((size_t)nq * fs * 8);
         s.Fp[b] = take((size_t)nq * fs * 4);
     }
-    s.drd = take((size_t)nq * kr * 8);
-    s.drp = take((size_t)nq * kr * 4);
+    for (int b = 0; b < 2; ++b) {  // round r's rows live in buffer r & 1
+        s.drd[b] = take((size_t)nq * kr * 8);
+        s.drp[b] = take((size_t)nq * kr * 4);
+    }
     s.thr = take((size_t)nq * 8);
     s.uraw = take((size_t)nq * kl * 4);
     s.total = off;
@@ -567,10 +585,13 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
         int32_t* Fp = (int32_t*)(ws + s.Fp[cur]);
         const bool thresholded = ((r > 0) && use_threshold) || (r == 0 && thr_round0);
         const int mode = (r == 0 && thr_round0) ? 1 : (thresholded ? 2 : 0);
-        hipLaunchKernelGGL(replay_thr_kernel, qgrid, dim3(kT), 0, st, nq, k_round, fs, wF, mode, Fd,
-                           thr_round0, (double*)(ws + s.thr), (double*)(ws + s.drd),
-                           (int32_t*)(ws + s.drp));
-        LMI_LAUNCH_CHECK("replay_thr_kernel");
+        double* drd = (double*)(ws + s.drd[r & 1]);
+        int32_t* drp = (int32_t*)(ws + s.drp[r & 1]);
+        if (r == 0) {  // later rounds: fused into the previous round's merge
+            hipLaunchKernelGGL(replay_thr_kernel, qgrid, dim3(kT), 0, st, nq, k_round, fs, wF, mode,
+                               Fd, thr_round0, (double*)(ws + s.thr), drd, drp);
+            LMI_LAUNCH_CHECK("replay_thr_kernel");
+        }
         RoundArgs a{};
         a.classes = classes;
         a.nq = nq;
@@ -585,8 +606,8 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
         a.groups = groups;
         a.thresholded = thresholded ? 1 : 0;
         a.thr = (const double*)(ws + s.thr);
-        a.dr_d = (double*)(ws + s.drd);
-        a.dr_p = (int32_t*)(ws + s.drp);
+        a.dr_d = drd;
+        a.dr_p = drp;
         a.uraw = (int32_t*)(ws + s.uraw);
         a.status = status;
 #ifdef LMI_ABLATION
@@ -594,13 +615,16 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
 #endif
         hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, a);
         LMI_LAUNCH_CHECK("replay_group_kernel");
+        const bool last = r + 1 == R;
         const int wn = (r == 0) ? k_round : std::min(k_final, wF + k_round);
         const int n = (r == 0) ? k_round : wF + k_round;
         const dim3 mgrid((unsigned)(((int64_t)nq * n + kT - 1) / kT));
         hipLaunchKernelGGL(replay_merge_kernel, mgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
                            r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
-                           (int32_t*)(ws + s.Fp[cur ^ 1]), (const double*)(ws + s.drd),
-                           (const int32_t*)(ws + s.drp));
+                           (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp,
+                           last ? nullptr : (double*)(ws + s.thr),
+                           last ? nullptr : (double*)(ws + s.drd[(r + 1) & 1]),
+                           last ? nullptr : (int32_t*)(ws + s.drp[(r + 1) & 1]));
         LMI_LAUNCH_CHECK("replay_merge_kernel");
         cur ^= 1;
         wF = wn;
