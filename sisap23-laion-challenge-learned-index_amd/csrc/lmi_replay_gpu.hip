@@ -244,16 +244,37 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
         // (a global member among the smallest `want` is among its share's)
         const int lane = tid & 63, wv = tid >> 6;
         int prev = -1, cnt = 0;
-        for (; cnt < want; ++cnt) {
-            int m = INT32_MAX;
-            for (int e = wv * 64 + lane; e < nU; e += kTG) {
-                const int32_t p = U[e];
-                if (p > prev && p < m) m = p;
+        constexpr int kUReg = kUCap / kTG;  // share entries a lane keeps in registers
+        if (nU <= kUReg * kTG) {
+            // the lane's share read once; the `want` rounds then run on registers
+            int uc[kUReg];
+#pragma unroll
+            for (int i = 0; i < kUReg; ++i) {
+                const int e = wv * 64 + lane + i * kTG;
+                uc[i] = e < nU ? U[e] : INT32_MAX;
             }
-            m = wave_min_i(m);
-            if (m == INT32_MAX) break;
-            if (lane == 0) Sw[wv][cnt] = m;
-            prev = m;
+            for (; cnt < want; ++cnt) {
+                int m = INT32_MAX;
+#pragma unroll
+                for (int i = 0; i < kUReg; ++i)
+                    if (uc[i] > prev && uc[i] < m) m = uc[i];
+                m = wave_min_i(m);
+                if (m == INT32_MAX) break;
+                if (lane == 0) Sw[wv][cnt] = m;
+                prev = m;
+            }
+        } else {
+            for (; cnt < want; ++cnt) {
+                int m = INT32_MAX;
+                for (int e = wv * 64 + lane; e < nU; e += kTG) {
+                    const int32_t p = U[e];
+                    if (p > prev && p < m) m = p;
+                }
+                m = wave_min_i(m);
+                if (m == INT32_MAX) break;
+                if (lane == 0) Sw[wv][cnt] = m;
+                prev = m;
+            }
         }
         if (lane == 0) nsw[wv] = cnt;
         __syncthreads();
