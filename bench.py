@@ -239,6 +239,9 @@ def main():
     for _ in range(3):
         searcher.search(qn, q, args.R, k=args.k, use_threshold=True, timings=tm)
     breakdown = {kk: round(v / 3, 3) for kk, v in tm.items()}
+    # the optional exact-top-k semantics over the same probed buckets (untimed;
+    # every rank takes part: with G > 1 the search has collectives)
+    _, anns_x = searcher.search(qn, q, args.R, k=args.k, semantics="exact")
     classes, _ = router.topr(qn, args.R)
     classes = classes.cpu().numpy()
     byts, flops, rows = algorithmic_bytes(index, classes, args.nq)
@@ -261,8 +264,6 @@ def main():
     truth = exact_knn(x, q[:sample], args.k)
     recall = float(np.mean([len(set(anns[i][: args.k]) & set(truth[i])) / args.k
                             for i in range(sample)]))
-    # the optional exact-top-k semantics over the same probed buckets (untimed)
-    _, anns_x = searcher.search(qn, q, args.R, k=args.k, semantics="exact")
     recall_x = float(np.mean([len(set(anns_x[i][: args.k]) & set(truth[i])) / args.k
                               for i in range(sample)]))
     cpu = None
