@@ -228,7 +228,8 @@ def main():
     n_ev = lib.lmi_timing_read(ms, args.steps)
     scan_ms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
+        t = torch.tensor([el], dtype=torch.float64,
+                         device=device if torch.distributed.get_backend() == "nccl" else "cpu")
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         el = float(t.item())
     ms_step = el / args.steps * 1e3

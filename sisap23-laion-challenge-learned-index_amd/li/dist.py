@@ -32,12 +32,25 @@ def init_from_env(backend: Optional[str] = None):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # LMI_DIST_BACKEND=gloo: control-flow rehearsal of several ranks on one
+        # GPU (RCCL refuses two ranks on one device); collectives then stage
+        # through host memory (_all_gather).  The product path is RCCL.
+        backend = os.environ.get("LMI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
         dist.init_process_group(backend=backend, rank=rank, world_size=world)
     return rank, world, local
+
+
+def _all_gather(out: torch.Tensor, part: torch.Tensor, group=None):
+    """all_gather_into_tensor; device tensors go through host copies on gloo."""
+    if part.is_cuda and dist.get_backend(group) == "gloo":
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, part.cpu(), group=group)
+        out.copy_(h)
+        return
+    dist.all_gather_into_tensor(out, part, group=group)
 
 
 def all_gather_lists(d: torch.Tensor, pos: torch.Tensor, group=None):
@@ -47,7 +60,7 @@ def all_gather_lists(d: torch.Tensor, pos: torch.Tensor, group=None):
     both = torch.stack((d.contiguous().view(torch.int32), pos.to(torch.int32).contiguous()), dim=-1)
     # concatenated along dim 0 (the form both RCCL and gloo accept), viewed [G, ...]
     out = torch.empty((G * both.shape[0],) + tuple(both.shape[1:]), dtype=both.dtype, device=both.device)
-    dist.all_gather_into_tensor(out, both, group=group)
+    _all_gather(out, both, group)
     out = out.view((G,) + tuple(both.shape))
     gd = out[..., 0].contiguous().view(torch.float32)
     gp = out[..., 1].contiguous().to(pos.dtype)
@@ -82,5 +95,5 @@ def route_sharded(router, q_nav: torch.Tensor, R: int, group=None) -> torch.Tens
         c, _ = router.topr(q_nav[lo:hi], R)
         part[: hi - lo] = c
     out = torch.empty((G * per, R), dtype=torch.int32, device=q_nav.device)
-    dist.all_gather_into_tensor(out, part, group=group)
+    _all_gather(out, part, group)
     return out[:nq]
