@@ -175,6 +175,12 @@ def pmc_traffic(kernel_ms):
 
 
 def main():
+    # Libraries print banners to stdout (RCCL's version block at communicator
+    # init): fd 1 goes to stderr for the run, and only the JSON line is written
+    # to the original stdout.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -286,7 +292,7 @@ def main():
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
         "recall_sample": sample, "breakdown_ms": breakdown,
     }
-    print(json.dumps(out), flush=True)
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         torch.distributed.barrier()
 
