@@ -12,16 +12,23 @@ from li.index import DeviceIndex, DeviceRouter, Searcher
 ap = argparse.ArgumentParser()
 ap.add_argument("--worlds", default="1,8")
 ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--chunk", type=int, default=0, help="chunk rows (0: the bench default by world)")
+ap.add_argument("--scale", default="10M", choices=["10M", "100M"],
+                help="100M: configs[4] random vectors, generated per chunk into the shard (li.index.RowSource)")
 a = ap.parse_args()
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1"); os.environ.setdefault("MASTER_PORT", "29533")
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1)
 dev = torch.device("cuda", 0)
-x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
-router = DeviceRouter(layers)
-labels = router.argmax(xn); del xn
+if a.scale == "100M":
+    x, q, qn, layers, labels = synth.build_random_workload(100_000_000, 10_000, 122, "MLP-5", dev)
+    router = DeviceRouter(layers)
+else:
+    x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
+    router = DeviceRouter(layers)
+    labels = router.argmax(xn); del xn
 for W in map(int, a.worlds.split(",")):
-    ck = 8192 if W == 1 else 4096 if W <= 4 else 2048
+    ck = a.chunk or (8192 if W == 1 else 4096 if W <= 4 else 2048)
     ix = DeviceIndex(x, labels, 122, chunk_rows=ck, rank=0, world=W)
     s = Searcher(ix, router)
     for _ in range(3):
