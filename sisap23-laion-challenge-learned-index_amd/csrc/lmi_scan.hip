@@ -221,6 +221,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
             for (int x = 0; x < kGroups; ++x) {
                 meta[x] = goff[x];
                 meta[kGroups + x] = g0_all[x] + gr_all[x];
+                meta[2 * kGroups + 1 + x] = g0_all[x];  // the group's chunk-0 (seed) tiles
                 work[x] = 0;
             }
             meta[2 * kGroups] = acc;
@@ -292,6 +293,57 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
         }
         tiles[pos] = t;
     }
+}
+
+// Tail balance: in every group queue the tiles after the seeds are stably
+// partitioned, heavy first, so the light ones (a partial chunk or a partial
+// query block: under half a full tile's rows x waves) run last, when the CUs
+// start to run dry.  Only the order changes (results are order-independent).
+__global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ tiles,
+                                                          Tile* __restrict__ tmp,
+                                                          const int32_t* __restrict__ meta,
+                                                          const int64_t* __restrict__ bucket_off,
+                                                          int32_t chunk_rows, int32_t QB) {
+    __shared__ int wc[16];
+    const int x = blockIdx.x;
+    const int seeds = meta[2 * kGroups + 1 + x];
+    const int base = meta[x] + seeds;
+    const int n = meta[kGroups + x] - seeds;
+    if (n <= 1) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t full = (int64_t)chunk_rows * ((QB + 31) / 32);
+    int heavy_off = 0, light_off = 0;
+    for (int b0 = 0; b0 < n; b0 += 1024) {
+        const int i = b0 + tid;
+        Tile t{};
+        bool heavy = false;
+        if (i < n) {
+            t = tiles[base + i];
+            const int64_t r0 = bucket_off[t.c] + (int64_t)t.chunk * chunk_rows;
+            const int64_t rows = min((int64_t)chunk_rows, bucket_off[t.c + 1] - r0);
+            heavy = 2 * rows * ((t.np + 31) / 32) >= full;
+        }
+        const uint64_t mh = __ballot(i < n && heavy), ml = __ballot(i < n && !heavy);
+        if (lane == 0) wc[w] = __popcll(mh);
+        __syncthreads();  // (every read of this block is done: heavy writes land at or below it)
+        int hb = 0, ht = 0;
+        for (int v = 0; v < 16; ++v) {
+            hb += (v < w) ? wc[v] : 0;
+            ht += wc[v];
+        }
+        const int nb = min(1024, n - b0);
+        const int lb = (w * 64 - hb);  // light entries in the waves before this one (all full)
+        const uint64_t lt = (1ull << lane) - 1ull;
+        if (i < n) {
+            if (heavy) tiles[base + heavy_off + hb + __popcll(mh & lt)] = t;
+            else tmp[light_off + lb + __popcll(ml & lt)] = t;
+        }
+        heavy_off += ht;
+        light_off += nb - ht;
+        __syncthreads();
+    }
+    __threadfence_block();
+    for (int i = tid; i < light_off; i += 1024) tiles[base + heavy_off + i] = tmp[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -1603,7 +1655,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
 // host side
 // ---------------------------------------------------------------------------
 struct WsLayout {
-    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, ntiles, work, partial, thr_g, pref,
+    size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, tiles_tmp, ntiles, work, partial, thr_g, pref,
         pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
     int32_t qb;      // queries per tile
@@ -1648,7 +1700,8 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     const size_t mt = (P / QB + 1) * (size_t)std::max(idx->max_chunks, 1) + (size_t)idx->n_chunks;
     w.max_tiles = (int32_t)std::min<size_t>(mt, (size_t)INT32_MAX);
     w.tiles = take((size_t)w.max_tiles * sizeof(Tile));
-    w.ntiles = take(4 * (2 * kGroups + 1));
+    w.tiles_tmp = take((size_t)w.max_tiles * sizeof(Tile));
+    w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));
     w.partial = take(P * (size_t)std::max(idx->max_chunks, 1) * KL * sizeof(uint64_t));
     w.thr_g = take(P * sizeof(uint64_t));
@@ -1914,6 +1967,11 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
                        idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !getenv("LMI_SCAN_NO_PREF");
+    if (!nearest_first && env_int("LMI_SCAN_ORDER", 1, 0, 1)) {
+        hipLaunchKernelGGL(tile_order_kernel, dim3(ng), dim3(1024), 0, s, tiles, (Tile*)(ws + w.tiles_tmp),
+                           meta, idx->bucket_off, idx->chunk_rows, QB);
+        LMI_LAUNCH_CHECK("tile_order_kernel");
+    }
     if (nearest_first) {
         int32_t* pref = (int32_t*)(ws + w.pref);
         int32_t* n_seed = (int32_t*)(ws + w.n_seed);
