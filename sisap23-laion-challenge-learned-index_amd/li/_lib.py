@@ -167,6 +167,19 @@ def ptr(t) -> int:
     return t.ctypes.data  # numpy
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_handle(device=None) -> int:
-    """hipStream_t of torch's current stream on `device`."""
+    """hipStream_t of torch's current stream on `device` (the raw-pointer query
+    when torch has it: a few microseconds cheaper per call on the hot path)."""
+    if _raw_stream is not None:
+        if device is None:
+            idx = torch.cuda.current_device()
+        elif isinstance(device, int):
+            idx = device
+        else:
+            d = torch.device(device)
+            idx = d.index if d.index is not None else torch.cuda.current_device()
+        return _raw_stream(idx)
     return torch.cuda.current_stream(device).cuda_stream

@@ -619,8 +619,11 @@ class Searcher:
 
             rd, ra, rst = run_replay(d, pos)
             t0 = lap("replay", t0)
-            h_d = self._host("rd", tuple(rd.shape), torch.float64)
-            h_a = self._host("ra", tuple(ra.shape), torch.int32)
+            # fresh pinned outputs from torch's caching host allocator: handed
+            # to the caller as they are (no host copy; a buffer returns to the
+            # cache when the caller drops the arrays)
+            h_d = torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True)
+            h_a = torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True)
             h_d.copy_(rd, non_blocking=True)
             h_a.copy_(ra, non_blocking=True)
             h_st[0:1].copy_(status, non_blocking=True)
@@ -635,7 +638,7 @@ class Searcher:
                 rd, ra, rst = run_replay(d, pos)
                 h_d.copy_(rd)
                 h_a.copy_(ra)
-            return h_d.numpy().copy(), h_a.numpy().view(np.uint32).copy()
+            return h_d.numpy(), h_a.numpy().view(np.uint32)
         h_cls = self._host("cls", (nq, R), torch.int32)
         h_d = self._host("d", tuple(d.shape), torch.float32)
         h_pos = self._host("pos", tuple(pos.shape), torch.int32)
