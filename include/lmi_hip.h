@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 3
+#define LMI_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -145,6 +145,39 @@ int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32
 int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
                    int32_t k, float* out_d, int32_t* out_pos, void* stream);
 
+/* ---- float64 distances (ABI 4) ---------------------------------------- */
+/* The reference computes 1 - cosine_similarity in float32 only when BOTH
+ * operands are float32; otherwise — the real data: clip768 'emb' is float16 —
+ * sklearn promotes to float64 (utils.py:11, :19; check_pairwise_arrays) and
+ * the threshold test (utils.py:23) and the merges (LearnedIndex.py:86-97) see
+ * float64 values.  lmi_bucket_topk_f64 returns those float64 lists:
+ *   - the fp32 scan keeps the top-KL (KL = 16 > k) per (query, probe);
+ *   - every list entry within 2*eps of the fp32 k-th distance is recomputed
+ *     in float64 from the stored row (sklearn normalize + dot; exact fp16
+ *     inputs), sorted by (d64, position); with fewer than KL entries in that
+ *     band the result is the exact float64 top-k whenever eps bounds the fp32
+ *     error |d32 - d64| (LMI_REFINE_EPS is 40x the largest error measured);
+ *   - pairs whose band fills the list are recomputed in float64 over their
+ *     whole bucket shard (exact, rare: ties or near-ties of > KL-k objects).
+ * Same arguments and layout as lmi_bucket_topk; out_d is float64 [nq][R][k]
+ * (+inf past the bucket's size), out_pos global positions (-1 past it).
+ * 1 <= k <= LMI_MAX_K, d <= 1024. */
+#define LMI_REFINE_EPS 1.52587890625e-05 /* 2^-16 */
+size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
+                                    int32_t k, int32_t qmode);
+int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                        const int32_t* classes, int32_t R, int32_t k, int32_t qmode, double eps,
+                        double* out_d, int32_t* out_pos, int32_t* status, void* workspace,
+                        size_t ws_bytes, void* stream);
+/* Diagnostic (synchronises `stream`): how many (query, probe) pairs of the
+ * last lmi_bucket_topk_f64 call on this workspace took the whole-bucket path. */
+int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx, int32_t nq,
+                              int32_t R, int32_t k, int32_t qmode, int32_t* count_out,
+                              void* stream);
+/* K3 on float64 lists: order (d64, pos). */
+int lmi_merge_topk_f64(const double* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
+                       int32_t k, double* out_d, int32_t* out_pos, void* stream);
+
 /* ---- host replay of the reference's multi-round merge ----------------- */
 /* Reproduces LearnedIndex.search (LearnedIndex.py:22-101) and search_single
  * (:103-195) — thresholds, per-category groups, the <k padding quirk
@@ -172,6 +205,13 @@ int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
                const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
                const double* thr_round0, double* dists_out, uint32_t* anns_out,
                int32_t* w_out);
+/* ABI 4: the same replay of float64 lists (lmi_bucket_topk_f64). */
+int lmi_replay_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                   const double* lists_d, const int32_t* lists_pos, int32_t k_round,
+                   int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
+                   const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
+                   const double* thr_round0, double* dists_out, uint32_t* anns_out,
+                   int32_t* w_out);
 
 /* The same replay on the device (ABI 2): identical results to lmi_replay
  * (checked bit for bit by tests/test_gpu_replay.py), no host round trip.
@@ -189,6 +229,13 @@ int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, int32_t k_l
                       const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
                       const double* thr_round0, double* dists_out, uint32_t* anns_out,
                       int32_t* status, void* workspace, size_t ws_bytes, void* stream);
+/* ABI 4: the same device replay of float64 lists (lmi_bucket_topk_f64). */
+int lmi_replay_device_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                          const double* lists_d, const int32_t* lists_pos, int32_t k_round,
+                          int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
+                          const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
+                          const double* thr_round0, double* dists_out, uint32_t* anns_out,
+                          int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---- k-means for the index build (ABI 3) -------------- */
 /* Replaces faiss.Kmeans(d, k, seed=2023).train(X) and

@@ -193,10 +193,13 @@ def layout(labels, n_buckets):
 def bucket_lists(labels, data_search, queries_search, classes, R, k, n_buckets):
     """Exact per-(q, r) top-k inside bucket classes[q, r], ordered by
     (distance, position), padded with (inf, -1).  Distances are computed per
-    (r, c) group with the same shapes the reference uses (LearnedIndex.py:166-169)."""
+    (r, c) group with the same shapes the reference uses (LearnedIndex.py:166-169),
+    in the reference's dtype: float32 for float32 inputs, float64 otherwise
+    (sklearn's rule, utils.py:11)."""
     order, off = layout(labels, n_buckets)
     nq = queries_search.shape[0]
-    out_d = np.full((nq, R, k), np.inf, np.float32)
+    dt = _float_dtype(np.asarray(queries_search), np.asarray(data_search))
+    out_d = np.full((nq, R, k), np.inf, dt)
     out_p = np.full((nq, R, k), -1, np.int32)
     for r in range(R):
         col = classes[:, r]

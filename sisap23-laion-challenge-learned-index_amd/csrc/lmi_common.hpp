@@ -89,6 +89,24 @@ __device__ inline void list_insert(uint64_t (&L)[KL], uint64_t x) {
     L[0] = (x < L[0]) ? x : L[0];
 }
 
+// list_insert that carries a payload word beside every key (the local row of
+// an entry whose key holds its global position)
+template <int KL>
+__device__ inline void list_insert_pair(uint64_t (&L)[KL], int32_t (&W)[KL], uint64_t x,
+                                        int32_t w) {
+#pragma unroll
+    for (int i = KL - 1; i > 0; --i) {
+        const bool take_prev = x < L[i - 1];
+        const bool take_x = !take_prev && x < L[i];
+        W[i] = take_prev ? W[i - 1] : (take_x ? w : W[i]);
+        L[i] = take_prev ? L[i - 1] : (take_x ? x : L[i]);
+    }
+    if (x < L[0]) {
+        L[0] = x;
+        W[0] = w;
+    }
+}
+
 template <int KL>
 __device__ inline void list_clear(uint64_t (&L)[KL]) {
 #pragma unroll
@@ -96,5 +114,15 @@ __device__ inline void list_clear(uint64_t (&L)[KL]) {
 }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- internal entry points shared between translation units -------------
+// K2 up to the merged per-pair lists (lmi_scan.hip): lmi_bucket_topk with an
+// optional third output, the shard-local row of every entry (-1 = empty).
+int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                     const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
+                     int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
+                     size_t ws_bytes, hipStream_t s);
+size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
+                            int32_t qmode);
 
 }  // namespace lmi

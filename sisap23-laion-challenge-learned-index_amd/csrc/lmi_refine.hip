@@ -1,0 +1,409 @@
+// K2 in float64 — the reference's distance arithmetic on fp16 data (gfx950).
+//
+// sklearn's cosine_similarity runs in float32 only when both operands are
+// float32; the real clip768 'emb' is float16, so the reference computes
+// d = 1 - <x/|x|, y/|y|> in float64 (utils.py:11, :19 via
+// check_pairwise_arrays/_return_float_dtype) and thresholds and merges float64
+// values (utils.py:23, LearnedIndex.py:86-97).  The fp32 scan (lmi_scan.hip)
+// cannot order two objects whose float64 distances differ by less than its
+// rounding, so for that case K2 runs in two steps:
+//
+//   1. the fp32 MFMA scan keeps per (query, probe) the top-KL (KL > k) by the
+//      fp32 distance d32 (bucket_topk_impl, with local rows);
+//   2. refine_kernel, one wave per (query, probe): with eps >= |d32 - d64|
+//      for every row, every object of the float64 top-k has
+//      d32 <= d32[k-1] + 2 eps.  If fewer than KL list entries lie in that
+//      band, the list holds all of them (a row outside the list has
+//      d32 >= d32[KL-1]); their float64 distances are recomputed from the
+//      stored rows (exact fp16 values), sorted by (d64, global position) and
+//      the first k written.  Otherwise the pair is queued for
+//   3. fallback_kernel, one workgroup per queued pair: float64 distances of
+//      every row of its bucket shard, top-k by (d64, position).
+//
+// The float64 arithmetic follows sklearn.normalize + GEMM: |q| = sqrt(sum q^2)
+// with the `norm < 10 eps -> 1` rule, q^ = q/|q|, d = 1 - (sum q^_e y_e)/|y|.
+// It differs from the reference's BLAS dgemm only in summation order (a few
+// ulp of 1.0), so ids agree except where the reference's own float64 values
+// tie to that level.
+#include "lmi_common.hpp"
+
+#include <algorithm>
+
+namespace lmi {
+namespace {
+
+constexpr int kKLMax = 16;     // longest scan list refined (LMI_MAX_K)
+constexpr int kRefT = 256;     // refine: 4 waves, one pair each
+constexpr int kFbT = 1024;     // fallback: 16 waves on one pair
+constexpr int kFbRows = 4;     // rows per wave in flight (fallback)
+constexpr double kEps64 = 2.220446049250313e-16;
+
+struct RefineArgs {
+    const void* corpus;
+    int32_t dtype;  // LMI_F16 / LMI_F32
+    int32_t d, d_pad;
+    const int32_t* gpos;
+    const int64_t* bucket_off;
+    int64_t n_rows;
+    const float* q;
+    int32_t ldq;
+    const int32_t* classes;
+    int32_t nq, R, kl, k;
+    double eps;
+    const float* ld;       // [nq][R][kl] d32 ascending
+    const int32_t* lrow;   // [nq][R][kl] local rows (-1 empty)
+    const int32_t* lpos;   // [nq][R][kl] global positions
+    double* out_d;         // [nq][R][k]
+    int32_t* out_pos;
+    int32_t* failed;       // [nq*R] queued pairs
+    int32_t* n_failed;
+    int32_t* status;
+};
+
+__device__ inline double wave_sum_d(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// the 4-element pieces of a row a lane owns: piece l + 64 i (i < nps)
+template <typename TC>
+__device__ inline void load_piece(const TC* row, int piece, int d, double (&v)[4]) {
+    const int e0 = 4 * piece;
+    if constexpr (sizeof(TC) == 2) {
+        if (e0 + 4 <= d) {
+            const uint2 raw = *reinterpret_cast<const uint2*>(row + e0);
+            _Float16 h[4];
+            __builtin_memcpy(h, &raw, 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = (double)h[j];
+            return;
+        }
+    } else {
+        if (e0 + 4 <= d) {
+            const float4 f = *reinterpret_cast<const float4*>(row + e0);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+            return;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (e0 + j < d) ? (double)row[e0 + j] : 0.0;
+}
+
+constexpr int kMaxPieces = 4;  // d <= 1024 (4 pieces of 4 per lane)
+
+// q^ for this lane's pieces (sklearn normalize of the query row, float64)
+__device__ inline void query_hat(const float* qrow, int d, int nps, double (&qh)[kMaxPieces][4]) {
+    const int lane = threadIdx.x & 63;
+    double ss = 0.0;
+#pragma unroll
+    for (int i = 0; i < kMaxPieces; ++i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * (lane + 64 * i) + j;
+            const double v = (i < nps && e < d) ? (double)qrow[e] : 0.0;
+            qh[i][j] = v;
+            ss = fma(v, v, ss);
+        }
+    }
+    double n = sqrt(wave_sum_d(ss));
+    if (n < 10.0 * kEps64) n = 1.0;  // sklearn _handle_zeros_in_scale
+#pragma unroll
+    for (int i = 0; i < kMaxPieces; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qh[i][j] = qh[i][j] / n;
+}
+
+// 1 - <q^, y/|y|> of one stored row, float64 (every lane gets the value)
+template <typename TC>
+__device__ inline double row_dist64(const TC* row, int d, int nps, const double (&qh)[kMaxPieces][4]) {
+    const int lane = threadIdx.x & 63;
+    double dot = 0.0, ss = 0.0;
+#pragma unroll
+    for (int i = 0; i < kMaxPieces; ++i) {
+        if (i < nps) {
+            double v[4];
+            load_piece<TC>(row, lane + 64 * i, d, v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                dot = fma(qh[i][j], v[j], dot);
+                ss = fma(v[j], v[j], ss);
+            }
+        }
+    }
+    dot = wave_sum_d(dot);
+    double n = sqrt(wave_sum_d(ss));
+    if (n < 10.0 * kEps64) n = 1.0;
+    return 1.0 - dot / n;
+}
+
+__device__ inline bool lt_dp(double a, int32_t pa, double b, int32_t pb) {
+    return a < b || (a == b && pa < pb);
+}
+
+template <typename TC>
+__global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * (kRefT / 64) + (threadIdx.x >> 6);
+    const int64_t P = (int64_t)a.nq * a.R;
+    if (p >= P) return;
+    const int kl = a.kl, k = a.k;
+    const size_t li = (size_t)p * kl;
+    // lane j < kl holds list entry j
+    const bool has = lane < kl;
+    const float dj = has ? a.ld[li + lane] : __builtin_inff();
+    const int32_t rj = has ? a.lrow[li + lane] : -1;
+    const int32_t gj = has ? a.lpos[li + lane] : -1;
+    const uint64_t valid = __ballot(rj >= 0);
+    const int n_valid = __popcll(valid);
+    double* od = a.out_d + (size_t)p * k;
+    int32_t* op = a.out_pos + (size_t)p * k;
+    int m;
+    if (n_valid < kl) {
+        m = n_valid;  // the shard's whole bucket is listed
+    } else {
+        const float dk = __shfl(dj, k - 1);
+        const double t = (double)dk + 2.0 * a.eps;
+        m = __popcll(__ballot(has && (double)dj <= t));
+        if (m >= kl) {  // the band may continue past the list: exact fallback
+            if (lane == 0) a.failed[atomicAdd(a.n_failed, 1)] = (int32_t)p;
+            return;
+        }
+    }
+    if (has && rj >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);
+    const int nps = (a.d + 255) / 256;
+    double qh[kMaxPieces][4];
+    query_hat(a.q + (size_t)(p / a.R) * a.ldq, a.d, nps, qh);
+    double mine = __builtin_inf();
+    for (int j = 0; j < m; ++j) {
+        const int32_t r = __shfl(rj, j);
+        if (r < 0 || r >= a.n_rows) continue;
+        const TC* row = reinterpret_cast<const TC*>(a.corpus) + (size_t)r * a.d_pad;
+        const double dv = row_dist64<TC>(row, a.d, nps, qh);
+        if (lane == j) mine = dv;
+    }
+    // rank of entry `lane` among the m refined entries by (d64, position)
+    int rank = 0;
+    for (int i = 0; i < m; ++i) {
+        const double di = __shfl(mine, i);
+        const int32_t gi = __shfl(gj, i);
+        rank += (i != lane && lt_dp(di, gi, mine, gj)) ? 1 : 0;
+    }
+    if (lane < m && rank < k) {
+        od[rank] = mine;
+        op[rank] = gj;
+    }
+    for (int j = m + lane; j < k; j += 64) {
+        od[j] = __builtin_inf();
+        op[j] = -1;
+    }
+}
+
+// One workgroup per queued pair: float64 distance of every row of its bucket
+// shard (a wave per row, kFbRows rows in flight), per-lane-0 top-k lists
+// merged through LDS.
+template <typename TC>
+__global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
+    __shared__ double sd[kFbT / 64][kKLMax];
+    __shared__ int32_t sp[kFbT / 64][kKLMax];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nf = *a.n_failed;
+    const int k = a.k;
+    const int nps = (a.d + 255) / 256;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        const int64_t p = a.failed[f];
+        const int c = a.classes[p];  // classes is [nq][R]: pair p = q*R + r
+        const int64_t b0 = a.bucket_off[c], b1 = a.bucket_off[c + 1];
+        double qh[kMaxPieces][4];
+        query_hat(a.q + (size_t)(p / a.R) * a.ldq, a.d, nps, qh);
+        double L[kKLMax];
+        int32_t G[kKLMax];
+#pragma unroll
+        for (int i = 0; i < kKLMax; ++i) {
+            L[i] = __builtin_inf();
+            G[i] = INT32_MAX;
+        }
+        for (int64_t r0 = b0 + (int64_t)w * kFbRows; r0 < b1; r0 += (int64_t)(kFbT / 64) * kFbRows) {
+            double dv[kFbRows];
+#pragma unroll
+            for (int u = 0; u < kFbRows; ++u) {
+                const int64_t r = r0 + u;
+                const TC* row = reinterpret_cast<const TC*>(a.corpus) +
+                                (size_t)(r < b1 ? r : b0) * a.d_pad;
+                dv[u] = row_dist64<TC>(row, a.d, nps, qh);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int u = 0; u < kFbRows; ++u) {
+                    const int64_t r = r0 + u;
+                    if (r >= b1) break;
+                    const double x = dv[u];
+                    const int32_t g = a.gpos[r];
+                    if (!lt_dp(x, g, L[k - 1], G[k - 1])) continue;
+                    // insertion into the ascending list of k entries
+                    int i = k - 1;
+                    while (i > 0 && lt_dp(x, g, L[i - 1], G[i - 1])) {
+                        L[i] = L[i - 1];
+                        G[i] = G[i - 1];
+                        --i;
+                    }
+                    L[i] = x;
+                    G[i] = g;
+                }
+            }
+        }
+        if (lane == 0)
+            for (int i = 0; i < k; ++i) {
+                sd[w][i] = L[i];
+                sp[w][i] = G[i];
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int head[kFbT / 64] = {};
+            double* od = a.out_d + (size_t)p * k;
+            int32_t* op = a.out_pos + (size_t)p * k;
+            for (int j = 0; j < k; ++j) {
+                int best = -1;
+                for (int v = 0; v < kFbT / 64; ++v) {
+                    if (head[v] >= k) continue;
+                    if (best < 0 || lt_dp(sd[v][head[v]], sp[v][head[v]], sd[best][head[best]],
+                                          sp[best][head[best]]))
+                        best = v;
+                }
+                const double x = sd[best][head[best]];
+                const int32_t g = sp[best][head[best]];
+                ++head[best];
+                const bool empty = g == INT32_MAX;
+                od[j] = empty ? __builtin_inf() : x;
+                op[j] = empty ? -1 : g;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+struct RefineWs {
+    size_t scan, ld, lrow, lpos, failed, nfailed, total;
+};
+
+int pick_kl_f64(int k) { return k <= 10 ? 16 : LMI_MAX_K; }
+
+RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
+    RefineWs w{};
+    const int kl = pick_kl_f64(k);
+    const size_t P = (size_t)nq * R;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = off;
+        off = align_up(off + bytes, 256);
+        return at;
+    };
+    w.ld = take(P * kl * 4);
+    w.lrow = take(P * kl * 4);
+    w.lpos = take(P * kl * 4);
+    w.failed = take(P * 4);
+    w.nfailed = take(256);
+    w.scan = take(scan_workspace_bytes(idx, nq, R, kl, qmode));
+    w.total = off;
+    return w;
+}
+
+int num_cus_ref() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 256;
+        return v > 0 ? v : 256;
+    }();
+    return n;
+}
+
+}  // namespace
+}  // namespace lmi
+
+extern "C" size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
+                                               int32_t k, int32_t qmode) {
+    if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K) return 0;
+    return lmi::refine_ws(idx, nq, R, k, qmode).total;
+}
+
+extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, int32_t nq,
+                                   int32_t ldq, const int32_t* classes, int32_t R, int32_t k,
+                                   int32_t qmode, double eps, double* out_d, int32_t* out_pos,
+                                   int32_t* status, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+    using namespace lmi;
+    LMI_CHECK_ARG(idx != nullptr, "null index");
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
+    LMI_CHECK_ARG(idx->d >= 1 && idx->d <= 4 * 256, "d=%d outside [1, 1024] for float64 refinement",
+                  idx->d);
+    LMI_CHECK_ARG(eps >= 0.0 && eps < 1.0, "eps must lie in [0, 1)");
+    if (nq == 0) return LMI_OK;
+    LMI_CHECK_ARG(q && classes && out_d && out_pos && status && workspace, "null pointer");
+    const RefineWs w = refine_ws(idx, nq, R, k, qmode);
+    if (ws_bytes < w.total) {
+        set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
+        return LMI_E_WORKSPACE;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    const int kl = pick_kl_f64(k);
+    RefineArgs a{};
+    a.corpus = idx->corpus;
+    a.dtype = idx->dtype;
+    a.d = idx->d;
+    a.d_pad = idx->d_pad;
+    a.gpos = idx->gpos;
+    a.bucket_off = idx->bucket_off;
+    a.n_rows = idx->n_rows;
+    a.q = q;
+    a.ldq = ldq;
+    a.classes = classes;
+    a.nq = nq;
+    a.R = R;
+    a.kl = kl;
+    a.k = k;
+    a.eps = eps;
+    a.ld = (const float*)(ws + w.ld);
+    a.lrow = (const int32_t*)(ws + w.lrow);
+    a.lpos = (const int32_t*)(ws + w.lpos);
+    a.out_d = out_d;
+    a.out_pos = out_pos;
+    a.failed = (int32_t*)(ws + w.failed);
+    a.n_failed = (int32_t*)(ws + w.nfailed);
+    a.status = status;
+    LMI_HIP_TRY(hipMemsetAsync(ws + w.nfailed, 0, 4, s));
+    int rc = bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
+                              (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
+                              ws + w.scan, w.total - w.scan, s);
+    if (rc != LMI_OK) return rc;
+    const int64_t P = (int64_t)nq * R;
+    const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));
+    if (idx->dtype == LMI_F16)
+        hipLaunchKernelGGL(refine_kernel<_Float16>, grid, dim3(kRefT), 0, s, a);
+    else
+        hipLaunchKernelGGL(refine_kernel<float>, grid, dim3(kRefT), 0, s, a);
+    LMI_LAUNCH_CHECK("refine_kernel");
+    // one workgroup per queued pair (the grid strides over the queue; the
+    // queue length is read on the device, usually 0)
+    const dim3 fgrid((unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref())));
+    if (idx->dtype == LMI_F16)
+        hipLaunchKernelGGL(fallback_kernel<_Float16>, fgrid, dim3(kFbT), 0, s, a);
+    else
+        hipLaunchKernelGGL(fallback_kernel<float>, fgrid, dim3(kFbT), 0, s, a);
+    LMI_LAUNCH_CHECK("fallback_kernel");
+    return LMI_OK;
+}
+
+extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx,
+                                         int32_t nq, int32_t R, int32_t k, int32_t qmode,
+                                         int32_t* count_out, void* stream) {
+    using namespace lmi;
+    LMI_CHECK_ARG(workspace && idx && count_out, "null pointer");
+    const RefineWs w = refine_ws(idx, nq, R, k, qmode);
+    LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + w.nfailed, 4,
+                               hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
+    LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return LMI_OK;
+}

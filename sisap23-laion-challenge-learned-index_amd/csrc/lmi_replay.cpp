@@ -99,13 +99,44 @@ void quirk_row(const std::vector<double>& row, const std::vector<int64_t>& u_pos
 
 }  // namespace
 
+namespace {
+int replay_impl(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list, const void* lists_dv,
+                bool lists_f64, const int32_t* lists_pos, int32_t k_round, int32_t k_final,
+                const int64_t* bucket_size, int32_t n_buckets, const int64_t* pos_to_id,
+                int64_t n_total, int32_t use_threshold, const double* thr_round0,
+                double* dists_out, uint32_t* anns_out, int32_t* w_out);
+}  // namespace
+
 extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
                           const float* lists_d, const int32_t* lists_pos, int32_t k_round,
                           int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
                           const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
                           const double* thr_round0, double* dists_out, uint32_t* anns_out,
                           int32_t* w_out) {
+    return replay_impl(classes, nq, R, k_list, lists_d, false, lists_pos, k_round, k_final,
+                       bucket_size, n_buckets, pos_to_id, n_total, use_threshold, thr_round0,
+                       dists_out, anns_out, w_out);
+}
+
+extern "C" int lmi_replay_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                              const double* lists_d, const int32_t* lists_pos, int32_t k_round,
+                              int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
+                              const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
+                              const double* thr_round0, double* dists_out, uint32_t* anns_out,
+                              int32_t* w_out) {
+    return replay_impl(classes, nq, R, k_list, lists_d, true, lists_pos, k_round, k_final,
+                       bucket_size, n_buckets, pos_to_id, n_total, use_threshold, thr_round0,
+                       dists_out, anns_out, w_out);
+}
+
+namespace {
+int replay_impl(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list, const void* lists_dv,
+                bool lists_f64, const int32_t* lists_pos, int32_t k_round, int32_t k_final,
+                const int64_t* bucket_size, int32_t n_buckets, const int64_t* pos_to_id,
+                int64_t n_total, int32_t use_threshold, const double* thr_round0,
+                double* dists_out, uint32_t* anns_out, int32_t* w_out) {
     using lmi::set_error;
+    const void* lists_d = lists_dv;
     if (nq < 0 || R < 1 || k_round < 1 || k_final < 1 || k_list < 1 || n_buckets < 1) {
         set_error("lmi_replay: bad sizes");
         return LMI_E_INVALID;
@@ -182,7 +213,8 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
         auto list_at = [&](int q, int j, double& d, int64_t& pos) {
             const size_t o = ((size_t)q * R + r) * k_list + j;
             pos = lists_pos[o];
-            d = (double)lists_d[o];
+            d = lists_f64 ? static_cast<const double*>(lists_dv)[o]
+                          : (double)static_cast<const float*>(lists_dv)[o];
         };
 #pragma omp parallel for schedule(dynamic, 1)
         for (int c = 0; c < n_buckets; ++c) {
@@ -345,3 +377,4 @@ extern "C" int lmi_replay(const int32_t* classes, int32_t nq, int32_t R, int32_t
     }
     return LMI_OK;
 }
+}  // namespace

@@ -67,7 +67,8 @@ __device__ inline int wave_min_i(int v) { return __ockl_wfred_min_i32(v); }
 struct RoundArgs {
     const int32_t* classes;
     int32_t nq, R, r, kl, kr, C;
-    const float* lists_d;    // [nq][R][kl]
+    const void* lists_d;     // [nq][R][kl] float, or double when lists_f64
+    int32_t lists_f64;
     const int32_t* lists_p;  // [nq][R][kl]
     const int64_t* bucket_size;
     int32_t* groups;         // [nq] this round's groups, category c at [g0(c), g1(c))
@@ -81,10 +82,17 @@ struct RoundArgs {
     int32_t abl;  // diagnostic builds: 1/2/3 stop after grouping / U / selection
 };
 
+// a list distance as the reference holds it: float32 widened, or float64
+// (lmi_bucket_topk_f64 lists, the reference's arithmetic on fp16 data)
+__device__ inline double list_d(const RoundArgs& a, size_t o) {
+    return a.lists_f64 ? reinterpret_cast<const double*>(a.lists_d)[o]
+                       : (double)reinterpret_cast<const float*>(a.lists_d)[o];
+}
+
 __device__ inline void list_at(const RoundArgs& a, int q, int j, double& d, int32_t& pos) {
     const size_t o = ((size_t)q * a.R + a.r) * a.kl + j;
     pos = a.lists_p[o];
-    d = (double)a.lists_d[o];
+    d = list_d(a, o);
 }
 
 // LearnedIndex.py:174-193 (quirk_row of lmi_replay.cpp): row (n_row values),
@@ -229,7 +237,7 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
             const int q = G[gi];
             const size_t o = ((size_t)q * a.R + a.r) * a.kl + j;
             const int32_t pos = a.lists_p[o];
-            const bool rel = pos >= 0 && (double)a.lists_d[o] < a.thr[q];
+            const bool rel = pos >= 0 && list_d(a, o) < a.thr[q];
             U[e] = rel ? pos : INT32_MAX;
             nb_tot += rel ? 1 : 0;
         }
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
                 if (p == INT32_MAX) continue;
                 const int gi = g0 + e / kl_use, j = e - (e / kl_use) * kl_use;
                 const int q = G[gi];
-                a.dr_d[(size_t)q * kr + j] = (double)a.lists_d[((size_t)q * a.R + a.r) * a.kl + j];
+                a.dr_d[(size_t)q * kr + j] = list_d(a, ((size_t)q * a.R + a.r) * a.kl + j);
                 a.dr_p[(size_t)q * kr + j] = p;
             }
             for (int gi = g0 + tid; gi < g1; gi += kTG) {
@@ -564,12 +572,48 @@ extern "C" size_t lmi_replay_device_workspace_bytes(int32_t nq, int32_t R, int32
     return lmi::replay_ws(nq, R, k_list, k_round, w, n_buckets).total;
 }
 
+namespace lmi {
+int replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                       const void* lists_d, int lists_f64, const int32_t* lists_pos,
+                       int32_t k_round, int32_t k_final, const int64_t* bucket_size,
+                       int32_t n_buckets, const int64_t* pos_to_id, int64_t n_total,
+                       int32_t use_threshold, const double* thr_round0, double* dists_out,
+                       uint32_t* anns_out, int32_t* status, void* workspace, size_t ws_bytes,
+                       void* stream);
+}  // namespace lmi
+
 extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
                                  const float* lists_d, const int32_t* lists_pos, int32_t k_round,
                                  int32_t k_final, const int64_t* bucket_size, int32_t n_buckets,
                                  const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
                                  const double* thr_round0, double* dists_out, uint32_t* anns_out,
                                  int32_t* status, void* workspace, size_t ws_bytes, void* stream) {
+    return lmi::replay_device_impl(classes, nq, R, k_list, lists_d, 0, lists_pos, k_round, k_final,
+                                   bucket_size, n_buckets, pos_to_id, n_total, use_threshold,
+                                   thr_round0, dists_out, anns_out, status, workspace, ws_bytes,
+                                   stream);
+}
+
+extern "C" int lmi_replay_device_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                                     const double* lists_d, const int32_t* lists_pos,
+                                     int32_t k_round, int32_t k_final, const int64_t* bucket_size,
+                                     int32_t n_buckets, const int64_t* pos_to_id, int64_t n_total,
+                                     int32_t use_threshold, const double* thr_round0,
+                                     double* dists_out, uint32_t* anns_out, int32_t* status,
+                                     void* workspace, size_t ws_bytes, void* stream) {
+    return lmi::replay_device_impl(classes, nq, R, k_list, lists_d, 1, lists_pos, k_round, k_final,
+                                   bucket_size, n_buckets, pos_to_id, n_total, use_threshold,
+                                   thr_round0, dists_out, anns_out, status, workspace, ws_bytes,
+                                   stream);
+}
+
+int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
+                            const void* lists_d, int lists_f64, const int32_t* lists_pos,
+                            int32_t k_round, int32_t k_final, const int64_t* bucket_size,
+                            int32_t n_buckets, const int64_t* pos_to_id, int64_t n_total,
+                            int32_t use_threshold, const double* thr_round0, double* dists_out,
+                            uint32_t* anns_out, int32_t* status, void* workspace, size_t ws_bytes,
+                            void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && k_round >= 1 && k_final >= 1 && k_list >= 1 && n_buckets >= 1,
                   "lmi_replay_device: bad sizes");
@@ -622,6 +666,7 @@ extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, 
         a.kr = k_round;
         a.C = C;
         a.lists_d = lists_d;
+        a.lists_f64 = lists_f64;
         a.lists_p = lists_pos;
         a.bucket_size = bucket_size;
         a.groups = groups;

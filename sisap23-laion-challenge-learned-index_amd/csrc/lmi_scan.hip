@@ -87,6 +87,7 @@ __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict_
                                                         int32_t* __restrict__ status,
                                                         float* __restrict__ out_d,
                                                         int32_t* __restrict__ out_pos,
+                                                        int32_t* __restrict__ out_row,
                                                         int32_t out_per_q) {
     __shared__ float red[kThreads / 64];
     const int row = blockIdx.x;
@@ -122,6 +123,7 @@ __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict_
     for (int e = tid; e < out_per_q; e += kThreads) {
         out_d[(size_t)row * out_per_q + e] = __builtin_inff();
         out_pos[(size_t)row * out_per_q + e] = -1;
+        if (out_row) out_row[(size_t)row * out_per_q + e] = -1;
     }
 }
 
@@ -1596,22 +1598,27 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
 // ---------------------------------------------------------------------------
 // chunk merge
 // ---------------------------------------------------------------------------
-template <int KL>
+template <int KL, bool ROWS>
 __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, float* __restrict__ out_d,
-    int32_t* __restrict__ out_pos, int64_t n_rows, int32_t* __restrict__ status) {
+    int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, int64_t n_rows,
+    int32_t* __restrict__ status) {
     // one thread per pair, 64-thread blocks (spread over every CU); each
     // chunk list is read with all its loads in flight, then its global
     // positions gathered the same way, then merged into a register list
+    // (ROWS: the local row of every entry travels beside its key)
     const int pp = blockIdx.x * 64 + threadIdx.x;
     if (pp >= P) return;
     const int c = pair_bucket[pp];
     if (c < 0) return;
     const int nch = chunk_first[c + 1] - chunk_first[c];
     uint64_t M[KL];
+    int32_t W[KL];
     list_clear<KL>(M);
+#pragma unroll
+    for (int i = 0; i < KL; ++i) W[i] = -1;
     // A chunk list is ordered by (distance, row); rows inside a chunk are in
     // ascending global position (the index layout guarantees it), so mapping
     // each key to (distance, global position) keeps the list ordered, and the
@@ -1636,7 +1643,12 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
         for (int i = 0; i < KL; ++i) {
             if (g[i] < 0) continue;
             const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
-            if (key < M[KL - 1]) list_insert<KL>(M, key);
+            if (key < M[KL - 1]) {
+                if constexpr (ROWS)
+                    list_insert_pair<KL>(M, W, key, (int32_t)(uint32_t)K[i]);
+                else
+                    list_insert<KL>(M, key);
+            }
         }
     }
     const size_t o = (size_t)pair_q[pp] * k;
@@ -1647,6 +1659,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
             const bool empty = key == kEmptyKey;
             out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
             out_pos[o + i] = empty ? -1 : (int32_t)(uint32_t)key;
+            if constexpr (ROWS) out_row[o + i] = empty ? -1 : W[i];
         }
     }
 }
@@ -1890,10 +1903,15 @@ extern "C" int32_t lmi_plan_chunks(const int64_t* bucket_off_host, int32_t n_buc
     return maxc;
 }
 
-extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
-                                           int32_t k, int32_t qmode) {
+size_t lmi::scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
+                                 int32_t qmode) {
     if (!idx || nq < 0 || R < 1 || k < 1) return 0;
     return lmi::ws_layout(idx, nq, R, k, qmode).total;
+}
+
+extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
+                                           int32_t k, int32_t qmode) {
+    return lmi::scan_workspace_bytes(idx, nq, R, k, qmode);
 }
 
 namespace {
@@ -1909,6 +1927,14 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
                                const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
                                float* out_d, int32_t* out_pos, int32_t* status, void* workspace,
                                size_t ws_bytes, void* stream) {
+    return lmi::bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
+                                 status, workspace, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                          const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
+                          int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
+                          size_t ws_bytes, hipStream_t s) {
     using namespace lmi;
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(idx->dtype == LMI_F16 || idx->dtype == LMI_F32, "bad corpus dtype");
@@ -1930,7 +1956,6 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
         set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
         return LMI_E_WORKSPACE;
     }
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     auto* ws = reinterpret_cast<unsigned char*>(workspace);
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
     const int QB = w.qb;
@@ -1940,11 +1965,11 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     if (f16math) {
         hipLaunchKernelGGL(prep_kernel<true>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
                            idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
-                           out_pos, R * k);
+                           out_pos, out_row, R * k);
     } else {
         hipLaunchKernelGGL(prep_kernel<false>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
                            idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
-                           out_pos, R * k);
+                           out_pos, out_row, R * k);
     }
     LMI_LAUNCH_CHECK("prep_kernel");
     if (idx->n_rows == 0) return LMI_OK;
@@ -2047,15 +2072,16 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     if (rc != LMI_OK) return rc;
 
     const int grid = (P + 63) / 64;
+#define LMI_CM(KLV, ROWSV)                                                                         \
+    hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
+                       a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, out_d, \
+                       out_pos, out_row, idx->n_rows, status)
     if (KL == 10) {
-        hipLaunchKernelGGL(chunk_merge_kernel<10>, dim3(grid), dim3(64), 0, s, a.partial,
-                           a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, out_d,
-                           out_pos, idx->n_rows, status);
+        if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
     } else {
-        hipLaunchKernelGGL(chunk_merge_kernel<16>, dim3(grid), dim3(64), 0, s, a.partial,
-                           a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, out_d,
-                           out_pos, idx->n_rows, status);
+        if (out_row) LMI_CM(16, true); else LMI_CM(16, false);
     }
+#undef LMI_CM
     LMI_LAUNCH_CHECK("chunk_merge_kernel");
     return LMI_OK;
 }

@@ -17,9 +17,9 @@ threshold/grouping/padding procedure is replayed from the k-lists on the GPU
 reproduces its output exactly on tie-free inputs (tests/test_oracle_golden.py,
 tests/test_gpu_golden.py, tests/test_gpu_replay.py).
 
-The bucket-sorted corpus is built in HBM on first use and cached while the
-same DataFrames and labels are passed again (the reference re-gathers every
-bucket on every call: LearnedIndex.py:152-153, :168).
+The bucket-sorted corpus is built in HBM on first use and cached while
+byte-identical data, ids and labels are passed again (`content_key`; the
+reference re-gathers every bucket on every call: LearnedIndex.py:152-153, :168).
 """
 from __future__ import annotations
 
@@ -36,10 +36,46 @@ torch.manual_seed(2023)
 np.random.seed(2023)
 
 
-def _fingerprint(a: np.ndarray):
-    a = np.ascontiguousarray(a)
-    step = max(1, a.size // 4096)
-    return (a.size, a.dtype.str, int(a.astype(np.int64).sum()), a[::step].tobytes())
+def content_key(a) -> tuple:
+    """Shape, dtype and a 64-bit hash of every byte of an array or DataFrame
+    (its values in their own memory order, no copy of a contiguous block).
+
+    Keys the HBM index cache: a cached corpus is reused only for byte-identical
+    inputs, so a frame changed in place, or a new frame that happens to reuse
+    a freed one's id(), is rebuilt rather than served stale.  xxh3 reads
+    ≈7 GB/s on one core (15 GB of fp16 clip768 at 10M: ≈2 s per call, against
+    the reference re-gathering every bucket on every call)."""
+    import xxhash
+    v = a.to_numpy() if hasattr(a, "to_numpy") else np.asarray(a)
+    if not v.flags.c_contiguous and v.T.flags.c_contiguous:
+        mem, order = v.T, "F"
+    else:
+        mem, order = np.ascontiguousarray(v), "C"
+    return (v.shape, v.dtype.str, order, xxhash.xxh3_64_intdigest(mem))
+
+
+def _search_frame(data_search):
+    """data_search as search_single sees it: without a 'category' column
+    (LearnedIndex.py:140-141)."""
+    if hasattr(data_search, "columns") and "category" in data_search.columns:
+        return data_search.drop("category", axis=1, errors="ignore")
+    return data_search
+
+
+def _dtypes(a) -> set:
+    if hasattr(a, "dtypes") and hasattr(a.dtypes, "__iter__"):
+        return {np.dtype(t) for t in a.dtypes}
+    return {np.asarray(a).dtype}
+
+
+def dist_dtype(data_search, queries_search) -> str:
+    """The arithmetic the reference's distances run in (utils.py:11, :19):
+    sklearn's cosine_similarity works in float32 only when both operands are
+    float32 (check_pairwise_arrays / _return_float_dtype) and in float64
+    otherwise — the clip768 'emb' of the real data is float16, so 'f64'."""
+    f32 = {np.dtype(np.float32)}
+    return "f32" if _dtypes(_search_frame(data_search)) == f32 and \
+        _dtypes(queries_search) == f32 else "f64"
 
 
 class LearnedIndex(Logger):
@@ -59,16 +95,18 @@ class LearnedIndex(Logger):
         """DeviceIndex of data_search rows in data_navigation order."""
         from .index import DeviceIndex
         labels = np.asarray(labels).astype(np.int64)
-        key = (id(data_navigation), id(data_search), _fingerprint(labels))
+        ds = _search_frame(data_search)
+        ids = np.asarray(data_navigation.index)
+        key = (content_key(ds), content_key(labels), content_key(ids),
+               content_key(np.asarray(ds.index)) if hasattr(ds, "index") else None)
         if self._index is not None and self._cache_key == key:
             return self._index
-        ds = data_search.drop("category", axis=1, errors="ignore") \
-            if hasattr(data_search, "columns") and "category" in data_search.columns else data_search
-        ids = np.asarray(data_navigation.index)
+        # fp16 data (the real clip768 'emb') stays fp16 on its way to HBM
+        dt = np.float16 if _dtypes(ds) == {np.dtype(np.float16)} else np.float32
         if hasattr(ds, "index") and not ds.index.equals(data_navigation.index):
-            rows = ds.loc[data_navigation.index].to_numpy(dtype=np.float32)  # :152-153, :168
+            rows = ds.loc[data_navigation.index].to_numpy(dtype=dt)  # :152-153, :168
         else:
-            rows = np.asarray(ds, dtype=np.float32)
+            rows = np.asarray(ds, dtype=dt)
         n_buckets = self._n_buckets(labels)
         self._index = DeviceIndex(rows, labels, n_buckets, ids=ids)
         self._cache_key = key
@@ -96,23 +134,25 @@ class LearnedIndex(Logger):
         q_nav = data_X_to_torch(queries_navigation).to(index.device)
         q_search = torch.from_numpy(np.ascontiguousarray(queries_search, dtype=np.float32)).to(index.device)
         return Searcher(index, router).search(q_nav, q_search, n_buckets, k=k, k_round=10,
-                                              use_threshold=use_threshold, semantics=semantics)
+                                              use_threshold=use_threshold, semantics=semantics,
+                                              dist=dist_dtype(data_search, queries_search))
 
     def search_single(self, data_navigation, data_search, queries_search, pred_categories,
                       k=10, threshold_dist=None):
         """One bucket per query (LearnedIndex.py:103-195).  `pred_categories`
         is the per-query bucket; object labels come from
         data_navigation['category'] as in the reference's groupby (:143)."""
-        from .index import bucket_topk, replay_device
+        from .index import Searcher, replay_device
         index = self._device_index(data_navigation, data_search,
                                    np.asarray(data_navigation['category']))
         dev = index.device
         q = torch.from_numpy(np.ascontiguousarray(queries_search, dtype=np.float32)).to(dev)
         cls = np.asarray(pred_categories).astype(np.int32).reshape(-1, 1)
         classes = torch.from_numpy(cls).to(dev)
-        d, pos, st = bucket_topk(index, q, classes, k)
-        if int(st.item()) & _lib.LMI_STATUS_QUERY_NOT_F16:
-            d, pos, _ = bucket_topk(index, q, classes, k, qmode=_lib.LMI_Q_F32)
+        _, d, pos, st = Searcher(index, None).lists(None, q, 1, k, classes=classes,
+                                                    dist=dist_dtype(data_search, queries_search))
+        if int(st.item()) & _lib.LMI_STATUS_INTERNAL:
+            raise RuntimeError(f"search_single: scan status {int(st.item())}")
         thr = None if threshold_dist is None else torch.from_numpy(
             np.ascontiguousarray(np.asarray(threshold_dist, dtype=np.float64).ravel())).to(dev)
         dd, aa, rst = replay_device(

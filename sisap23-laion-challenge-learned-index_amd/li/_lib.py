@@ -37,6 +37,7 @@ LMI_Q_F32 = 1
 LMI_MAX_LAYERS = 8
 LMI_MAX_K = 16
 LMI_KMEANS_MAX_D = 128
+LMI_REFINE_EPS = 2.0 ** -16
 
 # every symbol include/lmi_hip.h declares (tests check the export table)
 EXPORTS = (
@@ -45,9 +46,15 @@ EXPORTS = (
     "lmi_scan_workspace_bytes",
     "lmi_bucket_topk",
     "lmi_merge_topk",
+    "lmi_scan_f64_workspace_bytes",
+    "lmi_bucket_topk_f64",
+    "lmi_refine_fallback_count",
+    "lmi_merge_topk_f64",
     "lmi_replay",
+    "lmi_replay_f64",
     "lmi_replay_device_workspace_bytes",
     "lmi_replay_device",
+    "lmi_replay_device_f64",
     "lmi_kmeans_assign",
     "lmi_kmeans_workspace_bytes",
     "lmi_kmeans_update",
@@ -77,7 +84,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class IndexDesc(C.Structure):
@@ -110,11 +117,21 @@ _SIGNATURES = {
     "lmi_bucket_topk": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _I32, _I32,
                                   _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_merge_topk": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),
+    "lmi_scan_f64_workspace_bytes": (C.c_size_t, [C.POINTER(IndexDesc), _I32, _I32, _I32, _I32]),
+    "lmi_bucket_topk_f64": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _I32, _I32,
+                                      C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
+    "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,
+                                            _P]),
+    "lmi_merge_topk_f64": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),
     "lmi_replay": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _I32,
                              _P, _P, _P, _P]),
+    "lmi_replay_f64": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64,
+                                 _I32, _P, _P, _P, _P]),
     "lmi_replay_device_workspace_bytes": (C.c_size_t, [_I32, _I32, _I32, _I32, _I32, _I32]),
     "lmi_replay_device": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64,
                                     _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
+    "lmi_replay_device_f64": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P,
+                                        _I64, _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_kmeans_assign": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P]),
     "lmi_kmeans_workspace_bytes": (C.c_size_t, [_I64, _I32, _I32]),
     "lmi_kmeans_update": (C.c_int, [_P, _I64, _I32, _P, _I32, _P, _P, _P, _P, C.c_size_t, _P]),

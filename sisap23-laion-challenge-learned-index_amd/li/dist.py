@@ -53,31 +53,50 @@ def _all_gather(out: torch.Tensor, part: torch.Tensor, group=None):
     dist.all_gather_into_tensor(out, part, group=group)
 
 
-def all_gather_lists(d: torch.Tensor, pos: torch.Tensor, group=None):
+def all_gather_lists(d: torch.Tensor, pos: torch.Tensor, group=None,
+                     status: Optional[torch.Tensor] = None):
     """[nq, R, k] per rank -> [G, nq, R, k] on every rank, in ONE collective:
-    the f32 distances travel bit-for-bit as int32 beside the positions."""
+    the distances (float32 or float64) travel bit for bit as int32 words beside
+    the positions, and the rank's device status word (lmi_bucket_topk's
+    LMI_STATUS_* bits) rides along, so every rank sees every rank's status
+    and all ranks fail together (returned as [G] int32 when given)."""
     G = dist.get_world_size(group)
-    both = torch.stack((d.contiguous().view(torch.int32), pos.to(torch.int32).contiguous()), dim=-1)
-    # concatenated along dim 0 (the form both RCCL and gloo accept), viewed [G, ...]
-    out = torch.empty((G * both.shape[0],) + tuple(both.shape[1:]), dtype=both.dtype, device=both.device)
-    _all_gather(out, both, group)
-    out = out.view((G,) + tuple(both.shape))
-    gd = out[..., 0].contiguous().view(torch.float32)
-    gp = out[..., 1].contiguous().to(pos.dtype)
-    return gd, gp
+    parts = [d.contiguous().view(torch.int32).reshape(-1),
+             pos.to(torch.int32).contiguous().reshape(-1)]
+    if status is not None:
+        parts.append(status.to(torch.int32).reshape(-1)[:1])
+    flat = torch.cat(parts)
+    out = torch.empty((G * flat.numel(),), dtype=torch.int32, device=flat.device)
+    _all_gather(out, flat, group)
+    out = out.view(G, flat.numel())
+    nd, npos = parts[0].numel(), parts[1].numel()
+    gd = out[:, :nd].contiguous().view(d.dtype).view((G,) + tuple(d.shape))
+    gp = out[:, nd:nd + npos].contiguous().view((G,) + tuple(pos.shape)).to(pos.dtype)
+    if status is None:
+        return gd, gp
+    return gd, gp, out[:, nd + npos]
 
 
 def gather_merge(d: torch.Tensor, pos: torch.Tensor, k: int, group=None,
-                 merge: Optional[Callable] = None):
+                 merge: Optional[Callable] = None, status: Optional[torch.Tensor] = None):
     """All-gather the shard lists and merge them (K3 on the GPU by default).
 
     `merge(gd, gp, k) -> (d, pos)` can be swapped for a CPU checker in the
-    gloo tests; the product path always uses lmi_merge_topk."""
-    gd, gp = all_gather_lists(d, pos, group)
+    gloo tests; the product path always uses lmi_merge_topk(_f64).  With
+    `status`, returns a third value: the OR of every rank's status word."""
+    got = all_gather_lists(d, pos, group, status)
+    gd, gp = got[0], got[1]
     if merge is None:
         from .index import merge_topk
-        return merge_topk(gd, gp, k)
-    return merge(gd, gp, k)
+        md, mp = merge_topk(gd, gp, k)
+    else:
+        md, mp = merge(gd, gp, k)
+    if status is None:
+        return md, mp
+    st = got[2][0:1].clone()
+    for g in range(1, got[2].shape[0]):
+        st = torch.bitwise_or(st, got[2][g:g + 1])
+    return md, mp, st
 
 
 def route_sharded(router, q_nav: torch.Tensor, R: int, group=None) -> torch.Tensor:

@@ -405,27 +405,66 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
     return out_d, out_pos, status
 
 
+def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
+                    qmode: Optional[int] = None, eps: float = _lib.LMI_REFINE_EPS, stream=None,
+                    fallback_count: bool = False):
+    """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
+    arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
+    (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback])."""
+    lib = _lib.load()
+    q = _as_torch(q, index.device, torch.float32)
+    classes = _as_torch(classes, index.device, torch.int32)
+    nq, R = classes.shape
+    if q.shape[0] != nq or q.shape[1] != index.d:
+        raise ValueError("query shape does not match the index")
+    if qmode is None:
+        qmode = _lib.LMI_Q_F16 if index.storage == "f16" else _lib.LMI_Q_F32
+    out_d = torch.empty((nq, R, k), dtype=torch.float64, device=index.device)
+    out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
+    status = torch.zeros((1,), dtype=torch.int32, device=index.device)
+    need = lib.lmi_scan_f64_workspace_bytes(C.byref(index.desc), nq, R, k, qmode)
+    ws = index._ws.get("f64")
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 256), dtype=torch.uint8, device=index.device)
+        index._ws["f64"] = ws
+    s = stream if stream is not None else _lib.stream_handle(index.device)
+    check("lmi_bucket_topk_f64", lib.lmi_bucket_topk_f64(
+        C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(classes), R, k, qmode, float(eps),
+        ptr(out_d), ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
+    if not fallback_count:
+        return out_d, out_pos, status
+    n = C.c_int32(0)
+    check("lmi_refine_fallback_count", lib.lmi_refine_fallback_count(
+        ptr(ws), C.byref(index.desc), nq, R, k, qmode, C.byref(n), s))
+    return out_d, out_pos, status, int(n.value)
+
+
 def merge_topk(d_in: torch.Tensor, pos_in: torch.Tensor, k: int, stream=None):
-    """K3: merge [G, rows, k] lists -> [rows, k] by (distance, global position)."""
+    """K3: merge [G, rows, k] lists -> [rows, k] by (distance, global position);
+    float32 (lmi_merge_topk) or float64 (lmi_merge_topk_f64) distances."""
     G = d_in.shape[0]
     rows = d_in[0].numel() // k
-    out_d = torch.empty(d_in.shape[1:], dtype=torch.float32, device=d_in.device)
+    f64 = d_in.dtype == torch.float64
+    out_d = torch.empty(d_in.shape[1:], dtype=d_in.dtype, device=d_in.device)
     out_pos = torch.empty(d_in.shape[1:], dtype=torch.int32, device=d_in.device)
     s = stream if stream is not None else _lib.stream_handle(d_in.device)
-    check("lmi_merge_topk", _lib.load().lmi_merge_topk(ptr(d_in.contiguous()), ptr(pos_in.contiguous()),
-                                                       G, rows, k, ptr(out_d), ptr(out_pos), s))
+    fn = "lmi_merge_topk_f64" if f64 else "lmi_merge_topk"
+    check(fn, getattr(_lib.load(), fn)(ptr(d_in.contiguous()), ptr(pos_in.contiguous()), G, rows, k,
+                                       ptr(out_d), ptr(out_pos), s))
     return out_d, out_pos
 
 
 def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k_round: int,
            k_final: int, bucket_size: np.ndarray, pos_to_id: np.ndarray, use_threshold: bool,
            thr_round0: Optional[np.ndarray] = None):
-    """A5 on the host (lmi_replay): per-(query, probe) lists -> reference output."""
+    """A5 on the host (lmi_replay, or lmi_replay_f64 for float64 lists):
+    per-(query, probe) lists -> reference output."""
     classes = np.ascontiguousarray(classes, dtype=np.int32)
     if classes.ndim == 1:
         classes = classes[:, None]
     nq, R = classes.shape
-    lists_d = np.ascontiguousarray(lists_d, dtype=np.float32).reshape(nq, R, -1)
+    f64 = np.asarray(lists_d).dtype == np.float64
+    lists_d = np.ascontiguousarray(lists_d, dtype=np.float64 if f64 else np.float32).reshape(nq, R, -1)
     lists_pos = np.ascontiguousarray(lists_pos, dtype=np.int32).reshape(nq, R, -1)
     k_list = lists_d.shape[2]
     bucket_size = np.ascontiguousarray(bucket_size, dtype=np.int64)
@@ -439,7 +478,8 @@ def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k
         if thr.shape != (nq,):
             raise ValueError("threshold_dist must have one value per query")
     w_out = C.c_int32(0)
-    check("lmi_replay", _lib.load().lmi_replay(
+    fn = "lmi_replay_f64" if f64 else "lmi_replay"
+    check(fn, getattr(_lib.load(), fn)(
         classes.ctypes.data, nq, R, k_list, lists_d.ctypes.data, lists_pos.ctypes.data,
         k_round, k_final, bucket_size.ctypes.data, bucket_size.size, pos_to_id.ctypes.data,
         pos_to_id.size, int(bool(use_threshold)), ptr(thr), dists.ctypes.data, anns.ctypes.data,
@@ -450,15 +490,17 @@ def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k
 def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch.Tensor, *,
                   k_round: int, k_final: int, bucket_size: torch.Tensor, pos_to_id: torch.Tensor,
                   use_threshold: bool, thr_round0: Optional[torch.Tensor] = None, stream=None):
-    """A5 on the device (lmi_replay_device): same results as `replay`, device
-    tensors in and out: (dists f64 [nq, w], anns uint32-as-int32 [nq, w], status)."""
+    """A5 on the device (lmi_replay_device, or lmi_replay_device_f64 for
+    float64 lists): same results as `replay`, device tensors in and out:
+    (dists f64 [nq, w], anns uint32-as-int32 [nq, w], status)."""
     lib = _lib.load()
     dev = lists_d.device
     classes = _as_torch(classes, dev, torch.int32)
     if classes.dim() == 1:
         classes = classes[:, None].contiguous()
     nq, R = classes.shape
-    lists_d = _as_torch(lists_d, dev, torch.float32).reshape(nq, R, -1).contiguous()
+    f64 = lists_d.dtype == torch.float64
+    lists_d = _as_torch(lists_d, dev, torch.float64 if f64 else torch.float32).reshape(nq, R, -1).contiguous()
     lists_pos = _as_torch(lists_pos, dev, torch.int32).reshape(nq, R, -1).contiguous()
     k_list = lists_d.shape[2]
     w = k_round if R == 1 else k_final
@@ -474,7 +516,8 @@ def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch
         if thr.numel() != nq:
             raise ValueError("threshold_dist must have one value per query")
     s = stream if stream is not None else _lib.stream_handle(dev)
-    check("lmi_replay_device", lib.lmi_replay_device(
+    fn = "lmi_replay_device_f64" if f64 else "lmi_replay_device"
+    check(fn, getattr(lib, fn)(
         ptr(classes), nq, R, k_list, ptr(lists_d), ptr(lists_pos), k_round, k_final,
         ptr(bucket_size), n_b, ptr(pos_to_id), int(pos_to_id.numel()), int(bool(use_threshold)),
         ptr(thr), ptr(dists), ptr(anns), ptr(status), ptr(ws), ws.numel(), s))
@@ -491,6 +534,7 @@ class Searcher:
         self.router = router
         self.group = group
         self._pinned = {}
+        self._qcheck = None
 
     def _host(self, name, shape, dtype):
         buf = self._pinned.get(name)
@@ -499,15 +543,42 @@ class Searcher:
             self._pinned[name] = buf
         return buf
 
+    def qmode(self, q_search: torch.Tensor) -> int:
+        """The scan's query path, decided before the scan: LMI_Q_F16 (exact
+        fp16 MFMA products) when the corpus is stored fp16 and every query
+        value is fp16-representable, else LMI_Q_F32 (exact fp32 MFMA).  The
+        check is one device reduction, run once per query batch (cached by the
+        tensor's storage, shape and version counter); every rank holds the same
+        batch, so every rank decides the same."""
+        if self.index.storage != "f16":
+            return _lib.LMI_Q_F32
+        q = q_search
+        key = (q.data_ptr(), q._version, tuple(q.shape), q.dtype, q.device)
+        if self._qcheck is not None and self._qcheck[0] == key:
+            return self._qcheck[1]
+        mode = _lib.LMI_Q_F16 if fp16_exact(q) else _lib.LMI_Q_F32
+        self._qcheck = (key, mode)
+        return mode
+
+    def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool):
+        """K2 on this shard (+ all-gather and K3 for G > 1 ranks, the status
+        words riding along so every rank sees every rank's bits)."""
+        if f64:
+            d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode)
+        else:
+            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode)
+        if self.index.world > 1:
+            from .dist import gather_merge
+            d, pos, status = gather_merge(d, pos, k_list, self.group, status=status)
+        return d, pos, status
+
     def lists(self, q_nav: torch.Tensor, q_search: torch.Tensor, R: int, k_list: int,
-              classes: Optional[torch.Tensor] = None):
+              classes: Optional[torch.Tensor] = None, dist: str = "f32"):
         """Device part: router + scan (+ RCCL merge).  Returns device tensors."""
         if classes is None:
             classes = self.route(q_nav, R)
-        d, pos, status = bucket_topk(self.index, q_search, classes, k_list)
-        if self.index.world > 1:
-            from .dist import gather_merge
-            d, pos = gather_merge(d, pos, k_list, self.group)
+        q_search = _as_torch(q_search, self.index.device, torch.float32)
+        d, pos, status = self._scan(q_search, classes, k_list, self.qmode(q_search), dist == "f64")
         return classes, d, pos, status
 
     def route(self, q_nav, R: int) -> torch.Tensor:
@@ -532,7 +603,7 @@ class Searcher:
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
                use_threshold: bool = True, classes: Optional[torch.Tensor] = None,
                timings: Optional[dict] = None, replay_on: str = "device",
-               semantics: str = "reference"):
+               semantics: str = "reference", dist: str = "f32"):
         """Whole hot path for one batch -> (dists f64 [nq, w], anns u32 [nq, w]).
 
         semantics="reference" (default) reproduces LearnedIndex.search's round
@@ -541,6 +612,11 @@ class Searcher:
         position), of the union of each query's R probed buckets (K3 merge of
         its R lists on the device; fewer than k objects pad with (10000, 0)),
         the option SURVEY.md §8(a) asks for beside the reference semantics.
+
+        dist="f32": distances in float32, the reference's arithmetic when the
+        corpus and the queries are both float32; dist="f64": float64 distances
+        (lmi_bucket_topk_f64), its arithmetic otherwise — e.g. the real clip768
+        'emb', which is float16 (utils.py:11, :19).
 
         replay_on="device" (default) runs the reference's round merge on the GPU
         (lmi_replay_device) and copies back only the result; "host" copies the
@@ -552,10 +628,13 @@ class Searcher:
             raise ValueError("replay_on must be 'device' or 'host'")
         if semantics not in ("reference", "exact"):
             raise ValueError("semantics must be 'reference' or 'exact'")
+        if dist not in ("f32", "f64"):
+            raise ValueError("dist must be 'f32' or 'f64'")
         k_list = k_round if semantics == "reference" else max(k_round, k)
         if k_list > _lib.LMI_MAX_K:
             raise ValueError(f"k={k_list} > {_lib.LMI_MAX_K}")
         dev = self.index.device
+        f64 = dist == "f64"
         sync = (lambda: torch.cuda.current_stream(dev).synchronize()) if timings is not None else None
 
         def lap(name, t0):
@@ -566,21 +645,24 @@ class Searcher:
                 return t1
             return t0
 
-        def scan(qmode=None):
-            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode)
-            if self.index.world > 1:
-                from .dist import gather_merge
-                d, pos = gather_merge(d, pos, k_list, self.group)
-            return d, pos, status
-
         t0 = time.perf_counter()
+        q_search = _as_torch(q_search, dev, torch.float32)
+        qmode = self.qmode(q_search)
         if classes is None:
             classes = self.route(q_nav, R)
         t0 = lap("router", t0)
-        d, pos, status = scan()
+        d, pos, status = self._scan(q_search, classes, k_list, qmode, f64)
         t0 = lap("scan", t0)
         nq = classes.shape[0]
         h_st = self._host("st", (2,), torch.int32)
+
+        def check_status(st, rst=0):
+            # every rank holds the OR of all ranks' scan bits (they rode the
+            # all-gather) and runs the same replay: all ranks raise together
+            if st & _lib.LMI_STATUS_INTERNAL or rst:
+                raise RuntimeError(f"search: internal status {st}/{rst}")
+            return bool(st & _lib.LMI_STATUS_QUERY_NOT_F16)
+
         if semantics == "exact":
             _, p2id = self._device_tables()
 
@@ -603,12 +685,14 @@ class Searcher:
             h_st[0:1].copy_(status, non_blocking=True)
             torch.cuda.current_stream(dev).synchronize()
             t0 = lap("d2h", t0)
-            if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL:
-                raise RuntimeError(f"search: internal status {int(h_st[0])}")
-            if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
-                rd, ra = exact(*scan(qmode=_lib.LMI_Q_F32)[:2])
+            if check_status(int(h_st[0])):
+                # the cached fp16 check was stale: redo with exact fp32 MFMA
+                d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64)
+                rd, ra = exact(d, pos)
                 h_d.copy_(rd)
                 h_a.copy_(ra)
+                h_st[0:1].copy_(status)
+                check_status(int(h_st[0]) & ~_lib.LMI_STATUS_QUERY_NOT_F16)
             return h_d.numpy().copy(), h_a.numpy().view(np.uint32).copy()
         if replay_on == "device":
             bsz, p2id = self._device_tables()
@@ -630,17 +714,17 @@ class Searcher:
             h_st[1:2].copy_(rst, non_blocking=True)
             torch.cuda.current_stream(dev).synchronize()
             t0 = lap("d2h", t0)
-            if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL or int(h_st[1]):
-                raise RuntimeError(f"search: internal status {int(h_st[0])}/{int(h_st[1])}")
-            if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
-                # queries are not fp16-exact: redo the scan with exact fp32 MFMA
-                d, pos, _ = scan(qmode=_lib.LMI_Q_F32)
+            if check_status(int(h_st[0]), int(h_st[1])):
+                d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64)
                 rd, ra, rst = run_replay(d, pos)
                 h_d.copy_(rd)
                 h_a.copy_(ra)
+                h_st[0:1].copy_(status)
+                h_st[1:2].copy_(rst)
+                check_status(int(h_st[0]) & ~_lib.LMI_STATUS_QUERY_NOT_F16, int(h_st[1]))
             return h_d.numpy(), h_a.numpy().view(np.uint32)
         h_cls = self._host("cls", (nq, R), torch.int32)
-        h_d = self._host("d", tuple(d.shape), torch.float32)
+        h_d = self._host("d", tuple(d.shape), d.dtype)
         h_pos = self._host("pos", tuple(pos.shape), torch.int32)
         h_cls.copy_(classes, non_blocking=True)
         h_d.copy_(d, non_blocking=True)
@@ -648,12 +732,12 @@ class Searcher:
         h_st[0:1].copy_(status, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
         t0 = lap("d2h", t0)
-        if int(h_st[0]) & _lib.LMI_STATUS_INTERNAL:
-            raise RuntimeError("lmi_bucket_topk: a list held an out-of-range row (internal error)")
-        if int(h_st[0]) & _lib.LMI_STATUS_QUERY_NOT_F16:
-            d, pos, _ = scan(qmode=_lib.LMI_Q_F32)
+        if check_status(int(h_st[0])):
+            d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64)
             h_d.copy_(d)
             h_pos.copy_(pos)
+            h_st[0:1].copy_(status)
+            check_status(int(h_st[0]) & ~_lib.LMI_STATUS_QUERY_NOT_F16)
         out = replay(h_cls.numpy(), h_d.numpy(), h_pos.numpy(), k_round=k_round, k_final=k,
                      bucket_size=self.index.bucket_size, pos_to_id=self.index.pos_to_id,
                      use_threshold=use_threshold)

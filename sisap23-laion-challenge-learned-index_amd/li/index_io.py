@@ -13,7 +13,8 @@ classes (same module paths `li.LearnedIndex` / `li.model`, same attributes), so
 
 The unpickler resolves only an allow-list of globals: the reference's `li.*`
 classes (mapped onto this package), torch's tensor/parameter rebuild helpers,
-`torch.nn` modules, `torch.optim` optimisers and a few builtins/collections.
+the exact torch classes such an index holds (Linear, ReLU, Sequential,
+CrossEntropyLoss, Adam) and a few builtins/collections.
 Tensor storages embedded by plain pickle are decoded with
 `torch.load(..., weights_only=True)`.  Anything else raises
 `pickle.UnpicklingError`.
@@ -55,6 +56,15 @@ _BUILTINS = {
     ("builtins", "list"),
     ("builtins", "tuple"),
 }
+# the torch classes a reference index pickles (model.py:18-83 Model layers,
+# model.py:114-147 loss and optimiser): nothing else from torch.nn / torch.optim
+_TORCH_CLASSES = {
+    ("torch.nn.modules.linear", "Linear"),
+    ("torch.nn.modules.activation", "ReLU"),
+    ("torch.nn.modules.container", "Sequential"),
+    ("torch.nn.modules.loss", "CrossEntropyLoss"),
+    ("torch.optim.adam", "Adam"),
+}
 
 
 def _load_storage(b: bytes):
@@ -69,12 +79,9 @@ class _IndexUnpickler(pickle.Unpickler):
             return getattr(importlib.import_module(module), name)
         if (module, name) == ("torch.storage", "_load_from_bytes"):
             return _load_storage
-        if (module, name) in _TORCH_FUNCS or (module, name) in _BUILTINS:
+        if (module, name) in _TORCH_FUNCS or (module, name) in _BUILTINS or \
+                (module, name) in _TORCH_CLASSES:
             return super().find_class(module, name)
-        if module.startswith("torch.nn.modules.") or module.startswith("torch.optim."):
-            obj = super().find_class(module, name)
-            if isinstance(obj, type):
-                return obj
         if module == "torch" and name.endswith("Storage"):
             return super().find_class(module, name)
         raise pickle.UnpicklingError(f"index pickle: global {module}.{name} is not allowed")

@@ -155,11 +155,16 @@ class NeuralNetwork(Logger):
         return out.cpu().numpy().astype(np.int64)
 
     def predict_proba(self, data_X: torch.FloatTensor):
-        """(probs, classes) over all classes, descending (model.py:214-229)."""
+        """(probs, classes) over all classes, descending (model.py:214-229).
+
+        A 1-D input raises IndexError as the reference does: it takes the
+        softmax over dim 0 and then `prob.topk(prob.shape[1])` (model.py:222-227)
+        indexes a shape of length 1."""
         self.model.eval()
         x = data_X.to(self.device)
         if x.dim() == 1:
-            x = x[None]
+            raise IndexError("tuple index out of range (predict_proba of a 1-D input, "
+                             "reference model.py:227)")
         r = self.router()
         classes, probs = r.topr(x, r.n_classes, with_probs=True)
         return probs.cpu().numpy(), classes.cpu().numpy().astype(np.int64)

@@ -75,6 +75,14 @@ def _worker(rank, world, port, result_path):
     gpos, _ = BucketLayout.from_labels(w["labels"], C).shard(rank, world)
     d, p = _shard_lists(w, classes, R, k, C, gpos)
     md, mp_ = gather_merge(torch.from_numpy(d), torch.from_numpy(p), k, merge=_oracle_merge)
+    # float64 lists (lmi_bucket_topk_f64) through the same collective, with
+    # every rank's status word OR-ed into the result on every rank
+    md64, mp64, st = gather_merge(torch.from_numpy(d.astype(np.float64)), torch.from_numpy(p), k,
+                                  merge=_oracle_merge,
+                                  status=torch.tensor([1 << rank], dtype=torch.int32))
+    f64_ok = md64.dtype == torch.float64 and \
+        np.array_equal(md64.numpy().astype(np.float32), md.numpy()) and \
+        np.array_equal(mp64.numpy(), mp_.numpy()) and int(st[0]) == (1 << world) - 1
 
     class _OracleRouter:  # K1's contract on the CPU: per-query top-R classes
         def topr(self, x, R):
@@ -89,7 +97,7 @@ def _worker(rank, world, port, result_path):
         # shape-independent and is checked bitwise in test_gpu_parity.py)
         ok = O.compare_lists(fd, fp, md.numpy(), mp_.numpy()) == 0 and \
             np.array_equal(np.isfinite(md.numpy()), np.isfinite(fd)) and \
-            np.array_equal(routed, classes)
+            np.array_equal(routed, classes) and f64_ok
         with open(result_path, "w") as f:
             f.write("ok" if ok else "mismatch")
     dist.barrier()

@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
@@ -33,6 +33,15 @@ def test_invalid_arguments_fail_loudly_without_a_device():
     d = _lib.IndexDesc()
     rc = lib.lmi_bucket_topk(C.byref(d), None, 4, 768, None, 2, 10, 0, None, None, None, None, 0, None)
     assert rc == _lib.LMI_E_INVALID
+    rc = lib.lmi_bucket_topk_f64(C.byref(d), None, 4, 768, None, 2, 17, 0, _lib.LMI_REFINE_EPS, None,
+                                 None, None, None, 0, None)
+    assert rc == _lib.LMI_E_INVALID and b"k=17" in lib.lmi_last_error()
+    d.d = 2048
+    rc = lib.lmi_bucket_topk_f64(C.byref(d), None, 4, 768, None, 2, 10, 0, _lib.LMI_REFINE_EPS, None,
+                                 None, None, None, 0, None)
+    assert rc == _lib.LMI_E_INVALID and b"d=2048" in lib.lmi_last_error()
+    rc = lib.lmi_merge_topk_f64(None, None, 2, 10, 0, None, None, None)
+    assert rc == _lib.LMI_E_INVALID and b"k=0" in lib.lmi_last_error()
 
 
 def test_plan_chunks():
@@ -119,3 +128,27 @@ def test_subcluster_layout_keeps_rows_and_chunk_order():
     assert torch.equal(ix.inv_norm, base.inv_norm[idx])
     nrm = ix.chunk_centroid[:, : ix.d].norm(dim=1)
     assert torch.allclose(nrm, torch.ones_like(nrm), atol=1e-5)
+
+
+def test_dist_dtype_follows_sklearn_rule():
+    """float32 DataFrame + float32 queries: the reference's float32 branch;
+    float16 (the real clip768 'emb') or float64 on either side: float64
+    (utils.py:11 -> check_pairwise_arrays)."""
+    import pandas as pd
+    from li.LearnedIndex import dist_dtype
+    x = np.zeros((4, 3), np.float32)
+    assert dist_dtype(pd.DataFrame(x), x) == "f32"
+    assert dist_dtype(pd.DataFrame(x.astype(np.float16)), x) == "f64"
+    assert dist_dtype(pd.DataFrame(x), x.astype(np.float16)) == "f64"
+    assert dist_dtype(pd.DataFrame(x).assign(category=1), x) == "f32"
+    assert dist_dtype(x.astype(np.float64), x) == "f64"
+
+
+def test_content_key_sees_in_place_changes():
+    import pandas as pd
+    from li.LearnedIndex import content_key
+    df = pd.DataFrame(np.random.default_rng(0).standard_normal((50, 8)).astype(np.float16))
+    k0 = content_key(df)
+    assert content_key(df) == k0  # (a copy in another memory order may miss: safe)
+    df.iloc[37, 5] = df.iloc[37, 5] + np.float16(1)
+    assert content_key(df) != k0

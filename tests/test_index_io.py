@@ -47,6 +47,17 @@ def test_unpickler_refuses_other_globals(tmp_path):
         index_io.load_index(str(p))
 
 
+@pytest.mark.parametrize("obj", [torch.nn.Conv1d(2, 2, 1), torch.optim.lr_scheduler.partial(print),
+                                 torch.nn.modules.linear.Identity()])
+def test_unpickler_refuses_torch_names_outside_the_allow_list(tmp_path, obj):
+    # any other torch.nn module, and names torch.optim re-exports (functools.partial)
+    p = tmp_path / "other.pkl"
+    with open(p, "wb") as f:
+        pickle.dump(obj, f)
+    with pytest.raises(pickle.UnpicklingError):
+        index_io.load_index(str(p))
+
+
 def test_save_roundtrip_keeps_reference_format(tmp_path):
     ix = index_io.load_index(PKL)
     ix._index = object()  # a device cache must not be written

@@ -13,7 +13,36 @@ def clustered(n=6000, d=768, nq=200, C=16, arch="MLP", seed=7, label_mode="route
                 'skewed'  Dirichlet-skewed labels with empty and tiny buckets
                 'dup'     'skewed' plus exact duplicate vectors in the same
                           bucket (tied distances)
+                'near'    'skewed' plus near-duplicates: 10% of the rows are
+                          copies of another row of their bucket with one or two
+                          components moved by one fp16 ulp (distances that
+                          differ by 1e-9..1e-6, below fp32 rounding of a
+                          768-term dot), 2.5% exact duplicates, and 10% of the
+                          queries one ulp away from a corpus row
     """
+    if label_mode == "near":
+        w = clustered(n=n, d=d, nq=nq, C=C, arch=arch, seed=seed, label_mode="skewed",
+                      n_centres=n_centres)
+        x, xn, q, labels = w["x"], w["xn"], w["q"], w["labels"]
+        rng = np.random.Generator(np.random.PCG64(seed + 6))
+        perm = rng.permutation(n)
+        n_near, n_dup = n // 10, n // 40
+        src, dst = perm[:n_near + n_dup], perm[n_near + n_dup:2 * (n_near + n_dup)]
+        x16 = x.astype(np.float16)
+        for j, (s, t) in enumerate(zip(src, dst)):
+            x16[t] = x16[s]
+            xn[t] = xn[s]
+            labels[t] = labels[s]
+            if j < n_near:
+                for e in rng.choice(d, 1 + (j & 1), replace=False):
+                    x16[t, e] = np.nextafter(x16[t, e], np.float16(np.inf if (j >> 1) & 1 else -np.inf))
+        q16 = q.astype(np.float16)
+        for i in rng.choice(nq, nq // 10, replace=False):
+            q16[i] = x16[rng.integers(n)]
+            e = rng.integers(d)
+            q16[i, e] = np.nextafter(q16[i, e], np.float16(np.inf))
+        w.update(x=x16.astype(np.float32), xn=xn, q=q16.astype(np.float32), labels=labels)
+        return w
     x, cen = synth.np_mixture(n, d, n_centres, seed)
     q, _ = synth.np_mixture(nq, d, n_centres, seed + 1, centres=cen)
     P = synth.np_projection(d, 96, seed + 2)
