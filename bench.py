@@ -7,9 +7,10 @@ One step = one search of the whole 10k-query batch exactly as the reference
 times it (search.py:116-141): router (K1) + per-(query, probe) bucket scan
 (K2) [+ RCCL all-gather + K3 merge for N > 1] + D2H of the lists + the replay
 of the reference's merge (host C++).  Inputs (corpus index, queries) are
-resident in HBM before the timed region.  N > 1: launched by torchrun, one
-process per GPU, the corpus striped over the ranks; all ranks search the same
-batch (strong scaling: value = nq / max-over-ranks step time).
+resident in HBM before the timed region.  N > 1: one process per GPU,
+started by torchrun or, without one, by this script itself (launch_ranks);
+the corpus striped over the ranks; all ranks search the same batch (strong
+scaling: value = nq / max-over-ranks step time, the RCCL all-gather inside).
 
 Besides the JSON fields of the driver contract the line carries:
   roofline      K2 scan kernel: algorithmic bytes per launch / its average
@@ -174,7 +175,62 @@ def pmc_traffic(kernel_ms):
     return byts, os.path.relpath(files[-1], ROOT)
 
 
+def _gpus_arg(argv):
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def launch_ranks(n: int, argv, script: str = None) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes of
+    this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, one
+    GPU each: LOCAL_RANK = rank mod the visible device count, so on a 1-GPU box
+    with LMI_DIST_BACKEND=gloo the ranks share device 0 as a control-flow
+    rehearsal), relay rank 0's JSON line, and exit with the first failing
+    rank's code (the others are stopped: they would wait at a collective).
+    This process never initialises the GPU (it only counts devices)."""
+    import socket
+    import subprocess
+    ndev = max(1, torch.cuda.device_count())
+    if n > ndev and os.environ.get("LMI_DIST_BACKEND") != "gloo":
+        print(f"[bench] --gpus {n} but {ndev} visible GPU(s): RCCL needs one GPU per rank "
+              f"(LMI_DIST_BACKEND=gloo rehearses the ranks on shared devices)", file=sys.stderr)
+        return 2
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r % ndev), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv),
+                                      env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c
+                for o in live:
+                    procs[o].terminate()
+        time.sleep(0.05)
+    out = procs[0].stdout.read().decode()
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return rc
+
+
 def main():
+    if "WORLD_SIZE" not in os.environ and _gpus_arg(sys.argv[1:]) > 1:
+        sys.exit(launch_ranks(_gpus_arg(sys.argv[1:]), sys.argv[1:]))
     # Libraries print banners to stdout (RCCL's version block at communicator
     # init): fd 1 goes to stderr for the run, and only the JSON line is written
     # to the original stdout.
@@ -204,7 +260,8 @@ def main():
     if args.chunk_rows is None:
         args.chunk_rows = 8192 if world == 1 else 4096 if world <= 4 else 2048
     if world != args.gpus:
-        log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+        log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world} (set by the launcher); "
+            f"using {world}")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     group = None

@@ -560,16 +560,21 @@ class Searcher:
         self._qcheck = (key, mode)
         return mode
 
-    def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool):
+    def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool, lap=None):
         """K2 on this shard (+ all-gather and K3 for G > 1 ranks, the status
-        words riding along so every rank sees every rank's bits)."""
+        words riding along so every rank sees every rank's bits).  `lap`
+        (measurement only) is called after the scan and after the exchange."""
         if f64:
             d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode)
         else:
             d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode)
+        if lap:
+            lap("scan")
         if self.index.world > 1:
             from .dist import gather_merge
             d, pos, status = gather_merge(d, pos, k_list, self.group, status=status)
+            if lap:
+                lap("allgather")
         return d, pos, status
 
     def lists(self, q_nav: torch.Tensor, q_search: torch.Tensor, R: int, k_list: int,
@@ -651,8 +656,13 @@ class Searcher:
         if classes is None:
             classes = self.route(q_nav, R)
         t0 = lap("router", t0)
-        d, pos, status = self._scan(q_search, classes, k_list, qmode, f64)
-        t0 = lap("scan", t0)
+        tl = [t0]
+
+        def lap_at(name):
+            tl[0] = lap(name, tl[0])
+
+        d, pos, status = self._scan(q_search, classes, k_list, qmode, f64, lap_at if sync else None)
+        t0 = tl[0]
         nq = classes.shape[0]
         h_st = self._host("st", (2,), torch.int32)
 

@@ -1,18 +1,13 @@
 #!/bin/bash
-# Control-flow rehearsal of the multi-rank bench on a 1-GPU box: two ranks,
-# both on device 0 (RANK 0/1, WORLD_SIZE 2, LOCAL_RANK 0), gloo (RCCL refuses
-# two ranks on one device; collectives stage through host memory),
-# 1M workload.  Checks the collectives line up (barriers, all-gathers, the
-# max-over-ranks clock); the per-rank times are not a scaling measurement.
+# Control-flow rehearsal of the multi-rank bench on a 1-GPU box: bench.py
+# launches its own two ranks (bench.launch_ranks), both on device 0, over gloo
+# (RCCL refuses two ranks on one device; collectives stage through host
+# memory), 1M workload.  Checks the launcher, the barriers, the all-gathers and
+# the max-over-ranks clock line up: one JSON line with n_gpus 2.  The per-rank
+# times are not a scaling measurement.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
-export MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 WORLD_SIZE=2 LOCAL_RANK=0 LMI_DIST_BACKEND=gloo
-RANK=1 timeout -k 10 300 python -u bench.py --gpus 2 --scale 1M --steps 3 --warmup 1 \
-    > gpurun_out/r1.json 2> gpurun_out/r1.err &
-p1=$!
-RANK=0 timeout -k 10 300 python -u bench.py --gpus 2 --scale 1M --steps 3 --warmup 1 \
-    > gpurun_out/r0.json 2> gpurun_out/r0.err
-rc0=$?
-wait $p1; rc1=$?
-echo "rank0 rc=$rc0 rank1 rc=$rc1"
-cut -c1-400 gpurun_out/r0.json; grep -v amdgpu.ids gpurun_out/r0.err | tail -5; grep -v amdgpu.ids gpurun_out/r1.err | tail -5
-[ $rc0 -eq 0 ] && [ $rc1 -eq 0 ]
+LMI_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --scale 1M --steps 3 --warmup 1 \
+    --no-cpu-baseline > gpurun_out/two_ranks.json 2> gpurun_out/two_ranks.err
+rc=$?
+echo "two-rank bench rc=$rc"; cut -c1-600 gpurun_out/two_ranks.json; grep -v amdgpu.ids gpurun_out/two_ranks.err | tail -5
+exit $rc
