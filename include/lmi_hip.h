@@ -151,7 +151,7 @@ int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t 
  * sklearn promotes to float64 (utils.py:11, :19; check_pairwise_arrays) and
  * the threshold test (utils.py:23) and the merges (LearnedIndex.py:86-97) see
  * float64 values.  lmi_bucket_topk_f64 returns those float64 lists:
- *   - the fp32 scan keeps the top-KL (KL = 16 > k) per (query, probe);
+ *   - the fp32 scan keeps the top-KL (KL = 15 for k <= 10, else 16) per (query, probe);
  *   - every list entry within 2*eps of the fp32 k-th distance is recomputed
  *     in float64 from the stored row (sklearn normalize + dot; exact fp16
  *     inputs), sorted by (d64, position); with fewer than KL entries in that

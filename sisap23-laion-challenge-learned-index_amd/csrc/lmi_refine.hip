@@ -286,7 +286,7 @@ struct RefineWs {
     size_t scan, ld, lrow, lpos, failed, nfailed, total;
 };
 
-int pick_kl_f64(int k) { return k <= 10 ? 16 : LMI_MAX_K; }
+int pick_kl_f64(int k) { return k <= 10 ? 15 : LMI_MAX_K; }
 
 RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     RefineWs w{};

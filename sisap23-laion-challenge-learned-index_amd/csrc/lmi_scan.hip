@@ -1166,9 +1166,11 @@ constexpr int NSLOT = 2 * NST;         // two blocks: one read, the next in flig
 constexpr int NW = 8;
 constexpr int QB = NW * 32;
 constexpr int NQF = D / 16;
-constexpr int KL = 10;
-constexpr size_t lds_bytes = (size_t)NSLOT * STAGE + (size_t)NW * KL * 64 * 8 + 64;
-static_assert(lds_bytes <= 160 * 1024, "LDS budget");
+// lists of KL = 10 (k <= 10) or 15 (the float64 mode's 10 + 5 guard entries,
+// the most the 160-KiB LDS holds beside the ring)
+template <int KL>
+constexpr size_t lds_bytes() { return (size_t)NSLOT * STAGE + (size_t)NW * KL * 64 * 8 + 64; }
+static_assert(lds_bytes<15>() <= 160 * 1024, "LDS budget");
 }  // namespace v3
 
 
@@ -1212,26 +1214,53 @@ __device__ __forceinline__ void list_store(uint32_t addr, const uint64_t (&L)[KL
 }
 template <int KL, int OFF = 0>
 __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
-    static_assert(KL == 10, "one asm block of 10 reads");
-    // all reads in flight, one wait (a wait per read would serialise ~10 LDS
+    static_assert(KL == 10 || KL == 15, "one asm block of 10 or 15 reads");
+    // all reads in flight, one wait (a wait per read would serialise the LDS
     // round trips); one asm statement so no use can slip before the wait
-    asm volatile(
-        "ds_read_b64 %0, %10 offset:%11\n\t"
-        "ds_read_b64 %1, %10 offset:%12\n\t"
-        "ds_read_b64 %2, %10 offset:%13\n\t"
-        "ds_read_b64 %3, %10 offset:%14\n\t"
-        "ds_read_b64 %4, %10 offset:%15\n\t"
-        "ds_read_b64 %5, %10 offset:%16\n\t"
-        "ds_read_b64 %6, %10 offset:%17\n\t"
-        "ds_read_b64 %7, %10 offset:%18\n\t"
-        "ds_read_b64 %8, %10 offset:%19\n\t"
-        "ds_read_b64 %9, %10 offset:%20\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
-          "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9])
-        : "v"(addr), "i"(OFF), "i"(OFF + 512), "i"(OFF + 1024), "i"(OFF + 1536), "i"(OFF + 2048),
-          "i"(OFF + 2560), "i"(OFF + 3072), "i"(OFF + 3584), "i"(OFF + 4096), "i"(OFF + 4608)
-        : "memory");
+    if constexpr (KL == 10) {
+        asm volatile(
+            "ds_read_b64 %0, %10 offset:%11\n\t"
+            "ds_read_b64 %1, %10 offset:%12\n\t"
+            "ds_read_b64 %2, %10 offset:%13\n\t"
+            "ds_read_b64 %3, %10 offset:%14\n\t"
+            "ds_read_b64 %4, %10 offset:%15\n\t"
+            "ds_read_b64 %5, %10 offset:%16\n\t"
+            "ds_read_b64 %6, %10 offset:%17\n\t"
+            "ds_read_b64 %7, %10 offset:%18\n\t"
+            "ds_read_b64 %8, %10 offset:%19\n\t"
+            "ds_read_b64 %9, %10 offset:%20\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
+              "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9])
+            : "v"(addr), "i"(OFF), "i"(OFF + 512), "i"(OFF + 1024), "i"(OFF + 1536), "i"(OFF + 2048),
+              "i"(OFF + 2560), "i"(OFF + 3072), "i"(OFF + 3584), "i"(OFF + 4096), "i"(OFF + 4608)
+            : "memory");
+    } else {
+        asm volatile(
+            "ds_read_b64 %0, %15 offset:%16\n\t"
+            "ds_read_b64 %1, %15 offset:%17\n\t"
+            "ds_read_b64 %2, %15 offset:%18\n\t"
+            "ds_read_b64 %3, %15 offset:%19\n\t"
+            "ds_read_b64 %4, %15 offset:%20\n\t"
+            "ds_read_b64 %5, %15 offset:%21\n\t"
+            "ds_read_b64 %6, %15 offset:%22\n\t"
+            "ds_read_b64 %7, %15 offset:%23\n\t"
+            "ds_read_b64 %8, %15 offset:%24\n\t"
+            "ds_read_b64 %9, %15 offset:%25\n\t"
+            "ds_read_b64 %10, %15 offset:%26\n\t"
+            "ds_read_b64 %11, %15 offset:%27\n\t"
+            "ds_read_b64 %12, %15 offset:%28\n\t"
+            "ds_read_b64 %13, %15 offset:%29\n\t"
+            "ds_read_b64 %14, %15 offset:%30\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
+              "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9]), "=&v"(L[10]), "=&v"(L[11]),
+              "=&v"(L[12]), "=&v"(L[13]), "=&v"(L[14])
+            : "v"(addr), "i"(OFF), "i"(OFF + 512), "i"(OFF + 1024), "i"(OFF + 1536), "i"(OFF + 2048),
+              "i"(OFF + 2560), "i"(OFF + 3072), "i"(OFF + 3584), "i"(OFF + 4096), "i"(OFF + 4608),
+              "i"(OFF + 5120), "i"(OFF + 5632), "i"(OFF + 6144), "i"(OFF + 6656), "i"(OFF + 7168)
+            : "memory");
+    }
 }
 
 // In-place odd-even transposition sort of a short list (ascending keys).
@@ -1295,7 +1324,7 @@ __device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
     return x;
 }
 
-template <int ABL = 0>
+template <int KL, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
     // diagnostic builds only (results wrong for ABL != 0): 1 no insertion,
@@ -1681,16 +1710,27 @@ bool v2_eligible(const lmi_index_desc* idx, int qmode) {
     return idx->dtype == LMI_F16 && qmode == LMI_Q_F16 && idx->d_pad == v2::D;
 }
 
-int pick_kl(int k) { return k <= 10 ? 10 : 16; }
+bool v3_capable(const lmi_index_desc* idx, int qmode) {
+    if (getenv("LMI_SCAN_V2")) return false;  // diagnostic switch: force the 4-wave ring
+    return v2_eligible(idx, qmode);
+}
+
+// list length of the scan: 10 (k <= 10), 15 (k <= 15 on scan v3: the float64
+// mode's 10 + 5 guard entries), else 16
+int pick_kl(const lmi_index_desc* idx, int qmode, int k) {
+    if (k <= 10) return 10;
+    if (k <= 15 && v3_capable(idx, qmode)) return 15;
+    return 16;
+}
 
 bool v3_eligible(const lmi_index_desc* idx, int qmode, int k) {
-    if (getenv("LMI_SCAN_V2")) return false;  // diagnostic switch: force the 4-wave ring
-    return v2_eligible(idx, qmode) && pick_kl(k) == v3::KL;
+    const int kl = pick_kl(idx, qmode, k);
+    return v3_capable(idx, qmode) && (kl == 10 || kl == 15);
 }
 
 WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     WsLayout w{};
-    const int KL = pick_kl(k);
+    const int KL = pick_kl(idx, qmode, k);
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
     w.use_v3 = v3_eligible(idx, qmode, k);
     w.use_v2 = !w.use_v3 && v2_eligible(idx, qmode);
@@ -1818,13 +1858,13 @@ int launch_scan2_v(const Scan2Args& b, hipStream_t s) {
     return LMI_OK;
 }
 
-template <int ABL>
+template <int KL, int ABL>
 int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
-    constexpr size_t lds = v3::lds_bytes;
+    constexpr size_t lds = v3::lds_bytes<KL>();
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<ABL>,
+        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<KL, ABL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     LMI_HIP_TRY(attr_err);
@@ -1834,34 +1874,35 @@ int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
         const int rc = timing_record(s, true, ev);
         if (rc != LMI_OK) return rc;
     }
-    hipLaunchKernelGGL((scan3_kernel<ABL>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
+    hipLaunchKernelGGL((scan3_kernel<KL, ABL>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
     LMI_LAUNCH_CHECK("scan3_kernel");
     if (timed) return timing_record(s, false, ev);
     return LMI_OK;
 }
 
+template <int KL>
 int launch_scan3(const Scan2Args& b, hipStream_t s) {
 #ifdef LMI_ABLATION
     const char* e = getenv("LMI_SCAN_ABL");
     const int abl = e ? atoi(e) : 0;
-    if (abl == 1) return launch_scan3_v<1>(b, s);
-    if (abl == 2) return launch_scan3_v<2>(b, s);
-    if (abl == 3) return launch_scan3_v<3>(b, s);
-    if (abl == 4) return launch_scan3_v<4>(b, s);
-    if (abl == 5) return launch_scan3_v<5>(b, s);
-    if (abl == 6) return launch_scan3_v<6>(b, s);
-    if (abl == 7) return launch_scan3_v<7>(b, s);
-    if (abl == 14) return launch_scan3_v<14>(b, s);
-    if (abl == 21) return launch_scan3_v<21>(b, s);
-    if (abl == 31) return launch_scan3_v<31>(b, s);
-    if (abl == 32) return launch_scan3_v<32>(b, s);
-    if (abl == 33) return launch_scan3_v<33>(b, s);
-    if (abl == 40) return launch_scan3_v<40>(b, s);
-    if (abl == 41) return launch_scan3_v<41>(b, s);
-    if (abl == 42) return launch_scan3_v<42>(b, s);
-    if (abl == 43) return launch_scan3_v<43>(b, s);
+    if (abl == 1) return launch_scan3_v<KL, 1>(b, s);
+    if (abl == 2) return launch_scan3_v<KL, 2>(b, s);
+    if (abl == 3) return launch_scan3_v<KL, 3>(b, s);
+    if (abl == 4) return launch_scan3_v<KL, 4>(b, s);
+    if (abl == 5) return launch_scan3_v<KL, 5>(b, s);
+    if (abl == 6) return launch_scan3_v<KL, 6>(b, s);
+    if (abl == 7) return launch_scan3_v<KL, 7>(b, s);
+    if (abl == 14) return launch_scan3_v<KL, 14>(b, s);
+    if (abl == 21) return launch_scan3_v<KL, 21>(b, s);
+    if (abl == 31) return launch_scan3_v<KL, 31>(b, s);
+    if (abl == 32) return launch_scan3_v<KL, 32>(b, s);
+    if (abl == 33) return launch_scan3_v<KL, 33>(b, s);
+    if (abl == 40) return launch_scan3_v<KL, 40>(b, s);
+    if (abl == 41) return launch_scan3_v<KL, 41>(b, s);
+    if (abl == 42) return launch_scan3_v<KL, 42>(b, s);
+    if (abl == 43) return launch_scan3_v<KL, 43>(b, s);
 #endif
-    return launch_scan3_v<0>(b, s);
+    return launch_scan3_v<KL, 0>(b, s);
 }
 
 template <int KL>
@@ -1960,7 +2001,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
     const int QB = w.qb;
     const int P = nq * R;
-    const int KL = pick_kl(k);
+    const int KL = pick_kl(idx, qmode, k);
 
     if (f16math) {
         hipLaunchKernelGGL(prep_kernel<true>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
@@ -2056,7 +2097,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
 #endif
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
         if (w.use_v3)
-            rc = launch_scan3(b, s);
+            rc = (KL == 10) ? launch_scan3<10>(b, s) : launch_scan3<15>(b, s);
         else
             rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
     } else if (f16math) {
@@ -2078,6 +2119,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                        out_pos, out_row, idx->n_rows, status)
     if (KL == 10) {
         if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
+    } else if (KL == 15) {
+        if (out_row) LMI_CM(15, true); else LMI_CM(15, false);
     } else {
         if (out_row) LMI_CM(16, true); else LMI_CM(16, false);
     }
