@@ -271,6 +271,11 @@ int32_t lmi_timing_read(float* ms_out, int32_t max_n);
 /* ---- misc --------------------------------------------------------------- */
 const char* lmi_last_error(void);
 int32_t lmi_abi_version(void);
+/* The LMI_* environment switches (diagnostic variants and tuning knobs; results
+ * never depend on them) are read once, at the first launch.  Diagnostics that
+ * change them inside one process call this to re-read them; not for use while
+ * another thread launches. */
+int lmi_config_reload(void);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,7 @@
 #include <string>
 
 #include "../../include/lmi_hip.h"
+#include "lmi_env.hpp"
 
 namespace lmi {
 
@@ -114,6 +115,7 @@ __device__ inline void list_clear(uint64_t (&L)[KL]) {
 }
 
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
 
 // ---- internal entry points shared between translation units -------------
 // K2 up to the merged per-pair lists (lmi_scan.hip): lmi_bucket_topk with an

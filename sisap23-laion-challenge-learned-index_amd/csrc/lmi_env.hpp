@@ -1,0 +1,26 @@
+// Environment switches of liblmi_hip.so (host code only; shared by the HIP and
+// the g++ translation units).
+#pragma once
+
+namespace lmi {
+
+// ---- environment switches (diagnostics and tuning knobs) ----------------
+// Read once, at the first use in the process (thread-safe static init), so no
+// launch path calls getenv.  Defaults are the tuned values; results never
+// depend on them.
+struct EnvConfig {
+    bool scan_v1;        // LMI_SCAN_V1: force the general scan kernel
+    bool scan_v2;        // LMI_SCAN_V2: force the 4-wave ring
+    int scan_abl;        // LMI_SCAN_ABL (diagnostic builds)
+    int scan_groups;     // LMI_SCAN_GROUPS: tile queues (power of two <= 8), 0 = default
+    int scan_order;      // LMI_SCAN_ORDER: heavy-first tile order (default 1)
+    int scan_lag;        // LMI_SCAN_LAG
+    bool scan_no_pref;   // LMI_SCAN_NO_PREF
+    bool scan_keep_thr;  // LMI_SCAN_KEEP_THR (diagnostic builds)
+    bool router_fma;     // LMI_ROUTER_FMA: FMA-chain router instead of MFMA
+    int router_qg;       // LMI_ROUTER_QG: 1/2/4 query groups per workgroup, 0 = auto
+    int replay_abl;      // LMI_REPLAY_ABL (diagnostic builds)
+};
+const EnvConfig& env_config();
+
+}  // namespace lmi

@@ -677,7 +677,7 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         a.uraw = (int32_t*)(ws + s.uraw);
         a.status = status;
 #ifdef LMI_ABLATION
-        a.abl = getenv("LMI_REPLAY_ABL") ? atoi(getenv("LMI_REPLAY_ABL")) : 0;
+        a.abl = env_config().replay_abl;
 #endif
         hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, a);
         LMI_LAUNCH_CHECK("replay_group_kernel");

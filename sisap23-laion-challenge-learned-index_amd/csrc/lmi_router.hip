@@ -18,6 +18,8 @@
 // argmax.
 #include "lmi_common.hpp"
 
+#include <mutex>
+
 namespace lmi {
 namespace {
 
@@ -471,21 +473,22 @@ __global__ __launch_bounds__(256) void router_mfma_kernel(RouterArgs a) {
     }
 }
 
-int env_int_r(const char* name, int dflt) {
-    const char* v = getenv(name);
-    if (!v) return dflt;
-    const int x = atoi(v);
+int router_qg_or(int dflt) {
+    const int x = env_config().router_qg;
     return (x == 1 || x == 2 || x == 4) ? x : dflt;
 }
 
 template <int TQ>
 int launch_router(const RouterArgs& a, size_t lds, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        LMI_HIP_TRY(hipFuncSetAttribute((const void*)router_kernel<TQ>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr_set = true;
-    }
+    // the attribute is the kernel's maximum (160 KiB), set once per process
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+        attr_err = hipFuncSetAttribute((const void*)router_kernel<TQ>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    });
+    LMI_HIP_TRY(attr_err);
+    (void)lds;
     const int grid = (a.nq + TQ - 1) / TQ;
     hipLaunchKernelGGL(router_kernel<TQ>, dim3(grid), dim3(kThreads), lds, s, a);
     LMI_LAUNCH_CHECK("router_kernel");
@@ -539,27 +542,28 @@ extern "C" int lmi_router(const float* x, int32_t nq, int32_t ldx, const lmi_mlp
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // MFMA path: hidden and input widths multiples of 16 (k quarters of
     // float4 runs), 16-B aligned weights; the classes may be any width
-    bool mfma = a.w_vec4 && !getenv("LMI_ROUTER_FMA");
+    bool mfma = a.w_vec4 && !env_config().router_fma;
     for (int l = 0; l < mlp->n_layers; ++l)
         if (mlp->dims[l] % 16) mfma = false;
     if (mfma) {
         const int sm = ((maxdim + 15) / 16) * 16 + 4;  // room for the last tile's padding rows
         // 64 queries per workgroup (every weight load feeds 4 query groups)
         // when the grid still covers the CUs; else 32 or 16
-        int nqg = env_int_r("LMI_ROUTER_QG", nq >= 64 * 128 ? 4 : nq >= 32 * 128 ? 2 : 1);
+        int nqg = router_qg_or(nq >= 64 * 128 ? 4 : nq >= 32 * 128 ? 2 : 1);
         for (; nqg >= 1; nqg >>= 1) {
             const size_t lds = (size_t)(2 * kMQ * nqg * sm + 2 * kMQ * nqg) * sizeof(float);
             if (lds > 160 * 1024) continue;
             const void* fn = nqg == 4 ? (const void*)router_mfma_kernel<4>
                            : nqg == 2 ? (const void*)router_mfma_kernel<2>
                                       : (const void*)router_mfma_kernel<1>;
-            static bool attr[3] = {false, false, false};
+            static std::once_flag once[3];
+            static hipError_t attr_err[3] = {hipSuccess, hipSuccess, hipSuccess};
             const int ai = nqg == 4 ? 2 : nqg - 1;
-            if (!attr[ai]) {
-                LMI_HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                160 * 1024));
-                attr[ai] = true;
-            }
+            std::call_once(once[ai], [&] {
+                attr_err[ai] = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   160 * 1024);
+            });
+            LMI_HIP_TRY(attr_err[ai]);
             RouterArgs m = a;
             m.stride = sm;
             const dim3 grid((nq + kMQ * nqg - 1) / (kMQ * nqg));

@@ -1706,12 +1706,12 @@ struct WsLayout {
 };
 
 bool v2_eligible(const lmi_index_desc* idx, int qmode) {
-    if (getenv("LMI_SCAN_V1")) return false;  // diagnostic switch: force the general kernel
+    if (env_config().scan_v1) return false;  // diagnostic switch: force the general kernel
     return idx->dtype == LMI_F16 && qmode == LMI_Q_F16 && idx->d_pad == v2::D;
 }
 
 bool v3_capable(const lmi_index_desc* idx, int qmode) {
-    if (getenv("LMI_SCAN_V2")) return false;  // diagnostic switch: force the 4-wave ring
+    if (env_config().scan_v2) return false;  // diagnostic switch: force the 4-wave ring
     return v2_eligible(idx, qmode);
 }
 
@@ -1883,8 +1883,7 @@ int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
 template <int KL>
 int launch_scan3(const Scan2Args& b, hipStream_t s) {
 #ifdef LMI_ABLATION
-    const char* e = getenv("LMI_SCAN_ABL");
-    const int abl = e ? atoi(e) : 0;
+    const int abl = env_config().scan_abl;
     if (abl == 1) return launch_scan3_v<KL, 1>(b, s);
     if (abl == 2) return launch_scan3_v<KL, 2>(b, s);
     if (abl == 3) return launch_scan3_v<KL, 3>(b, s);
@@ -1908,8 +1907,7 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
 template <int KL>
 int launch_scan2(const Scan2Args& b, hipStream_t s) {
 #ifdef LMI_ABLATION
-    const char* e = getenv("LMI_SCAN_ABL");
-    const int abl = e ? atoi(e) : 0;
+    const int abl = env_config().scan_abl;
     if (abl == 1) return launch_scan2_v<KL, 1>(b, s);
     if (abl == 2) return launch_scan2_v<KL, 2>(b, s);
     if (abl == 3) return launch_scan2_v<KL, 3>(b, s);
@@ -1957,11 +1955,7 @@ extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq
 
 namespace {
 // tuning knobs (defaults are the tuned values; results do not depend on them)
-int env_int(const char* name, int dflt, int lo, int hi) {
-    const char* v = getenv(name);
-    if (!v || !*v) return dflt;
-    return std::max(lo, std::min(hi, atoi(v)));
-}
+int clamp_knob(int v, int dflt, int lo, int hi) { return v == 0 && dflt != 0 ? dflt : std::max(lo, std::min(hi, v)); }
 }  // namespace
 
 extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
@@ -2022,7 +2016,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     int32_t* meta = (int32_t*)(ws + w.ntiles);
     int32_t* work = (int32_t*)(ws + w.work);
     const int C = idx->n_buckets;
-    int ng = env_int("LMI_SCAN_GROUPS", kGroups, 1, kGroups);
+    int ng = clamp_knob(env_config().scan_groups, kGroups, 1, kGroups);
     while (ng & (ng - 1)) ng &= ng - 1;
 
     // pair_bucket = -1 marks pairs whose class is out of range (never filled)
@@ -2032,8 +2026,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
                        idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
-    const bool nearest_first = w.use_v3 && idx->chunk_centroid && !getenv("LMI_SCAN_NO_PREF");
-    if (!nearest_first && env_int("LMI_SCAN_ORDER", 1, 0, 1)) {
+    const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
+    if (!nearest_first && env_config().scan_order != 0) {
         hipLaunchKernelGGL(tile_order_kernel, dim3(ng), dim3(1024), 0, s, tiles, (Tile*)(ws + w.tiles_tmp),
                            meta, idx->bucket_off, idx->chunk_rows, QB);
         LMI_LAUNCH_CHECK("tile_order_kernel");
@@ -2089,11 +2083,11 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         b.partial = a.partial;
         b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
         b.ng = ng;
-        b.lag = env_int("LMI_SCAN_LAG", 0, 0, 3);
+        b.lag = std::max(0, std::min(3, env_config().scan_lag));
 #ifdef LMI_ABLATION
         // diagnostic: keep the previous call's per-pair bounds (near-final
         // seeds when the same batch is repeated) to measure seeding quality
-        if (!getenv("LMI_SCAN_KEEP_THR"))
+        if (!env_config().scan_keep_thr)
 #endif
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
         if (w.use_v3)

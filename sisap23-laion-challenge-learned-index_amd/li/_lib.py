@@ -62,6 +62,7 @@ EXPORTS = (
     "lmi_timing_read",
     "lmi_last_error",
     "lmi_abi_version",
+    "lmi_config_reload",
 )
 
 
@@ -139,6 +140,7 @@ _SIGNATURES = {
     "lmi_timing_read": (C.c_int32, [_P, _I32]),
     "lmi_last_error": (C.c_char_p, []),
     "lmi_abi_version": (C.c_int32, []),
+    "lmi_config_reload": (C.c_int, []),
 }
 
 _lock = threading.Lock()

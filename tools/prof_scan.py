@@ -32,6 +32,7 @@ lib = _lib.load()
 ref = None
 if a.check:
     os.environ["LMI_SCAN_ABL"] = "0"
+    _lib.load().lmi_config_reload()
     ref = bucket_topk(ix, q, classes, 10)[:2]
 runs = [(abl, "") for abl in a.abl.split(",")]
 if a.variants:
@@ -41,6 +42,7 @@ for abl, var in runs:
     for kv in filter(None, var.split(",")):
         kk, vv = kv.split("=")
         os.environ[kk] = vv
+    _lib.load().lmi_config_reload()
     for _ in range(2):
         bucket_topk(ix, q, classes, 10)
     torch.cuda.synchronize()

@@ -7,6 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
 import numpy as np
 import torch
+from li import _lib  # noqa: E402
 from li.index import replay_device
 
 
@@ -38,6 +39,7 @@ args = [torch.from_numpy(x).to(dev) for x in (classes, d, pos)]
 bsz, p2id = torch.from_numpy(size).to(dev), torch.from_numpy(ids).to(dev)
 for abl in (os.environ.get("ABLS", "0").split(",")):
     os.environ["LMI_REPLAY_ABL"] = abl
+    _lib.load().lmi_config_reload()
     fn = lambda: replay_device(*args, k_round=10, k_final=10, bucket_size=bsz, pos_to_id=p2id,
                                use_threshold=True)
     for _ in range(3):
