@@ -123,42 +123,77 @@ def algorithmic_bytes(index, classes, nq):
     return byts, flops, rows
 
 
-def cpu_baseline(index, q, classes, args, budget_s=15.0):
+def cpu_baseline(index, q, classes, lists_d, args, budget_s=15.0):
     """The oracle port (oracle/lmi_oracle.py) on a bounded sample of the same
     batch, shaped like the reference's own loop (LearnedIndex.py:143-172):
-    whole (round, bucket) groups, each one sklearn-normalize + fp32 GEMM of the
-    group's queries against the whole bucket (utils.py:10-11) and a full-row
-    argsort.  Groups are taken in batch order until `budget_s` is spent; the
-    rate is (query, probe) pairs / R per second, i.e. queries/s."""
+    whole (round, bucket) groups drawn at random (seeded) from ALL R rounds,
+    each: the gather of the bucket's rows (pandas .loc, :152-153/:168), then
+    round 0: pairwise_cosine (sklearn normalize + GEMM, utils.py:10-11);
+    rounds >= 1: pairwise_cosine_threshold (utils.py:14-43, its Python list
+    comprehension over the relevant pairs included) against the running k-th
+    distance of the earlier rounds (taken from the GPU's own lists); then the
+    full-row argsort (:170).  Groups are timed until `budget_s` is spent; the
+    rate is (query, probe) pairs / R per second, i.e. queries/s.  The
+    reference itself, timed in the build container (tools/ref_cpu_baseline.py),
+    is reported beside it from profiles/ref_cpu_*.json."""
+    import glob
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import lmi_oracle as O
     off = index.layout.bucket_off
     qh = q.cpu().numpy()
-    R = args.R
+    xh = index.corpus[:, : index.d].cpu().numpy()  # the corpus on the host (untimed)
+    R, k = args.R, args.k
+    ld = lists_d.cpu().numpy().astype(np.float64)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
     groups = [(r, int(c)) for r in range(R) for c in np.unique(classes[:, r])]
+    rng = np.random.default_rng(0)
+    groups = [groups[i] for i in rng.permutation(len(groups))]
     pairs = rows = ngroups = 0
+    per_round = [0] * R
     el = 0.0
     for r, c in groups:
         a, b = int(off[c]), int(off[c + 1])
         G = np.nonzero(classes[:, r] == c)[0]
         if a == b or G.size == 0:
             continue
-        y = index.corpus[a:b, : index.d].float().cpu().numpy()  # bucket rows (HBM -> host, untimed)
+        thr = None
+        if r > 0:  # running k-th distance after rounds < r (LearnedIndex.py:71-72)
+            thr = np.full(qh.shape[0], np.inf)
+            thr[G] = np.sort(ld[G, :r, :].reshape(G.size, -1), axis=1)[:, k - 1]
         t1 = time.time()
-        D = O.pairwise_cosine(qh[G], y)
-        np.argsort(D, axis=1, kind="quicksort")[:, : args.k]
+        y = xh[a:b].astype(np.float32)                      # the bucket gather
+        if r == 0:
+            D = O.pairwise_cosine(qh[G], y)
+        else:
+            D = O.pairwise_cosine_threshold(qh[G], y, thr, G, k)[0]
+        if D is not None:
+            np.argsort(D, axis=1, kind="quicksort")[:, :k]
         el += time.time() - t1
         ngroups += 1
+        per_round[r] += 1
         pairs += G.size
         rows += b - a
         if el > budget_s:
             break
-    return {"value": round(pairs / R / el, 3), "unit": "queries/s", "cores": threads, "kind": "port",
-            "sample": f"{ngroups} of the {len(groups)} (round, bucket) groups of the same {args.scale} "
-                      f"batch ({pairs} (query, probe) pairs over {rows} bucket rows, R={R}, k={args.k}): "
-                      f"per group sklearn-normalize + fp32 GEMM + full-row argsort as "
-                      f"LearnedIndex.py:143-172; rate = pairs / R / s; {threads} BLAS threads"}
+    out = {"value": round(pairs / R / el, 3), "unit": "queries/s", "cores": threads, "kind": "port",
+           "sample": f"{ngroups} of the {len(groups)} (round, bucket) groups of the same {args.scale} "
+                     f"batch, drawn at random from all rounds (per round {per_round}); "
+                     f"{pairs} (query, probe) pairs over {rows} bucket rows, R={R}, k={k}: per group "
+                     f"the bucket gather, sklearn-normalize + fp32 GEMM (round 0) or the threshold "
+                     f"variant (rounds >= 1), full-row argsort, as LearnedIndex.py:143-172; "
+                     f"rate = pairs / R / s; {threads} BLAS threads"}
+    refs = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "ref_cpu_*.json"))):
+        d = json.load(open(f))
+        refs[os.path.basename(f)[:-5]] = {kk: d[kk] for kk in ("size", "R", "dtype", "threads", "qps",
+                                                              "search_s", "nproc")}
+    if refs:
+        out["reference"] = {"kind": "reference", "unit": "queries/s",
+                            "what": "the reference's own LearnedIndex.search timed as search.py:116-141 "
+                                    "on the bench's synthetic workload in the build container "
+                                    "(tools/ref_cpu_baseline.py; it cannot run on the GPU box)",
+                            "runs": refs}
+    return out
 
 
 def pmc_traffic(kernel_ms):
@@ -254,6 +289,11 @@ def main():
                          "more (a shard's tiles must still fill 256 CUs; tools/gpu_shards.sh)")
     ap.add_argument("--recall-sample", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist", default="f32", choices=["f32", "f64"],
+                    help="distance arithmetic of the headline line: f32 = the reference's on "
+                         "float32 DataFrames (the synthetic corpus is float32 holding fp16-exact "
+                         "values); f64 = its arithmetic on float16 data (sklearn promotes). The "
+                         "other one is timed too and reported under 'other_dist'")
     args = ap.parse_args()
 
     rank, world, local = init_from_env()
@@ -268,40 +308,51 @@ def main():
     x, q, qn, router, index, labels = build_workload(args, device, rank, world)
     searcher = Searcher(index, router, group)
 
-    def step():
-        return searcher.search(qn, q, args.R, k=args.k, use_threshold=True)
-
-    for _ in range(args.warmup):
-        dists, anns = step()
     lib = _lib.load()
-    lib.lmi_timing_read(None, 0)  # drop warmup records
-    lib.lmi_timing_enable(1)
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dists, anns = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    el = time.perf_counter() - t0
-    lib.lmi_timing_enable(0)
-    ms = (_lib.C.c_float * max(args.steps, 1))()
-    n_ev = lib.lmi_timing_read(ms, args.steps)
-    scan_ms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64,
-                         device=device if torch.distributed.get_backend() == "nccl" else "cpu")
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
+
+    def timed(dist):
+        """W untimed warmup steps, then K steps bracketed by barrier +
+        synchronize; returns (max-over-ranks seconds, mean scan-kernel ms,
+        the last step's output)."""
+        out = None
+        for _ in range(args.warmup):
+            out = searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
+        lib.lmi_timing_read(None, 0)  # drop warmup records
+        lib.lmi_timing_enable(1)
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        lib.lmi_timing_enable(0)
+        ms = (_lib.C.c_float * max(args.steps, 1))()
+        n_ev = lib.lmi_timing_read(ms, args.steps)
+        kms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64,
+                             device=device if torch.distributed.get_backend() == "nccl" else "cpu")
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        return el, kms, out
+
+    el, scan_ms, (dists, anns) = timed(args.dist)
     ms_step = el / args.steps * 1e3
     value = args.nq / (el / args.steps)
+    # the other arithmetic, timed the same way (float64: the reference's on
+    # float16 data, e.g. the real clip768 'emb'; float32: on float32 data)
+    other = "f64" if args.dist == "f32" else "f32"
+    el_o, scan_ms_o, (dists_o, anns_o) = timed(other)
 
     # per-stage breakdown (separate, synchronised passes; not the timed loop)
     tm = {}
+    searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=args.dist)  # pinned buffers
     for _ in range(3):
-        searcher.search(qn, q, args.R, k=args.k, use_threshold=True, timings=tm)
+        searcher.search(qn, q, args.R, k=args.k, use_threshold=True, timings=tm, dist=args.dist)
     breakdown = {kk: round(v / 3, 3) for kk, v in tm.items()}
     # the optional exact-top-k semantics over the same probed buckets (untimed;
     # every rank takes part: with G > 1 the search has collectives)
@@ -314,16 +365,26 @@ def main():
             torch.distributed.barrier()
         return
     achieved = byts / (scan_ms * 1e-3) / 1e9
+    tflops = flops / (scan_ms * 1e-3) / 1e12
     # the committed PMC passes profile the default (10M, 1 GPU) command only
     traffic, traffic_src = pmc_traffic(scan_ms) if (args.scale == "10M" and world == 1) else (None, None)
-    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
+    # the bound is the roof the kernel's arithmetic intensity puts it under:
+    # flops / algorithmic bytes above the dense-fp16 ridge (2.5 PF / 8 TB/s =
+    # 312 flop/B) means MFMA-bound (401 flop/B at configs[2])
+    ai = flops / byts
+    mfma_bound = ai > F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
+    roof = {"bound": "mfma" if mfma_bound else "hbm",
+            "achieved": round(tflops if mfma_bound else achieved, 1),
+            "peak": F16_PEAK_TFLOPS if mfma_bound else HBM_PEAK_GBS,
+            "unit": "TFLOP/s" if mfma_bound else "GB/s",
+            "frac": round(tflops / F16_PEAK_TFLOPS if mfma_bound else achieved / HBM_PEAK_GBS, 4),
             "traffic": None if traffic is None else int(traffic),
             "traffic_source": traffic_src,
             "kernel": "scan3_kernel (lmi_bucket_topk)", "kernel_ms": round(scan_ms, 4),
+            "arithmetic_intensity_flop_per_byte": round(ai, 1),
             "algorithmic_bytes": int(byts), "flops": flops,
-            "mfma_tflops": round(flops / (scan_ms * 1e-3) / 1e12, 1),
-            "mfma_frac": round(flops / (scan_ms * 1e-3) / 1e12 / F16_PEAK_TFLOPS, 4)}
+            "hbm_gbs": round(achieved, 1), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+            "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / F16_PEAK_TFLOPS, 4)}
     sample = min(args.recall_sample, args.nq)
     truth = exact_knn(x, q[:sample], args.k)
     recall = float(np.mean([len(set(anns[i][: args.k]) & set(truth[i])) / args.k
@@ -332,13 +393,14 @@ def main():
                               for i in range(sample)]))
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(index, q, classes, args)
+        _, lists_d, _, _ = searcher.lists(qn, q, args.R, args.k, dist=args.dist)
+        cpu = cpu_baseline(index, q, classes, lists_d, args)
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "queries/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
         "higher_is_better": True, "scaling": "strong",
         "vs_baseline": round(value / PUBLISHED_QPS_10M, 1) if args.scale == "10M" else None,
-        "dtype": "f16", "data": "synthetic",
+        "dtype": "f16" if args.dist == "f32" else "f16+f64", "data": "synthetic",
         "config": {"workload": f"{args.scale} {'random unit (configs[4])' if args.scale == '100M' else 'clip768-like'} synthetic (fp16-exact), {args.n_buckets} "
                                f"buckets, R={args.R}, k={args.k}, {args.nq} queries, router "
                                f"{args.arch}", "n": SCALES[args.scale], "d": 768, "nq": args.nq,
@@ -348,6 +410,12 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
         "recall_sample": sample, "breakdown_ms": breakdown,
+        "dist": args.dist,
+        "other_dist": {"dist": other, "value": round(args.nq / (el_o / args.steps), 1),
+                       "ms_per_step": round(el_o / args.steps * 1e3, 3),
+                       "scan_kernel_ms": round(scan_ms_o, 4),
+                       "recall": round(float(np.mean([len(set(anns_o[i][: args.k]) & set(truth[i])) /
+                                                      args.k for i in range(sample)])), 4)},
     }
     os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
