@@ -56,7 +56,9 @@ extern "C" {
 #define LMI_Q_F32 1 /* general queries: exact-fp32 MFMA path (16x the MFMA time)   */
 
 #define LMI_MAX_LAYERS 8
-#define LMI_MAX_K 16 /* largest k the bucket scan keeps per list in this build */
+#define LMI_MAX_K 16          /* largest k of one scan pass (and of K3 / the float32 ABI 1 lists) */
+#define LMI_MAX_K_PASSES 1024 /* lmi_bucket_topk: k > LMI_MAX_K runs ceil(k/15) lower-bound passes */
+#define LMI_MAX_K_F64 240     /* lmi_bucket_topk_f64: k + 5 guard entries in <= 256-entry lists */
 
 /* ---- router ----------------------------------------------------------- */
 /* A torch nn.Sequential of nn.Linear layers with ReLU between consecutive
@@ -133,7 +135,10 @@ size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R
  *   out_d    device [nq][R][k] f32 ascending, +inf past the bucket's size
  *   out_pos  device [nq][R][k] int32 global row positions, -1 past the end
  *   status   device int32, OR-ed with LMI_STATUS_* bits (caller zeroes it)
- * 1 <= k <= LMI_MAX_K. */
+ * 1 <= k <= LMI_MAX_K_PASSES.  k > LMI_MAX_K (the reference takes any k on its
+ * R == 1 path, search.py:134-140 -> LearnedIndex.py:103-111, and in
+ * Baseline.py:14-19) runs ceil(k/15) scan passes, each keeping the next 15
+ * entries of the (distance, position) order after the previous pass's last. */
 int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                     const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
                     float* out_d, int32_t* out_pos, int32_t* status,
@@ -151,7 +156,7 @@ int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t 
  * sklearn promotes to float64 (utils.py:11, :19; check_pairwise_arrays) and
  * the threshold test (utils.py:23) and the merges (LearnedIndex.py:86-97) see
  * float64 values.  lmi_bucket_topk_f64 returns those float64 lists:
- *   - the fp32 scan keeps the top-KL (KL = 15 for k <= 10, else 16) per (query, probe);
+ *   - the fp32 scan keeps the top-KL (KL >= k + 5: 15 for k <= 10) per (query, probe);
  *   - every list entry within 2*eps of the fp32 k-th distance is recomputed
  *     in float64 from the stored row (sklearn normalize + dot; exact fp16
  *     inputs), sorted by (d64, position); with fewer than KL entries in that
@@ -161,7 +166,8 @@ int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t 
  *     whole bucket shard (exact, rare: ties or near-ties of > KL-k objects).
  * Same arguments and layout as lmi_bucket_topk; out_d is float64 [nq][R][k]
  * (+inf past the bucket's size), out_pos global positions (-1 past it).
- * 1 <= k <= LMI_MAX_K, d <= 1024. */
+ * 1 <= k <= LMI_MAX_K_F64, d <= 1024; k > 10 lists come from lower-bound
+ * passes (as lmi_bucket_topk's) of at least k + 5 entries. */
 #define LMI_REFINE_EPS 1.52587890625e-05 /* 2^-16 */
 size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                     int32_t k, int32_t qmode);

@@ -120,11 +120,24 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // ---- internal entry points shared between translation units -------------
 // K2 up to the merged per-pair lists (lmi_scan.hip): lmi_bucket_topk with an
 // optional third output, the shard-local row of every entry (-1 = empty).
+// lo_g (nullable, device [nq*R]): keep only objects after the (distance,
+// global position) key of their pair (the passes of k > 16); ldo: entries per
+// pair in the outputs (default k); prefill: write (+inf, -1) over all R*ldo
+// entries first (the first pass).
 int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                      const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                      int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
-                     size_t ws_bytes, hipStream_t s);
+                     size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g = nullptr,
+                     int32_t ldo = 0, bool prefill = true);
 size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
-                            int32_t qmode);
+                            int32_t qmode, bool lo = false);
+// k > LMI_MAX_K: passes_of() passes of kp-entry lists; bucket_topk_passes fills
+// [nq*R][ldo] lists (ldo >= passes * kp) with (d32, global position[, local row]).
+int passes_of(const lmi_index_desc* idx, int qmode, int k, int* kp_out);
+size_t passes_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k, int qmode);
+int bucket_topk_passes(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                       const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
+                       int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
+                       void* workspace, size_t ws_bytes, hipStream_t s);
 
 }  // namespace lmi

@@ -32,7 +32,6 @@
 namespace lmi {
 namespace {
 
-constexpr int kKLMax = 16;     // longest scan list refined (LMI_MAX_K)
 constexpr int kRefT = 256;     // refine: 4 waves, one pair each
 constexpr int kFbT = 1024;     // fallback: 16 waves on one pair
 constexpr int kFbRows = 4;     // rows per wave in flight (fallback)
@@ -141,6 +140,16 @@ __device__ inline bool lt_dp(double a, int32_t pa, double b, int32_t pb) {
     return a < b || (a == b && pa < pb);
 }
 
+constexpr int kSlots = 4;  // list entries per lane: lists of <= 256 entries
+
+// the slot-`s` value of lane `l` of a wave-uniform (s, l)
+template <typename T>
+__device__ inline T shfl_slot(const T (&v)[kSlots], int j) {
+    const int s = j >> 6, l = j & 63;
+    const T x = s == 0 ? v[0] : s == 1 ? v[1] : s == 2 ? v[2] : v[3];
+    return __shfl(x, l);
+}
+
 template <typename TC>
 __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
     const int lane = threadIdx.x & 63;
@@ -149,49 +158,72 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
     if (p >= P) return;
     const int kl = a.kl, k = a.k;
     const size_t li = (size_t)p * kl;
-    // lane j < kl holds list entry j
-    const bool has = lane < kl;
-    const float dj = has ? a.ld[li + lane] : __builtin_inff();
-    const int32_t rj = has ? a.lrow[li + lane] : -1;
-    const int32_t gj = has ? a.lpos[li + lane] : -1;
-    const uint64_t valid = __ballot(rj >= 0);
-    const int n_valid = __popcll(valid);
+    // lane l, slot s holds list entry 64 s + l
+    float dj[kSlots];
+    int32_t rj[kSlots], gj[kSlots];
+    int n_valid = 0;
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        const int e = 64 * s + lane;
+        const bool has = e < kl;
+        dj[s] = has ? a.ld[li + e] : __builtin_inff();
+        rj[s] = has ? a.lrow[li + e] : -1;
+        gj[s] = has ? a.lpos[li + e] : -1;
+        n_valid += __popcll(__ballot(rj[s] >= 0));
+    }
     double* od = a.out_d + (size_t)p * k;
     int32_t* op = a.out_pos + (size_t)p * k;
     int m;
     if (n_valid < kl) {
         m = n_valid;  // the shard's whole bucket is listed
     } else {
-        const float dk = __shfl(dj, k - 1);
-        const double t = (double)dk + 2.0 * a.eps;
-        m = __popcll(__ballot(has && (double)dj <= t));
+        const double t = (double)a.ld[li + k - 1] + 2.0 * a.eps;
+        m = 0;
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+            m += __popcll(__ballot(64 * s + lane < kl && (double)dj[s] <= t));
         if (m >= kl) {  // the band may continue past the list: exact fallback
             if (lane == 0) a.failed[atomicAdd(a.n_failed, 1)] = (int32_t)p;
             return;
         }
     }
-    if (has && rj >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s)
+        if (rj[s] >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);
     const int nps = (a.d + 255) / 256;
     double qh[kMaxPieces][4];
     query_hat(a.q + (size_t)(p / a.R) * a.ldq, a.d, nps, qh);
-    double mine = __builtin_inf();
+    double mine[kSlots];
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) mine[s] = __builtin_inf();
     for (int j = 0; j < m; ++j) {
-        const int32_t r = __shfl(rj, j);
+        const int32_t r = shfl_slot(rj, j);
         if (r < 0 || r >= a.n_rows) continue;
         const TC* row = reinterpret_cast<const TC*>(a.corpus) + (size_t)r * a.d_pad;
         const double dv = row_dist64<TC>(row, a.d, nps, qh);
-        if (lane == j) mine = dv;
+        if (lane == (j & 63)) {
+            const int s = j >> 6;
+            mine[0] = s == 0 ? dv : mine[0];
+            mine[1] = s == 1 ? dv : mine[1];
+            mine[2] = s == 2 ? dv : mine[2];
+            mine[3] = s == 3 ? dv : mine[3];
+        }
     }
-    // rank of entry `lane` among the m refined entries by (d64, position)
-    int rank = 0;
+    // rank of every refined entry among the m by (d64, position)
+    int rank[kSlots] = {};
     for (int i = 0; i < m; ++i) {
-        const double di = __shfl(mine, i);
-        const int32_t gi = __shfl(gj, i);
-        rank += (i != lane && lt_dp(di, gi, mine, gj)) ? 1 : 0;
+        const double di = shfl_slot(mine, i);
+        const int32_t gi = shfl_slot(gj, i);
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+            rank[s] += (64 * s + lane != i && lt_dp(di, gi, mine[s], gj[s])) ? 1 : 0;
     }
-    if (lane < m && rank < k) {
-        od[rank] = mine;
-        op[rank] = gj;
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) {
+        if (64 * s + lane < m && rank[s] < k) {
+            od[rank[s]] = mine[s];
+            op[rank[s]] = gj[s];
+        }
     }
     for (int j = m + lane; j < k; j += 64) {
         od[j] = __builtin_inf();
@@ -200,12 +232,13 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
 }
 
 // One workgroup per queued pair: float64 distance of every row of its bucket
-// shard (a wave per row, kFbRows rows in flight), per-lane-0 top-k lists
-// merged through LDS.
+// shard (a wave per row, kFbRows rows in flight); lane 0 of every wave keeps
+// the wave's top-k in LDS, thread 0 merges the waves' lists.
+constexpr int kFbK = 256;
 template <typename TC>
 __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
-    __shared__ double sd[kFbT / 64][kKLMax];
-    __shared__ int32_t sp[kFbT / 64][kKLMax];
+    __shared__ double sd[kFbT / 64][kFbK];
+    __shared__ int32_t sp[kFbT / 64][kFbK];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nf = *a.n_failed;
     const int k = a.k;
@@ -216,13 +249,13 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
         const int64_t b0 = a.bucket_off[c], b1 = a.bucket_off[c + 1];
         double qh[kMaxPieces][4];
         query_hat(a.q + (size_t)(p / a.R) * a.ldq, a.d, nps, qh);
-        double L[kKLMax];
-        int32_t G[kKLMax];
-#pragma unroll
-        for (int i = 0; i < kKLMax; ++i) {
-            L[i] = __builtin_inf();
-            G[i] = INT32_MAX;
-        }
+        double* L = sd[w];
+        int32_t* G = sp[w];
+        if (lane == 0)
+            for (int i = 0; i < k; ++i) {
+                L[i] = __builtin_inf();
+                G[i] = INT32_MAX;
+            }
         for (int64_t r0 = b0 + (int64_t)w * kFbRows; r0 < b1; r0 += (int64_t)(kFbT / 64) * kFbRows) {
             double dv[kFbRows];
 #pragma unroll
@@ -252,11 +285,6 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
                 }
             }
         }
-        if (lane == 0)
-            for (int i = 0; i < k; ++i) {
-                sd[w][i] = L[i];
-                sp[w][i] = G[i];
-            }
         __syncthreads();
         if (threadIdx.x == 0) {
             int head[kFbT / 64] = {};
@@ -284,13 +312,20 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
 
 struct RefineWs {
     size_t scan, ld, lrow, lpos, failed, nfailed, total;
+    int kl;       // scan list length refined (>= k + 5, or 15 for k <= 10)
+    int passes;   // 0: one scan of kl entries, else lower-bound passes
 };
-
-int pick_kl_f64(int k) { return k <= 10 ? 15 : LMI_MAX_K; }
 
 RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     RefineWs w{};
-    const int kl = pick_kl_f64(k);
+    if (k + 5 <= 15) {
+        w.kl = 15;
+        w.passes = 0;
+    } else {
+        int kp;
+        w.passes = passes_of(idx, qmode, k + 5, &kp);
+        w.kl = w.passes * kp;
+    }
     const size_t P = (size_t)nq * R;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -298,12 +333,13 @@ RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
         off = align_up(off + bytes, 256);
         return at;
     };
-    w.ld = take(P * kl * 4);
-    w.lrow = take(P * kl * 4);
-    w.lpos = take(P * kl * 4);
+    w.ld = take(P * w.kl * 4);
+    w.lrow = take(P * w.kl * 4);
+    w.lpos = take(P * w.kl * 4);
     w.failed = take(P * 4);
     w.nfailed = take(256);
-    w.scan = take(scan_workspace_bytes(idx, nq, R, kl, qmode));
+    w.scan = take(w.passes ? passes_ws_bytes(idx, nq, R, k + 5, qmode)
+                           : scan_workspace_bytes(idx, nq, R, w.kl, qmode));
     w.total = off;
     return w;
 }
@@ -323,7 +359,7 @@ int num_cus_ref() {
 
 extern "C" size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                                int32_t k, int32_t qmode) {
-    if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K) return 0;
+    if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_F64) return 0;
     return lmi::refine_ws(idx, nq, R, k, qmode).total;
 }
 
@@ -334,7 +370,7 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
                                    void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(idx != nullptr, "null index");
-    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_F64, "k=%d outside [1, %d]", k, LMI_MAX_K_F64);
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
     LMI_CHECK_ARG(idx->d >= 1 && idx->d <= 4 * 256, "d=%d outside [1, 1024] for float64 refinement",
                   idx->d);
@@ -348,7 +384,7 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
     }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     auto* ws = reinterpret_cast<unsigned char*>(workspace);
-    const int kl = pick_kl_f64(k);
+    const int kl = w.kl;
     RefineArgs a{};
     a.corpus = idx->corpus;
     a.dtype = idx->dtype;
@@ -374,9 +410,13 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
     a.n_failed = (int32_t*)(ws + w.nfailed);
     a.status = status;
     LMI_HIP_TRY(hipMemsetAsync(ws + w.nfailed, 0, 4, s));
-    int rc = bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
-                              (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
-                              ws + w.scan, w.total - w.scan, s);
+    int rc = w.passes
+        ? bucket_topk_passes(idx, q, nq, ldq, classes, R, k + 5, qmode, (float*)(ws + w.ld),
+                             (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), kl, status,
+                             ws + w.scan, w.total - w.scan, s)
+        : bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
+                           (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
+                           ws + w.scan, w.total - w.scan, s);
     if (rc != LMI_OK) return rc;
     const int64_t P = (int64_t)nq * R;
     const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));

@@ -74,6 +74,8 @@ struct ScanArgs {
     const int32_t* meta;    // tile groups (plan_fill_kernel)
     int32_t* work;          // dequeue counters
     uint64_t* partial;      // [P][max_chunks][KL]
+    const int32_t* gpos;    // [n_rows] global positions (LO: ties at the lower bound)
+    const unsigned long long* lo_g;  // [nq*R] LO: keep only keys above (d, gpos) of the pair
 };
 
 // ---------------------------------------------------------------------------
@@ -535,11 +537,21 @@ size_t scan_lds_bytes(int d_pad) {
 // The epilogue of one 32x32 accumulator tile: lane holds query column
 // (lane & 31) and rows (reg&3) + 8*(reg>>2) + 4*(lane>>5), reg = 0..15
 // (C/D layout of the 32x32 MFMAs, dtype-independent on gfx950).
-template <int KL>
+// Lower-bound test of the k > 16 passes (lmi_bucket_topk with k > 16): keep
+// only objects after (distance, global position) `lo` of their pair, i.e. the
+// next entries of the (d, position) order; lo = 0 keeps everything.
+__device__ inline bool above_lo(float d, uint64_t lo, const int32_t* __restrict__ gpos,
+                                uint32_t row) {
+    const uint32_t o = f2ord(d), hi = (uint32_t)(lo >> 32);
+    return o > hi || (o == hi && (uint32_t)gpos[row] > (uint32_t)lo);
+}
+
+template <int KL, bool LO = false>
 __device__ inline void tile_epilogue(const f32x16& acc, uint64_t (&L)[KL], uint64_t* thr_slot,
                                      float invq, const float* __restrict__ inv_norm,
                                      uint32_t row_base, int valid_rows, uint64_t* queue,
-                                     int lane) {
+                                     int lane, uint64_t lo = 0,
+                                     const int32_t* __restrict__ gpos = nullptr) {
     const int h = lane >> 5;
     uint64_t thr = *thr_slot;
     float bound = key_dist_bound(thr);
@@ -550,7 +562,7 @@ __device__ inline void tile_epilogue(const f32x16& acc, uint64_t (&L)[KL], uint6
         const bool valid = i < valid_rows;
         const float inv = valid ? inv_norm[row_base + i] : 0.0f;
         const float d = fmaf(-acc[reg], invq * inv, 1.0f);
-        if (valid && d <= bound) {
+        if (valid && d <= bound && (!LO || above_lo(d, lo, gpos, row_base + (uint32_t)i))) {
             const uint64_t key = make_key(d, row_base + (uint32_t)i);
             if (key < thr) {
                 queue[cnt * 64] = key;
@@ -570,7 +582,7 @@ __device__ inline void tile_epilogue(const f32x16& acc, uint64_t (&L)[KL], uint6
                                    (unsigned long long)L[KL - 1]);
 }
 
-template <int KL, bool F16MATH, typename TC>
+template <int KL, bool F16MATH, typename TC, bool LO = false>
 __global__ __launch_bounds__(kThreads, 1) void scan_kernel(ScanArgs a) {
     using Cfg = ScanCfg<KL, F16MATH>;
     using QT = typename Cfg::QT;
@@ -634,8 +646,13 @@ __global__ __launch_bounds__(kThreads, 1) void scan_kernel(ScanArgs a) {
         __syncthreads();
 
         uint64_t L[NQF][KL];
+        uint64_t lo[NQF];
 #pragma unroll
-        for (int f = 0; f < NQF; ++f) list_clear<KL>(L[f]);
+        for (int f = 0; f < NQF; ++f) {
+            list_clear<KL>(L[f]);
+            const int r = 32 * f + col;
+            lo[f] = (LO && r < tile.np) ? (uint64_t)a.lo_g[a.pair_q[tile.pp0 + r]] : 0ull;
+        }
 
         const int nsub = (nrows + 31) / 32;
         for (int st = wave; st < nsub; st += kWaves) {
@@ -723,8 +740,8 @@ __global__ __launch_bounds__(kThreads, 1) void scan_kernel(ScanArgs a) {
 #pragma unroll
             for (int f = 0; f < NQF; ++f) {
                 const int qslot = 32 * f + col;
-                tile_epilogue<KL>(acc[f], L[f], &thr_s[qslot], invq_s[qslot], a.inv_norm, row_base,
-                                  valid_rows, queue, lane);
+                tile_epilogue<KL, LO>(acc[f], L[f], &thr_s[qslot], invq_s[qslot], a.inv_norm,
+                                      row_base, valid_rows, queue, lane, lo[f], a.gpos);
             }
         }
         __syncthreads();  // all waves done with Qs -> reuse as merge buffer
@@ -811,6 +828,8 @@ struct Scan2Args {
     unsigned long long* thr_g;  // [P] per-pair bound, EMPTY at start
     int32_t ng;                 // tile groups (power of two <= kGroups)
     int32_t lag;                // extra ring stages waited for (tuning knob, 0)
+    const int32_t* gpos;        // LO: global positions of the rows
+    const unsigned long long* lo_g;  // LO: [nq*R] lower-bound key (d, gpos) per pair id
 };
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
@@ -1324,7 +1343,7 @@ __device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
     return x;
 }
 
-template <int KL, int ABL = 0>
+template <int KL, int ABL = 0, bool LO = false>
 __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
     // diagnostic builds only (results wrong for ABL != 0): 1 no insertion,
@@ -1407,9 +1426,15 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         half8 qf[NQF];
         uint64_t thr = 0ull;
         float my_invq = 0.0f;
+        uint64_t lo = 0ull;  // LO: this pair's lower-bound key
+        float lo_d = -__builtin_inff();
         int cnt = 0;  // entries in this lane's list; < KL: an unsorted append buffer
         if (wave_live) {
             const int q = live ? a.pair_q[pp] / a.R : 0;
+            if (LO && live) {
+                lo = a.lo_g[a.pair_q[pp]];
+                if ((uint32_t)(lo >> 32) != 0u) lo_d = ord2f((uint32_t)(lo >> 32));
+            }
             const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
 #pragma unroll
             for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
@@ -1515,7 +1540,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 for (int e = 0; e < 4; ++e) {
                     const int reg = 4 * g + e;
                     const float d = fmaf(-acc[reg], my_invq * n4[e], 1.0f);
-                    mask |= (e + 8 * g < vr && d <= bound) ? (1u << reg) : 0u;
+                    mask |= (e + 8 * g < vr && d <= bound && (!LO || d >= lo_d)) ? (1u << reg) : 0u;
                 }
             }
 #ifdef LMI_ABLATION
@@ -1548,7 +1573,9 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                         const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
                         const float d = fmaf(-dot, my_invq * n1, 1.0f);
                         const uint64_t key = make_key(d, rb + (uint32_t)i);
-                        if (cnt < KL) {
+                        if (LO && !above_lo(d, lo, a.gpos, rb + (uint32_t)i)) {
+                            // at or before the pair's lower bound: not this pass's
+                        } else if (cnt < KL) {
                             // append mode: the first KL candidates are stored
                             // unsorted (a few instructions); a full buffer is
                             // sorted once and the lane switches to list mode
@@ -1631,7 +1658,7 @@ template <int KL, bool ROWS>
 __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
-    const int32_t* __restrict__ gpos, int32_t P, int32_t k, float* __restrict__ out_d,
+    const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, int64_t n_rows,
     int32_t* __restrict__ status) {
     // one thread per pair, 64-thread blocks (spread over every CU); each
@@ -1680,7 +1707,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
             }
         }
     }
-    const size_t o = (size_t)pair_q[pp] * k;
+    const size_t o = (size_t)pair_q[pp] * ldo;
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
         if (i < k) {
@@ -1691,6 +1718,37 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
             if constexpr (ROWS) out_row[o + i] = empty ? -1 : W[i];
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// k > 16: lower-bound passes
+// ---------------------------------------------------------------------------
+// After pass j (entries [j*kp, (j+1)*kp) of every pair's list): the next
+// pass's lower bound is the (distance, global position) key of the pass's last
+// entry; a pair whose pass came back short is exhausted (a key above every
+// real key: nothing passes).
+__global__ __launch_bounds__(256) void next_lo_kernel(const float* __restrict__ d,
+                                                      const int32_t* __restrict__ pos, int32_t P,
+                                                      int32_t ldo, int32_t last,
+                                                      unsigned long long* __restrict__ lo) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const size_t o = (size_t)p * ldo + last;
+    const int32_t g = pos[o];
+    lo[p] = g < 0 ? ~0ull : (((unsigned long long)f2ord(d[o]) << 32) | (uint32_t)g);
+}
+
+// first k of every pair's pass list -> the caller's [P][k] outputs
+__global__ __launch_bounds__(256) void take_k_kernel(const float* __restrict__ d,
+                                                     const int32_t* __restrict__ pos, int64_t P,
+                                                     int32_t ldo, int32_t k, float* __restrict__ out_d,
+                                                     int32_t* __restrict__ out_pos) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= P * k) return;
+    const int64_t p = t / k;
+    const int j = (int)(t - p * k);
+    out_d[t] = d[(size_t)p * ldo + j];
+    out_pos[t] = pos[(size_t)p * ldo + j];
 }
 
 // ---------------------------------------------------------------------------
@@ -1728,12 +1786,13 @@ bool v3_eligible(const lmi_index_desc* idx, int qmode, int k) {
     return v3_capable(idx, qmode) && (kl == 10 || kl == 15);
 }
 
-WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
+WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, bool lo = false) {
     WsLayout w{};
     const int KL = pick_kl(idx, qmode, k);
     const bool f16math = (idx->dtype == LMI_F16) && (qmode == LMI_Q_F16);
     w.use_v3 = v3_eligible(idx, qmode, k);
-    w.use_v2 = !w.use_v3 && v2_eligible(idx, qmode);
+    // the lower-bound passes (k > 16) run on v3 or the general kernel
+    w.use_v2 = !w.use_v3 && !lo && v2_eligible(idx, qmode);
     const int QB = w.use_v3 ? v3::QB : w.use_v2 ? v2::QB : (f16math ? 64 : 32);
     w.qb = QB;
     const size_t P = (size_t)nq * R;
@@ -1809,7 +1868,7 @@ int timing_record(hipStream_t s, bool start, std::pair<hipEvent_t, hipEvent_t>& 
     return LMI_OK;
 }
 
-template <int KL, bool F16MATH, typename TC>
+template <int KL, bool F16MATH, typename TC, bool LO = false>
 int launch_scan(const ScanArgs& a, int d_pad, hipStream_t s) {
     const size_t lds = scan_lds_bytes<KL, F16MATH>(d_pad);
     if (lds > 160 * 1024) {
@@ -1819,7 +1878,7 @@ int launch_scan(const ScanArgs& a, int d_pad, hipStream_t s) {
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute((const void*)scan_kernel<KL, F16MATH, TC>,
+        attr_err = hipFuncSetAttribute((const void*)scan_kernel<KL, F16MATH, TC, LO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     });
     LMI_HIP_TRY(attr_err);
@@ -1829,7 +1888,7 @@ int launch_scan(const ScanArgs& a, int d_pad, hipStream_t s) {
         const int rc = timing_record(s, true, ev);
         if (rc != LMI_OK) return rc;
     }
-    hipLaunchKernelGGL((scan_kernel<KL, F16MATH, TC>), dim3(num_cus()), dim3(kThreads), lds, s, a);
+    hipLaunchKernelGGL((scan_kernel<KL, F16MATH, TC, LO>), dim3(num_cus()), dim3(kThreads), lds, s, a);
     LMI_LAUNCH_CHECK("scan_kernel");
     if (timed) return timing_record(s, false, ev);
     return LMI_OK;
@@ -1858,13 +1917,13 @@ int launch_scan2_v(const Scan2Args& b, hipStream_t s) {
     return LMI_OK;
 }
 
-template <int KL, int ABL>
+template <int KL, int ABL, bool LO = false>
 int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
     constexpr size_t lds = v3::lds_bytes<KL>();
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<KL, ABL>,
+        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<KL, ABL, LO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     LMI_HIP_TRY(attr_err);
@@ -1874,7 +1933,7 @@ int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
         const int rc = timing_record(s, true, ev);
         if (rc != LMI_OK) return rc;
     }
-    hipLaunchKernelGGL((scan3_kernel<KL, ABL>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
+    hipLaunchKernelGGL((scan3_kernel<KL, ABL, LO>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
     LMI_LAUNCH_CHECK("scan3_kernel");
     if (timed) return timing_record(s, false, ev);
     return LMI_OK;
@@ -1943,14 +2002,19 @@ extern "C" int32_t lmi_plan_chunks(const int64_t* bucket_off_host, int32_t n_buc
 }
 
 size_t lmi::scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
-                                 int32_t qmode) {
+                                 int32_t qmode, bool lo) {
     if (!idx || nq < 0 || R < 1 || k < 1) return 0;
-    return lmi::ws_layout(idx, nq, R, k, qmode).total;
+    return lmi::ws_layout(idx, nq, R, k, qmode, lo).total;
 }
 
 extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                            int32_t k, int32_t qmode) {
-    return lmi::scan_workspace_bytes(idx, nq, R, k, qmode);
+    using namespace lmi;
+    if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_PASSES) return 0;
+    if (k <= LMI_MAX_K) return scan_workspace_bytes(idx, nq, R, k, qmode);
+    int kp;
+    const int ldo = passes_of(idx, qmode, k, &kp) * kp;
+    return 2 * align_up((size_t)nq * R * ldo * 4, 256) + passes_ws_bytes(idx, nq, R, k, qmode);
 }
 
 namespace {
@@ -1962,15 +2026,43 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
                                const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
                                float* out_d, int32_t* out_pos, int32_t* status, void* workspace,
                                size_t ws_bytes, void* stream) {
-    return lmi::bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
-                                 status, workspace, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+    using namespace lmi;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (k <= LMI_MAX_K)
+        return bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
+                                status, workspace, ws_bytes, s);
+    LMI_CHECK_ARG(idx != nullptr, "null index");
+    LMI_CHECK_ARG(k <= LMI_MAX_K_PASSES, "k=%d outside [1, %d]", k, LMI_MAX_K_PASSES);
+    LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
+    if (nq == 0) return LMI_OK;
+    LMI_CHECK_ARG(out_d && out_pos && workspace, "null pointer");
+    int kp;
+    const int ldo = passes_of(idx, qmode, k, &kp) * kp;
+    const size_t P = (size_t)nq * R;
+    const size_t lists = align_up(P * ldo * 4, 256);
+    if (ws_bytes < 2 * lists) {
+        set_error("workspace %zu B < required %zu B", ws_bytes, 2 * lists);
+        return LMI_E_WORKSPACE;
+    }
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    float* ld = reinterpret_cast<float*>(ws);
+    int32_t* lp = reinterpret_cast<int32_t*>(ws + lists);
+    const int rc = bucket_topk_passes(idx, q, nq, ldq, classes, R, k, qmode, ld, lp, nullptr, ldo,
+                                      status, ws + 2 * lists, ws_bytes - 2 * lists, s);
+    if (rc != LMI_OK) return rc;
+    hipLaunchKernelGGL(take_k_kernel, dim3((unsigned)((P * k + 255) / 256)), dim3(256), 0, s, ld, lp,
+                       (int64_t)P, ldo, k, out_d, out_pos);
+    LMI_LAUNCH_CHECK("take_k_kernel");
+    return LMI_OK;
 }
 
 int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                           const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                           int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
-                          size_t ws_bytes, hipStream_t s) {
+                          size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g, int32_t ldo,
+                          bool prefill) {
     using namespace lmi;
+    if (ldo <= 0) ldo = k;
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(idx->dtype == LMI_F16 || idx->dtype == LMI_F32, "bad corpus dtype");
     LMI_CHECK_ARG(idx->d >= 1 && idx->d_pad >= idx->d && idx->d_pad % 32 == 0, "bad d/d_pad");
@@ -1986,7 +2078,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     LMI_CHECK_ARG(idx->n_rows == 0 || (idx->corpus && idx->inv_norm && idx->gpos), "null corpus arrays");
     LMI_CHECK_ARG(idx->bucket_off && idx->chunk_first, "null bucket tables");
 
-    const WsLayout w = ws_layout(idx, nq, R, k, qmode);
+    const bool LOP = lo_g != nullptr;
+    const WsLayout w = ws_layout(idx, nq, R, k, qmode, LOP);
     if (ws_bytes < w.total) {
         set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
         return LMI_E_WORKSPACE;
@@ -2000,11 +2093,11 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     if (f16math) {
         hipLaunchKernelGGL(prep_kernel<true>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
                            idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
-                           out_pos, out_row, R * k);
+                           out_pos, out_row, prefill ? R * ldo : 0);
     } else {
         hipLaunchKernelGGL(prep_kernel<false>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
                            idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
-                           out_pos, out_row, R * k);
+                           out_pos, out_row, prefill ? R * ldo : 0);
     }
     LMI_LAUNCH_CHECK("prep_kernel");
     if (idx->n_rows == 0) return LMI_OK;
@@ -2064,6 +2157,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     a.meta = meta;
     a.work = work;
     a.partial = (uint64_t*)(ws + w.partial);
+    a.gpos = idx->gpos;
+    a.lo_g = lo_g;
 
     int rc;
     if (w.use_v2 || w.use_v3) {
@@ -2082,6 +2177,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         b.work = work;
         b.partial = a.partial;
         b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
+        b.gpos = idx->gpos;
+        b.lo_g = lo_g;
         b.ng = ng;
         b.lag = std::max(0, std::min(3, env_config().scan_lag));
 #ifdef LMI_ABLATION
@@ -2090,10 +2187,21 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         if (!env_config().scan_keep_thr)
 #endif
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
-        if (w.use_v3)
+        if (w.use_v3 && LOP)
+            rc = (KL == 10) ? launch_scan3_v<10, 0, true>(b, s) : launch_scan3_v<15, 0, true>(b, s);
+        else if (w.use_v3)
             rc = (KL == 10) ? launch_scan3<10>(b, s) : launch_scan3<15>(b, s);
         else
             rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
+    } else if (LOP) {
+        // lower-bound passes off v3: the general kernel, 16-entry lists
+        if (KL != 16) {
+            set_error("lower-bound scan passes need 16-entry lists off scan v3");
+            return LMI_E_UNSUPPORTED;
+        }
+        rc = f16math ? launch_scan<16, true, _Float16, true>(a, idx->d_pad, s)
+           : (idx->dtype == LMI_F16) ? launch_scan<16, false, _Float16, true>(a, idx->d_pad, s)
+                                     : launch_scan<16, false, float, true>(a, idx->d_pad, s);
     } else if (f16math) {
         rc = (KL == 10) ? launch_scan<10, true, _Float16>(a, idx->d_pad, s)
                         : launch_scan<16, true, _Float16>(a, idx->d_pad, s);
@@ -2109,8 +2217,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const int grid = (P + 63) / 64;
 #define LMI_CM(KLV, ROWSV)                                                                         \
     hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
-                       a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, out_d, \
-                       out_pos, out_row, idx->n_rows, status)
+                       a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo,  \
+                       out_d, out_pos, out_row, idx->n_rows, status)
     if (KL == 10) {
         if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
     } else if (KL == 15) {
@@ -2122,6 +2230,57 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     LMI_LAUNCH_CHECK("chunk_merge_kernel");
     return LMI_OK;
 }
+
+namespace lmi {
+// k > 16: ceil(k / kp) scan passes of kp-entry lists (kp = 15 on scan v3, else
+// 16), each keeping the next kp entries of the (distance, position) order
+// after the previous pass's last key.  Lists of ldo = passes * kp entries.
+int passes_of(const lmi_index_desc* idx, int qmode, int k, int* kp_out) {
+    const int kp = pick_kl(idx, qmode, 15) == 15 ? 15 : 16;
+    if (kp_out) *kp_out = kp;
+    return (k + kp - 1) / kp;
+}
+
+size_t passes_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
+    int kp;
+    const int np = passes_of(idx, qmode, k, &kp);
+    const size_t P = (size_t)nq * R;
+    return align_up(P * 8, 256) + scan_workspace_bytes(idx, nq, R, kp, qmode, true);
+}
+
+int bucket_topk_passes(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                       const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
+                       int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
+                       void* workspace, size_t ws_bytes, hipStream_t s) {
+    int kp;
+    const int np = passes_of(idx, qmode, k, &kp);
+    if (ldo < np * kp) {
+        set_error("pass lists of %d entries < %d passes x %d", ldo, np, kp);
+        return LMI_E_INVALID;
+    }
+    const size_t P = (size_t)nq * R;
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    auto* lo = reinterpret_cast<unsigned long long*>(ws);
+    const size_t lo_bytes = align_up(P * 8, 256);
+    if (ws_bytes < lo_bytes) {
+        set_error("workspace %zu B too small", ws_bytes);
+        return LMI_E_WORKSPACE;
+    }
+    LMI_HIP_TRY(hipMemsetAsync(lo, 0, P * 8, s));
+    for (int j = 0; j < np; ++j) {
+        const int rc = bucket_topk_impl(idx, q, nq, ldq, classes, R, kp, qmode, out_d + (size_t)j * kp,
+                                        out_pos + (size_t)j * kp, out_row ? out_row + (size_t)j * kp : nullptr,
+                                        status, ws + lo_bytes, ws_bytes - lo_bytes, s, lo, ldo, j == 0);
+        if (rc != LMI_OK) return rc;
+        if (j + 1 < np) {
+            hipLaunchKernelGGL(next_lo_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, out_d,
+                               out_pos, (int32_t)P, ldo, (j + 1) * kp - 1, lo);
+            LMI_LAUNCH_CHECK("next_lo_kernel");
+        }
+    }
+    return LMI_OK;
+}
+}  // namespace lmi
 
 #ifdef LMI_ABLATION
 // diagnostic builds: read and clear the scan's counters (lmi_dbg above)

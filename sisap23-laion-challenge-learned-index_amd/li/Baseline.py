@@ -5,7 +5,8 @@ top-k by (distance, row) is what `pairwise_cosine(data, queries).T.argsort()`
 and `np.sort` give on tie-free inputs (Baseline.py:17-19).  As in the
 reference, the distances are float32 when data and queries are both float32
 and float64 otherwise (sklearn's dtype rule, utils.py:11); the float64 case
-runs lmi_bucket_topk_f64.  k <= LMI_MAX_K.
+runs lmi_bucket_topk_f64.  k <= LMI_MAX_K_PASSES (float32) / LMI_MAX_K_F64 (float64); k > 16 runs the
+scan's lower-bound passes.
 """
 import time
 

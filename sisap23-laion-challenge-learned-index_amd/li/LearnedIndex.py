@@ -142,7 +142,7 @@ class LearnedIndex(Logger):
         """One bucket per query (LearnedIndex.py:103-195).  `pred_categories`
         is the per-query bucket; object labels come from
         data_navigation['category'] as in the reference's groupby (:143)."""
-        from .index import Searcher, replay_device
+        from .index import Searcher, replay, replay_device
         index = self._device_index(data_navigation, data_search,
                                    np.asarray(data_navigation['category']))
         dev = index.device
@@ -153,6 +153,11 @@ class LearnedIndex(Logger):
                                                     dist=dist_dtype(data_search, queries_search))
         if int(st.item()) & _lib.LMI_STATUS_INTERNAL:
             raise RuntimeError(f"search_single: scan status {int(st.item())}")
+        if k > _lib.LMI_REPLAY_DEVICE_MAX_KR:
+            # rows wider than the device replay holds: the host replay (C++)
+            return replay(cls, d.cpu().numpy(), pos.cpu().numpy(), k_round=k, k_final=k,
+                          bucket_size=index.bucket_size, pos_to_id=index.pos_to_id,
+                          use_threshold=False, thr_round0=threshold_dist)
         thr = None if threshold_dist is None else torch.from_numpy(
             np.ascontiguousarray(np.asarray(threshold_dist, dtype=np.float64).ravel())).to(dev)
         dd, aa, rst = replay_device(

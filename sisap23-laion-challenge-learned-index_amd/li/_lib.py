@@ -36,6 +36,10 @@ LMI_Q_F16 = 0
 LMI_Q_F32 = 1
 LMI_MAX_LAYERS = 8
 LMI_MAX_K = 16
+LMI_MAX_K_PASSES = 1024
+LMI_MAX_K_F64 = 240
+LMI_REPLAY_DEVICE_MAX_KR = 32
+LMI_REPLAY_DEVICE_MAX_K = 64
 LMI_KMEANS_MAX_D = 128
 LMI_REFINE_EPS = 2.0 ** -16
 
