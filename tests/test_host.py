@@ -33,9 +33,11 @@ def test_invalid_arguments_fail_loudly_without_a_device():
     d = _lib.IndexDesc()
     rc = lib.lmi_bucket_topk(C.byref(d), None, 4, 768, None, 2, 10, 0, None, None, None, None, 0, None)
     assert rc == _lib.LMI_E_INVALID
-    rc = lib.lmi_bucket_topk_f64(C.byref(d), None, 4, 768, None, 2, 17, 0, _lib.LMI_REFINE_EPS, None,
+    rc = lib.lmi_bucket_topk_f64(C.byref(d), None, 4, 768, None, 2, 241, 0, _lib.LMI_REFINE_EPS, None,
                                  None, None, None, 0, None)
-    assert rc == _lib.LMI_E_INVALID and b"k=17" in lib.lmi_last_error()
+    assert rc == _lib.LMI_E_INVALID and b"k=241" in lib.lmi_last_error()
+    rc = lib.lmi_bucket_topk(C.byref(d), None, 4, 768, None, 2, 1025, 0, None, None, None, None, 0, None)
+    assert rc == _lib.LMI_E_INVALID and b"k=1025" in lib.lmi_last_error()
     d.d = 2048
     rc = lib.lmi_bucket_topk_f64(C.byref(d), None, 4, 768, None, 2, 10, 0, _lib.LMI_REFINE_EPS, None,
                                  None, None, None, 0, None)
