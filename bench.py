@@ -289,6 +289,9 @@ def main():
                          "more (a shard's tiles must still fill 256 CUs; tools/gpu_shards.sh)")
     ap.add_argument("--recall-sample", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time the eager step (every launch from the host) instead of the "
+                         "HIP-graph replay of the captured step")
     ap.add_argument("--dist", default="f32", choices=["f32", "f64"],
                     help="distance arithmetic of the headline line: f32 = the reference's on "
                          "float32 DataFrames (the synthetic corpus is float32 holding fp16-exact "
@@ -310,10 +313,52 @@ def main():
 
     lib = _lib.load()
 
+    use_graph = not args.no_graph and (world == 1 or torch.distributed.get_backend() == "nccl")
+
+    def timed_graph(dist):
+        """The step captured once as a HIP graph (Searcher.graph) and replayed:
+        W untimed replays, then K replays bracketed by barrier + synchronize.
+        Events recorded into a graph cannot be timed on ROCm, so the scan
+        kernel's duration comes from HIP events around the same launches in K
+        eager steps right after (outside the timed region; a kernel runs the
+        same whichever way it is launched)."""
+        gs = searcher.graph(qn, q, args.R, k=args.k, dist=dist)
+        out = None
+        for _ in range(args.warmup):
+            out = gs.run()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = gs.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        out = (out[0].copy(), out[1].copy())
+        del gs
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        lib.lmi_timing_read(None, 0)
+        lib.lmi_timing_enable(1)
+        for _ in range(args.steps):
+            searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
+        torch.cuda.synchronize()
+        lib.lmi_timing_enable(0)
+        ms = (_lib.C.c_float * max(args.steps, 1))()
+        n_ev = lib.lmi_timing_read(ms, args.steps)
+        kms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
+        return el, kms, out
+
     def timed(dist):
         """W untimed warmup steps, then K steps bracketed by barrier +
         synchronize; returns (max-over-ranks seconds, mean scan-kernel ms,
         the last step's output)."""
+        if use_graph:
+            return timed_graph(dist)
         out = None
         for _ in range(args.warmup):
             out = searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
@@ -410,7 +455,7 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
         "recall_sample": sample, "breakdown_ms": breakdown,
-        "dist": args.dist,
+        "dist": args.dist, "step": "hip-graph replay" if use_graph else "eager launches",
         "other_dist": {"dist": other, "value": round(args.nq / (el_o / args.steps), 1),
                        "ms_per_step": round(el_o / args.steps * 1e3, 3),
                        "scan_kernel_ms": round(scan_ms_o, 4),

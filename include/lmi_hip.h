@@ -270,7 +270,7 @@ int lmi_kmeans_update(const float* x, int64_t n, int32_t d, const int32_t* label
  * its scan kernel (the roofline kernel).  lmi_timing_read waits for the pairs
  * recorded so far, writes up to max_n durations (ms) and clears the record;
  * it returns the number written or a negative LMI_E_* code.  Not for use
- * under graph capture. */
+ * under graph capture (events recorded into a hipGraph cannot be timed). */
 int lmi_timing_enable(int32_t on);
 int32_t lmi_timing_read(float* ms_out, int32_t max_n);
 

@@ -605,6 +605,11 @@ class Searcher:
             self._dev_tables = t
         return t
 
+    def graph(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "GraphedSearch":
+        """The step captured as a HIP graph (GraphedSearch): same results as
+        search(..., semantics="reference", replay_on="device")."""
+        return GraphedSearch(self, q_nav, q_search, R, k, **kw)
+
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
                use_threshold: bool = True, classes: Optional[torch.Tensor] = None,
                timings: Optional[dict] = None, replay_on: str = "device",
@@ -759,3 +764,80 @@ class Searcher:
                      use_threshold=use_threshold)
         lap("replay", t0) if sync else None
         return out
+
+
+class GraphedSearch:
+    """One search step (router + scan [+ all-gather + K3] + device replay +
+    the D2H of the answer and of the status words) captured once as a HIP
+    graph and replayed per batch: the ~25 launches of the step go to the GPU
+    as one graph launch, with no host work between them (the host gap between
+    steps in the kernel trace).
+
+    The graph reads the query tensors it was captured with: to search another
+    batch of the same shape, copy it into `q_nav` / `q_search` first.  The
+    query precision class (fp16-exact or not, Searcher.qmode) is fixed at
+    capture; a batch that is not fp16-exact under an fp16 capture is detected
+    by the scan's status word and answered by the eager path instead.
+    `run()` returns numpy views of the graph's pinned output buffers, valid
+    until the next run (copy them to keep them)."""
+
+    def __init__(self, searcher: "Searcher", q_nav: torch.Tensor, q_search: torch.Tensor, R: int,
+                 k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32"):
+        s = searcher
+        dev = s.index.device
+        self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
+        self.use_threshold, self.dist = use_threshold, dist
+        self.q_nav = _as_torch(q_nav, dev, torch.float32)
+        self.q_search = _as_torch(q_search, dev, torch.float32)
+        if k_round > _lib.LMI_MAX_K or (s.index.world > 1 and
+                                       torch.distributed.get_backend(s.group) != "nccl"):
+            raise ValueError("graph capture needs k_round <= 16 and RCCL collectives")
+        self.qmode = s.qmode(self.q_search)
+        f64 = dist == "f64"
+        bsz, p2id = s._device_tables()
+
+        def step():
+            classes = s.route(self.q_nav, R)
+            d, pos, status = s._scan(self.q_search, classes, k_round, self.qmode, f64)
+            rd, ra, rst = replay_device(classes, d, pos, k_round=k_round, k_final=k,
+                                        bucket_size=bsz, pos_to_id=p2id,
+                                        use_threshold=use_threshold)
+            return rd, ra, status, rst
+
+        # warm up on a side stream (allocations, kernel attributes, RCCL
+        # communicators), then capture
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                rd, ra, st, rst = step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize(dev)
+        self.h_d = torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True)
+        self.h_a = torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True)
+        self.h_st = torch.zeros((2,), dtype=torch.int32, pin_memory=True)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            rd, ra, st, rst = step()
+            self.h_d.copy_(rd, non_blocking=True)
+            self.h_a.copy_(ra, non_blocking=True)
+            self.h_st[0:1].copy_(st, non_blocking=True)
+            self.h_st[1:2].copy_(rst, non_blocking=True)
+        self._keep = (rd, ra, st, rst)
+        torch.cuda.synchronize(dev)
+
+    def run(self):
+        """Replay the step -> (dists f64 [nq, w], anns uint32 [nq, w])."""
+        dev = self.searcher.index.device
+        self.graph.replay()
+        torch.cuda.current_stream(dev).synchronize()
+        st, rst = int(self.h_st[0]), int(self.h_st[1])
+        if st & _lib.LMI_STATUS_INTERNAL or rst:
+            raise RuntimeError(f"search: internal status {st}/{rst}")
+        if st & _lib.LMI_STATUS_QUERY_NOT_F16:
+            # captured for fp16-exact queries; this batch is not: the eager path
+            self.searcher._qcheck = None
+            return self.searcher.search(self.q_nav, self.q_search, self.R, k=self.k,
+                                        k_round=self.k_round, use_threshold=self.use_threshold,
+                                        dist=self.dist)
+        return self.h_d.numpy(), self.h_a.numpy().view(np.uint32)

@@ -41,7 +41,15 @@ for W in map(int, a.worlds.split(",")):
     for _ in range(5):
         s.search(qn, q, 4, k=10, timings=tm)
     br = {k: round(v / 5, 3) for k, v in tm.items()}
-    print(f"world {W} chunk {ck}: step {el:.3f} ms -> {10000 / el * 1e3 * 1:.0f} q/s per rank-step; "
-          f"breakdown {br}", flush=True)
+    g = s.graph(qn, q, 4, k=10)
+    for _ in range(3):
+        g.run()
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g.run()
+    torch.cuda.synchronize(); elg = (time.perf_counter() - t0) / a.steps * 1e3
+    del g
+    print(f"world {W} chunk {ck}: step {el:.3f} ms eager, {elg:.3f} ms graph -> "
+          f"{10000 / min(el, elg) * 1e3:.0f} q/s per rank-step; breakdown {br}", flush=True)
     del ix, s; torch.cuda.empty_cache()
 dist.destroy_process_group()
