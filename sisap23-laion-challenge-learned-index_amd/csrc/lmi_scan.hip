@@ -1463,6 +1463,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         auto dma_stage = [&](int so, int b, int j) {
             if (kNoDma) return;
             unsigned char* sl = ring + so;
+            const int nb_area = b % 3;  // norms of block b: slot (b % 3)'s norm area
             if (kL2Src) b &= 3;
             __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
                                                      b * (32 * D * 2) + j * ROWB, 0, kAux);
@@ -1472,8 +1473,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                                                      vo_row, b * (32 * D * 2) + j * ROWB + 2 * D * 2,
                                                      0, kAux);
             if (j == NST - 1 && lane < 4)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(sl + NORM_OFF + 16 * wave), 4,
-                                                         (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(ring + nb_area * STAGE + NORM_OFF + 16 * wave),
+                                                         4, (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
         };
         // block b lives in slots NST*(b&1) .. +NST-1; block 0 is the prologue,
         // block b+1's DMA rides in block b
@@ -1483,54 +1484,18 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         const uint32_t lane_off = (uint32_t)(((lane >> 1) & 15) * PIECEP + (lane & 1) * 16 + (lane >> 5) * 32);
 
         f32x16 acc;
-        for (int blk = 0; blk < nblk; ++blk) {
-            const bool more = blk + 1 < nblk;
-            const int rs0 = (blk & 1) * NST * STAGE;        // this block's slots
-            const int ws0 = ((blk + 1) & 1) * NST * STAGE;  // the next block's (= block blk-1's)
-            // one barrier per block: this wave's DMA of block blk has landed
-            // (nothing newer is in flight yet) and, past the barrier, every
-            // wave's has, and every wave is done with block blk-1's slots
-            if (ABL != 14) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-            if (!kNoBar) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            // every kXch blocks: publish this lane's bound to the pair's global
-            // bound and take the global one back (tiles of the same pair on
-            // other chunks run concurrently); the returning atomic is consumed
-            // in this block's epilogue, behind its MFMAs
-            uint64_t xg = kEmptyKey;
-            if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live)
-                xg = atomicMin(&a.thr_g[pp], (unsigned long long)thr);
-#pragma unroll
-            for (int j = 0; j < NST; ++j) {
-                if (kDmaOnly || !wave_live) {
-                    if (more) dma_stage(ws0 + j * STAGE, blk + 1, j);
-                    continue;
-                }
-                const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
-#define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
-                half8 af[16];
-#pragma unroll
-                for (int tt = 0; tt < 3; ++tt) af[tt] = LMI_A3(tt);
-#pragma unroll
-                for (int tt = 0; tt < 16; ++tt) {
-                    if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
-                    acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
-                                              : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
-                    if (tt == (late ? kDmaLate : kDmaTT) && more)
-                        dma_stage(ws0 + j * STAGE, blk + 1, j);
-                    // keep the A-fragment reads 3 MFMAs ahead, no further
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-#undef LMI_A3
-            }
-            const int nso = rs0 + (NST - 1) * STAGE;  // slot holding this block's norms
-            if (kNoEpi || !wave_live) continue;
-            // ---- epilogue of this block ----------------------------------------
+        uint64_t xg_carry = kEmptyKey;  // global bounds fetched, not yet applied
+        // ---- epilogue of block eb (accumulators of its 48 MFMAs in acc) ------
+        auto epilogue = [&](int eb) {
             acc = mfma_drain_v(acc);
             const int ln = opaque(lane);
             const int hh = ln >> 5;
-            const unsigned char* nb = ring + nso + NORM_OFF + hh * 16;
-            const int vr = nrows - blk * 32 - 4 * hh;  // valid rows past this lane's offset
-            thr = std::min(thr, xg);
+            // block eb's norms: the norm area of slot eb % 3 (three blocks in
+            // flight: the late waves read block b's during block b + 1)
+            const unsigned char* nb = ring + (eb % 3) * STAGE + NORM_OFF + hh * 16;
+            const int vr = nrows - eb * 32 - 4 * hh;  // valid rows past this lane's offset
+            thr = std::min(thr, xg_carry);
+            xg_carry = kEmptyKey;
             const float bound = key_dist_bound(thr);
             uint32_t mask = 0;
 #pragma unroll
@@ -1555,7 +1520,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
 #endif
             if (!kNoIns && __any(mask != 0)) {
                 const uint32_t la = opaque_u(lbase);
-                const uint32_t rb = (uint32_t)(row0u + blk * 32 + 4 * hh);
+                const uint32_t rb = (uint32_t)(row0u + eb * 32 + 4 * hh);
                 // every lane walks its own candidates, lowest register first:
                 // iterations = the largest per-lane count (usually 1-2), the
                 // accumulator picked by a select tree.  Candidates: d <= the
@@ -1610,7 +1575,57 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 // every bound is an upper bound of the pair's k-th key: share it
                 thr = std::min(thr, partner_u64(thr, hh));
             }
+        };
+        // The two waves of a SIMD are staggered (MI355X_MICROARCH "two waves
+        // per SIMD", item 9): the early wave (slots 0-3) runs block b's MFMAs
+        // and then its epilogue; the late wave (slots 4-7) runs block b-1's
+        // epilogue first (its accumulators carried across the barrier) and
+        // then block b's MFMAs, so one wave's filter / insertion VALU runs
+        // beside the other's matrix work instead of both idling the pipe.
+        const bool defer = late && !kNoEpi && wave_live;
+        for (int blk = 0; blk < nblk; ++blk) {
+            const bool more = blk + 1 < nblk;
+            const int rs0 = (blk & 1) * NST * STAGE;        // this block's slots
+            const int ws0 = ((blk + 1) & 1) * NST * STAGE;  // the next block's (= block blk-1's)
+            // one barrier per block: this wave's DMA of block blk has landed
+            // (nothing newer is in flight yet) and, past the barrier, every
+            // wave's has, and every wave is done with block blk-1's slots
+            if (ABL != 14) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+            if (!kNoBar) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (defer && blk > 0) epilogue(blk - 1);
+            // every kXch blocks: publish this lane's bound to the pair's global
+            // bound and take the global one back (tiles of the same pair on
+            // other chunks run concurrently); the returning atomic is consumed
+            // in the next epilogue, behind this block's MFMAs
+            if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live)
+                xg_carry = std::min<uint64_t>(xg_carry, atomicMin(&a.thr_g[pp], (unsigned long long)thr));
+#pragma unroll
+            for (int j = 0; j < NST; ++j) {
+                if (kDmaOnly || !wave_live) {
+                    if (more) dma_stage(ws0 + j * STAGE, blk + 1, j);
+                    continue;
+                }
+                const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
+#define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
+                half8 af[16];
+#pragma unroll
+                for (int tt = 0; tt < 3; ++tt) af[tt] = LMI_A3(tt);
+#pragma unroll
+                for (int tt = 0; tt < 16; ++tt) {
+                    if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
+                    acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
+                                              : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
+                    if (tt == (late ? kDmaLate : kDmaTT) && more)
+                        dma_stage(ws0 + j * STAGE, blk + 1, j);
+                    // keep the A-fragment reads 3 MFMAs ahead, no further
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#undef LMI_A3
+            }
+            if (kNoEpi || !wave_live || defer) continue;
+            epilogue(blk);
         }
+        if (defer && nblk > 0) epilogue(nblk - 1);
         // lanes still in append mode hold an unsorted (EMPTY-padded) buffer
         if (__any(cnt < KL)) {
             if (cnt < KL) {
