@@ -1361,8 +1361,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     constexpr bool kNoBar = ABL == 6 || ABL == 21;
     // bound exchange period in blocks (diagnostic: 40 none, 41 every 4, 42 every 8, 43 every 16)
     constexpr int kXch = ABL == 40 ? 0 : ABL == 41 ? 4 : ABL == 42 ? 8 : ABL == 43 ? 16 : 32;
-    // An LDS-DMA issue holds its wave for ~45-60 cycles: the two waves of a
-    // SIMD issue theirs at different MFMAs (slots 0-3 early, 4-7 late)
+    // (ABL 53, round 1's placement: an LDS-DMA issue holds its wave for ~45-60
+    // cycles, so the two waves of a SIMD issued theirs at different MFMAs)
     constexpr int kDmaTT = 2, kDmaLate = 10;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
@@ -1396,6 +1396,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     }
     const int gx = xcc & (ng - 1);
     const bool late = slot >= NW / 2;
+    int partner = wave;  // the other wave of this SIMD
+    for (int w = 0; w < NW; ++w)
+        if (w != wave && wtab[w] == simd) partner = w;
+    partner = __builtin_amdgcn_readfirstlane(partner);
 #ifdef LMI_ABLATION
     const uint64_t clk0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -1459,23 +1463,25 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         // `so`: pieces 0, 1 = rows 4w+2i, 4w+2i+1 (lane l: row 4w + 2i + (l&1),
         // chunk l >> 1; piece 1 is piece 0 + 2 rows through soffset); in the
         // block's last phase the wave's 4 norms too.
-        const uint32_t vo_row = (uint32_t)((4 * wave + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
-        auto dma_stage = [&](int so, int b, int j) {
+        // the pieces of wave w (its 4 rows of the block and their norms)
+        auto dma_stage_w = [&](int so, int b, int j, int w) {
             if (kNoDma) return;
             unsigned char* sl = ring + so;
             const int nb_area = b % 3;  // norms of block b: slot (b % 3)'s norm area
             if (kL2Src) b &= 3;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave) * PIECEP), 16, vo_row,
+            const uint32_t vo_row = (uint32_t)((4 * w + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * w) * PIECEP), 16, vo_row,
                                                      b * (32 * D * 2) + j * ROWB, 0, kAux);
             // (+2 rows through soffset: an instruction offset would move the
             // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * wave + 1) * PIECEP), 16,
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * w + 1) * PIECEP), 16,
                                                      vo_row, b * (32 * D * 2) + j * ROWB + 2 * D * 2,
                                                      0, kAux);
             if (j == NST - 1 && lane < 4)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(ring + nb_area * STAGE + NORM_OFF + 16 * wave),
-                                                         4, (uint32_t)((4 * wave + lane) * 4), b * 128, 0, 0);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(ring + nb_area * STAGE + NORM_OFF + 16 * w),
+                                                         4, (uint32_t)((4 * w + lane) * 4), b * 128, 0, 0);
         };
+        auto dma_stage = [&](int so, int b, int j) { dma_stage_w(so, b, j, wave); };
         // block b lives in slots NST*(b&1) .. +NST-1; block 0 is the prologue,
         // block b+1's DMA rides in block b
 #pragma unroll
@@ -1592,7 +1598,25 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             // wave's has, and every wave is done with block blk-1's slots
             if (ABL != 14) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
             if (!kNoBar) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // Block blk+1's DMA (its slots are block blk-1's, free past the
+            // barrier): the early wave issues its pieces of all three stages
+            // right here, ahead of its MFMAs; the late wave right after its
+            // deferred epilogue.  A whole block of MFMAs then covers the
+            // fetch (7.45 vs 8.29 ms at 10M against issuing each stage's
+            // pieces inside that stage's MFMA stream, tools/prof_scan.py).
+            // Diagnostic placements: 53 = inside the MFMA stream (round 1),
+            // 50 = every wave at the head, 52 = the early wave issues its
+            // partner's pieces too.
+            constexpr bool kDmaStream = ABL == 53;
+            constexpr bool kDmaHead = !kDmaStream;
+            if (kDmaHead && more && !(ABL != 50 && late))
+                for (int j = 0; j < NST; ++j) {
+                    dma_stage(ws0 + j * STAGE, blk + 1, j);
+                    if (ABL == 52 && partner != wave) dma_stage_w(ws0 + j * STAGE, blk + 1, j, partner);
+                }
             if (defer && blk > 0) epilogue(blk - 1);
+            if (kDmaHead && ABL != 50 && ABL != 52 && more && late)
+                for (int j = 0; j < NST; ++j) dma_stage(ws0 + j * STAGE, blk + 1, j);
             // every kXch blocks: publish this lane's bound to the pair's global
             // bound and take the global one back (tiles of the same pair on
             // other chunks run concurrently); the returning atomic is consumed
@@ -1602,7 +1626,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
                 if (kDmaOnly || !wave_live) {
-                    if (more) dma_stage(ws0 + j * STAGE, blk + 1, j);
+                    if (more && !kDmaHead) dma_stage(ws0 + j * STAGE, blk + 1, j);
                     continue;
                 }
                 const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
@@ -1615,7 +1639,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                     if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
                     acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
                                               : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
-                    if (tt == (late ? kDmaLate : kDmaTT) && more)
+                    if (!kDmaHead && tt == (late ? kDmaLate : kDmaTT) && more)
                         dma_stage(ws0 + j * STAGE, blk + 1, j);
                     // keep the A-fragment reads 3 MFMAs ahead, no further
                     __builtin_amdgcn_sched_barrier(0);
@@ -1974,6 +1998,10 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 41) return launch_scan3_v<KL, 41>(b, s);
     if (abl == 42) return launch_scan3_v<KL, 42>(b, s);
     if (abl == 43) return launch_scan3_v<KL, 43>(b, s);
+    if (abl == 50) return launch_scan3_v<KL, 50>(b, s);
+    if (abl == 51) return launch_scan3_v<KL, 51>(b, s);
+    if (abl == 52) return launch_scan3_v<KL, 52>(b, s);
+    if (abl == 53) return launch_scan3_v<KL, 53>(b, s);
 #endif
     return launch_scan3_v<KL, 0>(b, s);
 }
