@@ -19,15 +19,21 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pmc $c rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 python3 - <<'PY'
-import csv, glob, json
-out = {}
+# per kernel template (the f32 bench launches scan3_kernel<10,...>, its f64
+# block scan3_kernel<15,...>); the top-level FETCH_SIZE / WRITE_SIZE are the
+# f32 step's kernel (what bench.py's roofline.traffic reads)
+import collections, csv, glob, json
+out = {"by_kernel": {}}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    vals = []
+    agg = collections.defaultdict(list)
     for f in glob.glob(f"gpurun_out/prof/pmc_{c}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == c:
-                vals.append(float(r["Counter_Value"]))
-    out[c] = {"launches": len(vals), "mean_kb": sum(vals) / max(len(vals), 1)}
+                agg[r["Kernel_Name"].split("(lmi::")[0].replace("void ", "")].append(float(r["Counter_Value"]))
+    for k, v in agg.items():
+        out["by_kernel"].setdefault(k, {})[c] = {"launches": len(v), "mean_kb": sum(v) / len(v)}
+        if "<10," in k:
+            out[c] = {"launches": len(v), "mean_kb": sum(v) / len(v), "kernel": k}
 print(json.dumps(out))
-json.dump(out, open("gpurun_out/prof/pmc_traffic.json", "w"))
+json.dump(out, open("gpurun_out/prof/pmc_traffic.json", "w"), indent=1)
 PY
