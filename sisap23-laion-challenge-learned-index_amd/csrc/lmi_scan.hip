@@ -1187,8 +1187,14 @@ constexpr int QB = NW * 32;
 constexpr int NQF = D / 16;
 // lists of KL = 10 (k <= 10) or 15 (the float64 mode's 10 + 5 guard entries,
 // the most the 160-KiB LDS holds beside the ring)
+// lists: KL = 10 lane-interleaved ([entry][lane]); KL = 15 (cooperative
+// insertion) one lane's entries contiguous, lanes list_stride entries apart
+// (an odd number of 8-byte bank pairs: both the per-lane accesses of 32 lanes
+// and the one-list-per-16-lanes accesses are free of bank conflicts)
 template <int KL>
-constexpr size_t lds_bytes() { return (size_t)NSLOT * STAGE + (size_t)NW * KL * 64 * 8 + 64; }
+constexpr int list_stride() { return KL == 10 ? 11 : KL; }
+template <int KL>
+constexpr size_t lds_bytes() { return (size_t)NSLOT * STAGE + (size_t)NW * 64 * list_stride<KL>() * 8 + 64; }
 static_assert(lds_bytes<15>() <= 160 * 1024, "LDS budget");
 }  // namespace v3
 
@@ -1206,6 +1212,19 @@ __device__ __forceinline__ f32x16 mfma_acc_v(const f32x16& c, const half8& a, co
     asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
     return d;
 }
+// The block's last MFMA with the wait for its result in the same asm
+// statement: the compiler does not know these are matrix instructions, so it
+// inserts no wait states before reading their results, and it may copy the
+// accumulators to other registers (a read) anywhere after the last MFMA;
+// nothing can come between this MFMA and its drain (16 passes: >= 18 wait
+// states before a VALU reads the result).  tests/test_codeobj.py checks it.
+__device__ __forceinline__ f32x16 mfma_last_v(const f32x16& c, const half8& a, const half8& b) {
+    f32x16 d = c;
+    asm volatile("v_mfma_f32_32x32x16_f16 %0, %1, %2, %0\n\ts_nop 7\n\ts_nop 7\n\ts_nop 3"
+                 : "+v"(d) : "v"(a), "v"(b));
+    return d;
+}
+// (diagnostic ABL 61: the wait at the epilogue instead)
 __device__ __forceinline__ f32x16 mfma_drain_v(const f32x16& c) {
     f32x16 d = c;
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(d));
@@ -1225,13 +1244,15 @@ __device__ __forceinline__ uint64_t lds_get_u64_at(uint32_t addr) {
     asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
     return v;
 }
-template <int KL, int OFF = 0>
+template <int KL, int OFF = 0, int ES = 512>
 __device__ __forceinline__ void list_store(uint32_t addr, const uint64_t (&L)[KL]) {
     [&]<int... I>(std::integer_sequence<int, I...>) {
-        (lds_put_u64_at<OFF + I * 512>(addr, L[I]), ...);
+        (lds_put_u64_at<OFF + I * ES>(addr, L[I]), ...);
     }(std::make_integer_sequence<int, KL>{});
 }
-template <int KL, int OFF = 0>
+// entry i at addr + OFF + i * ES (ES = 512: the lane-interleaved layout of
+// round 1, 8: one lane's entries contiguous)
+template <int KL, int OFF = 0, int ES = 512>
 __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
     static_assert(KL == 10 || KL == 15, "one asm block of 10 or 15 reads");
     // all reads in flight, one wait (a wait per read would serialise the LDS
@@ -1251,8 +1272,9 @@ __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
             "s_waitcnt lgkmcnt(0)"
             : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
               "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9])
-            : "v"(addr), "i"(OFF), "i"(OFF + 512), "i"(OFF + 1024), "i"(OFF + 1536), "i"(OFF + 2048),
-              "i"(OFF + 2560), "i"(OFF + 3072), "i"(OFF + 3584), "i"(OFF + 4096), "i"(OFF + 4608)
+            : "v"(addr), "i"(OFF), "i"(OFF + ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES),
+              "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES),
+              "i"(OFF + 8 * ES), "i"(OFF + 9 * ES)
             : "memory");
     } else {
         asm volatile(
@@ -1275,9 +1297,10 @@ __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
             : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
               "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9]), "=&v"(L[10]), "=&v"(L[11]),
               "=&v"(L[12]), "=&v"(L[13]), "=&v"(L[14])
-            : "v"(addr), "i"(OFF), "i"(OFF + 512), "i"(OFF + 1024), "i"(OFF + 1536), "i"(OFF + 2048),
-              "i"(OFF + 2560), "i"(OFF + 3072), "i"(OFF + 3584), "i"(OFF + 4096), "i"(OFF + 4608),
-              "i"(OFF + 5120), "i"(OFF + 5632), "i"(OFF + 6144), "i"(OFF + 6656), "i"(OFF + 7168)
+            : "v"(addr), "i"(OFF), "i"(OFF + ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES),
+              "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES),
+              "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES), "i"(OFF + 11 * ES),
+              "i"(OFF + 12 * ES), "i"(OFF + 13 * ES), "i"(OFF + 14 * ES)
             : "memory");
     }
 }
@@ -1296,6 +1319,36 @@ __device__ __forceinline__ void list_sort(uint64_t (&L)[KL]) {
     }
 }
 
+// The same on distance words only, equal distances kept in arrival order
+// (stable): the scan's per-lane lists, whose rows arrive in ascending order.
+template <int KL>
+__device__ __forceinline__ void list_sort_hi(uint64_t (&L)[KL]) {
+#pragma unroll
+    for (int r = 0; r < KL; ++r) {
+#pragma unroll
+        for (int i = r & 1; i + 1 < KL; i += 2) {
+            const uint64_t x = L[i], y = L[i + 1];
+            const bool sw = (uint32_t)(y >> 32) < (uint32_t)(x >> 32);
+            L[i] = sw ? y : x;
+            L[i + 1] = sw ? x : y;
+        }
+    }
+}
+// list_insert on distance words: x goes after the entries of equal distance
+// (it arrived later); caller guarantees dist(x) < dist(L[KL-1]).
+template <int KL>
+__device__ __forceinline__ void list_insert_hi(uint64_t (&L)[KL], uint64_t x) {
+    const uint32_t xh = (uint32_t)(x >> 32);
+    bool lt_i = xh < (uint32_t)(L[KL - 1] >> 32);
+#pragma unroll
+    for (int i = KL - 1; i > 0; --i) {
+        const bool lt_p = xh < (uint32_t)(L[i - 1] >> 32);
+        L[i] = lt_p ? L[i - 1] : (lt_i ? x : L[i]);
+        lt_i = lt_p;
+    }
+    L[0] = lt_i ? x : L[0];
+}
+
 extern "C" __device__ uint32_t __ockl_wfred_or_u32(uint32_t);
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 
@@ -1308,6 +1361,13 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // [10] earliest entry tick, [11] latest exit tick, [12] workgroups
 __device__ unsigned long long lmi_dbg[16];
 #endif
+
+// lowest set bit of a wave-uniform mask, -1 if none (s_ff1_i32_b64)
+__device__ __forceinline__ int sff1_u64(uint64_t m) {
+    int r;
+    asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    return r;
+}
 
 // Per-lane pick of acc[rg] (rg differs by lane): a 4-level select tree on
 // lane masks (inline asm: written as C++ ternaries the compiler turns the
@@ -1364,12 +1424,22 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     // (ABL 53, round 1's placement: an LDS-DMA issue holds its wave for ~45-60
     // cycles, so the two waves of a SIMD issued theirs at different MFMAs)
     constexpr int kDmaTT = 2, kDmaLate = 10;
+    // Top-k insertion.  KL = 10: every lane inserts into its own list (a
+    // register copy of it: load, insert, store).  KL = 15: a register copy of
+    // 15 entries does not fit beside the query fragments (the compiler
+    // spills them into the MFMA stream), so the lists are updated
+    // cooperatively, 16 lanes per list, an entry per lane, four lists per
+    // wave instruction.  ABL 65: cooperative at KL = 10 too (slower there).
+    constexpr bool kCoop = KL > 10 || ABL == 65;
+    constexpr int LS = kCoop ? list_stride<KL>() : KL;  // entries per lane column
+    constexpr int ES = kCoop ? 8 : 512;                  // bytes between a list's entries
+    constexpr uint32_t LSTR = kCoop ? LS * 8 : 8;        // bytes between lanes' lists
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     unsigned char* ring = smem;
-    // [wave][KL][64 lanes] u64: every lane's partial top-k list (lane-private
-    // column; registers are all spoken for by the query fragments)
+    // every lane's partial top-k list in LDS (registers are all spoken for
+    // by the query fragments): entry i of lane l at l * LSTR + i * ES
     uint64_t* lists = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
-    int* wtab = reinterpret_cast<int*>(lists + NW * KL * 64);  // [NW] SIMD ids, [NW] tile
+    int* wtab = reinterpret_cast<int*>(lists + NW * 64 * LS);  // [NW] SIMD ids, [NW] tile
     int& s_tile = wtab[NW];
 
     const int tid = threadIdx.x;
@@ -1404,8 +1474,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     const uint64_t clk0 = __builtin_amdgcn_s_memtime();
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    // this lane's list column: entry i at lbase + i * 512
-    const uint32_t lbase = (uint32_t)(uintptr_t)(lists + wave * KL * 64 + lane);
+    const uint32_t wbase = (uint32_t)(uintptr_t)(lists + wave * 64 * LS);  // this wave's lists
+    const uint32_t lbase = wbase + (uint32_t)lane * LSTR;                   // this lane's
 
     for (;;) {
         if (tid == 0) s_tile = dequeue_tile(a.meta, a.work, gx, ng);
@@ -1428,27 +1498,47 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         const int pp = tile.pp0 + 32 * slot + col;
 
         half8 qf[NQF];
-        uint64_t thr = 0ull;
+        // the lane's bound: only objects with ord(d) <= thr can enter the
+        // pair's top-KL (the distance part of a key: the bound may come from
+        // another chunk, whose rows are ordered differently, so ties at it
+        // survive to the chunk merge)
+        uint32_t thr = 0u;
         float my_invq = 0.0f;
-        uint64_t lo = 0ull;  // LO: this pair's lower-bound key
-        float lo_d = -__builtin_inff();
+        float lo_d = -__builtin_inff();  // LO: the distance of this pair's lower-bound key,
+        int lo_row = 0;                  // and the chunk's first row after its position
         int cnt = 0;  // entries in this lane's list; < KL: an unsorted append buffer
         if (wave_live) {
+            bool done = false;
             const int q = live ? a.pair_q[pp] / a.R : 0;
             if (LO && live) {
-                lo = a.lo_g[a.pair_q[pp]];
-                if ((uint32_t)(lo >> 32) != 0u) lo_d = ord2f((uint32_t)(lo >> 32));
+                // positions ascend inside a chunk, so "after the lower bound's
+                // position" is "at or after local row lo_row" (binary search,
+                // once per tile; the walk then needs no memory access)
+                const uint64_t lo = a.lo_g[a.pair_q[pp]];
+                if (lo == kEmptyKey) {
+                    done = true;  // the pair's objects are all listed: take nothing
+                } else if ((uint32_t)(lo >> 32) != 0u) {
+                    lo_d = ord2f((uint32_t)(lo >> 32));
+                    int l = 0, r = nrows;
+                    while (l < r) {
+                        const int mid = (l + r) >> 1;
+                        if ((uint32_t)a.gpos[row0u + mid] > (uint32_t)lo) r = mid;
+                        else l = mid + 1;
+                    }
+                    lo_row = l;
+                }
             }
             const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
 #pragma unroll
             for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
-            thr = live ? (uint64_t)a.thr_g[pp] : 0ull;  // dead slots reject everything
+            // dead slots (and exhausted pairs) reject everything
+            thr = live && !done ? (uint32_t)(a.thr_g[pp] >> 32) : 0u;
             my_invq = live ? a.invq[q] : 0.0f;
         }
         {
             uint64_t E[KL];
             list_clear<KL>(E);
-            list_store<KL>(opaque_u(lbase), E);
+            list_store<KL, 0, ES>(opaque_u(lbase), E);
         }
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         __syncthreads();
@@ -1479,7 +1569,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                                                      0, kAux);
             if (j == NST - 1 && lane < 4)
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(ring + nb_area * STAGE + NORM_OFF + 16 * w),
-                                                         4, (uint32_t)((4 * w + lane) * 4), b * 128, 0, 0);
+                                                         4, (uint32_t)((4 * w + opaque(lane)) * 4), b * 128, 0, 0);
         };
         auto dma_stage = [&](int so, int b, int j) { dma_stage_w(so, b, j, wave); };
         // block b lives in slots NST*(b&1) .. +NST-1; block 0 is the prologue,
@@ -1490,10 +1580,11 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         const uint32_t lane_off = (uint32_t)(((lane >> 1) & 15) * PIECEP + (lane & 1) * 16 + (lane >> 5) * 32);
 
         f32x16 acc;
-        uint64_t xg_carry = kEmptyKey;  // global bounds fetched, not yet applied
+        uint32_t xg_carry = 0xffffffffu;  // global bound fetched, not yet applied
         // ---- epilogue of block eb (accumulators of its 48 MFMAs in acc) ------
         auto epilogue = [&](int eb) {
-            acc = mfma_drain_v(acc);
+            // (acc is complete: the block's last MFMA carried its drain)
+            if (ABL == 61) acc = mfma_drain_v(acc);
             const int ln = opaque(lane);
             const int hh = ln >> 5;
             // block eb's norms: the norm area of slot eb % 3 (three blocks in
@@ -1501,19 +1592,32 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             const unsigned char* nb = ring + (eb % 3) * STAGE + NORM_OFF + hh * 16;
             const int vr = nrows - eb * 32 - 4 * hh;  // valid rows past this lane's offset
             thr = std::min(thr, xg_carry);
-            xg_carry = kEmptyKey;
-            const float bound = key_dist_bound(thr);
+            xg_carry = 0xffffffffu;
+            const float bound = key_dist_bound((uint64_t)thr << 32);
+            // the filter: a candidate mask, one bit per register, register 0
+            // in bit 15 (mask = 2 mask + ok); only the chunk's last block
+            // checks the row count
             uint32_t mask = 0;
+            auto filter = [&]<bool TAIL>() {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const f32x4 n4 = *reinterpret_cast<const f32x4*>(nb + 32 * g);
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 n4 = *reinterpret_cast<const f32x4*>(nb + 32 * g);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int reg = 4 * g + e;
-                    const float d = fmaf(-acc[reg], my_invq * n4[e], 1.0f);
-                    mask |= (e + 8 * g < vr && d <= bound && (!LO || d >= lo_d)) ? (1u << reg) : 0u;
+                    for (int e = 0; e < 4; ++e) {
+                        const int reg = 4 * g + e;
+                        const float d = fmaf(-acc[reg], my_invq * n4[e], 1.0f);
+            
+                        // (LO: lo_d <= d <= bound as one med3 and one compare)
+                        bool ok = LO ? __builtin_amdgcn_fmed3f(d, lo_d, bound) == d : d <= bound;
+                        if (TAIL) ok = ok && e + 8 * g < vr;
+                        mask = mask + mask + (ok ? 1u : 0u);
+                    }
                 }
-            }
+            };
+            if (eb + 1 < nblk && ABL != 62)
+                filter.template operator()<false>();
+            else
+                filter.template operator()<true>();
 #ifdef LMI_ABLATION
             if (ABL == 7) {
                 const uint32_t nc = __ockl_wfred_add_u32(__builtin_popcount(mask));
@@ -1525,61 +1629,118 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             }
 #endif
             if (!kNoIns && __any(mask != 0)) {
-                const uint32_t la = opaque_u(lbase);
                 const uint32_t rb = (uint32_t)(row0u + eb * 32 + 4 * hh);
-                // every lane walks its own candidates, lowest register first:
+                // Every lane walks its own candidates, lowest register first:
                 // iterations = the largest per-lane count (usually 1-2), the
                 // accumulator picked by a select tree.  Candidates: d <= the
                 // distance part of thr, a bound that may come from another
                 // chunk (rows ordered differently there), so no key test
-                // against it; ties at the bound are resolved by the chunk merge.
+                // against it; ties at the bound are resolved by the chunk
+                // merge.  A lane meets its rows in ascending order (registers
+                // ascending inside a block, blocks ascending), so a list
+                // ordered by distance with equal distances in arrival order is
+                // ordered by key: the list compares distance words only.
                 uint32_t m = mask;
+                if constexpr (kCoop) {
+                    // Round r: every lane with a candidate left offers its
+                    // next one; lane group g (16 lanes, lane j = entry j)
+                    // takes the list of the g-th offering lane: entry j stays
+                    // if it comes before the key, else takes the key (entry
+                    // j-1 comes before it, or j = 0) or entry j-1 (DPP row
+                    // shift).  "Before" = smaller distance, or equal distance
+                    // (it arrived earlier).
+                    const int grp = ln >> 4, j = ln & 15;
+#pragma unroll 1
+                    while (__any(m != 0)) {
+                        uint64_t key = kEmptyKey;
+                        if (m != 0) {
+                            const int hb = 31 - __builtin_clz(m);
+                            m ^= 1u << hb;
+                            const int rg = 15 - hb;
+                            const int i = (rg & 3) + 8 * (rg >> 2);
+                            const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
+                            const float d = fmaf(-select16(acc, rg), my_invq * n1, 1.0f);
+                            key = make_key(d, rb + (uint32_t)i);
+                            // (at or before the pair's lower bound: not this pass's)
+                            if (LO && d == lo_d && eb * 32 + 4 * hh + i < lo_row) key = kEmptyKey;
+                        }
+                        const bool offer = key != kEmptyKey && (uint32_t)(key >> 32) <= thr;
+                        uint64_t pend = __builtin_amdgcn_ballot_w64(offer);
+                        const uint32_t klo = (uint32_t)key, khi = (uint32_t)(key >> 32);
+#pragma unroll 1
+                        while (pend != 0) {
+                            // this batch's offering lanes (s_ff1 gives -1 once
+                            // pend is empty); group g takes the g-th one's key
+                            const int s0 = sff1_u64(pend);
+                            pend &= pend - 1;
+                            const int s1 = sff1_u64(pend);
+                            pend &= pend - 1;
+                            const int s2 = sff1_u64(pend);
+                            pend &= pend - 1;
+                            const int s3 = sff1_u64(pend);
+                            pend &= pend - 1;
+                            const int my = grp == 0 ? s0 : grp == 1 ? s1 : grp == 2 ? s2 : s3;
+                            const int sl = my < 0 ? 0 : my;
+                            const uint32_t kl = (uint32_t)__builtin_amdgcn_ds_bpermute(sl << 2, (int)klo);
+                            const uint32_t kh = (uint32_t)__builtin_amdgcn_ds_bpermute(sl << 2, (int)khi);
+                            const bool act = my >= 0 && j < KL;
+                            const uint32_t ea = wbase + (uint32_t)sl * LSTR + (uint32_t)j * 8u;
+                            uint64_t e = kEmptyKey;
+                            if (act) e = lds_get_u64(ea);
+                            const bool before = (uint32_t)(e >> 32) <= kh;
+                            const uint32_t pl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)e, 0x111, 0xf, 0xf, false);
+                            const uint32_t ph = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(e >> 32), 0x111, 0xf, 0xf, false);
+                            const int pb = __builtin_amdgcn_update_dpp(0, before ? 1 : 0, 0x111, 0xf, 0xf, false);
+                            const uint64_t nv = (j == 0 || pb != 0) ? (((uint64_t)kh << 32) | kl)
+                                                                     : (((uint64_t)ph << 32) | pl);
+                            if (act && !before) lds_put_u64(ea, nv);
+                        }
+                        // the offering lanes' lists changed: their KL-th key
+                        if (offer) thr = std::min(thr, (uint32_t)(lds_get_u64(lbase + (KL - 1) * 8) >> 32));
+                    }
+                } else {
+                const uint32_t la = opaque_u(lbase);
 #pragma unroll 1
                 while (__any(m != 0)) {
                     if (m != 0) {
-                        const int rg = __builtin_ctz(m);
-                        m &= m - 1;
-                        const float dot = select16(acc, rg);
+                        const int hb = 31 - __builtin_clz(m);
+                        m ^= 1u << hb;
+                        const int rg = 15 - hb;
                         const int i = (rg & 3) + 8 * (rg >> 2);
                         const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
-                        const float d = fmaf(-dot, my_invq * n1, 1.0f);
+                        const float d = fmaf(-select16(acc, rg), my_invq * n1, 1.0f);
                         const uint64_t key = make_key(d, rb + (uint32_t)i);
-                        if (LO && !above_lo(d, lo, a.gpos, rb + (uint32_t)i)) {
+                        if (LO && d == lo_d && eb * 32 + 4 * hh + i < lo_row) {
                             // at or before the pair's lower bound: not this pass's
                         } else if (cnt < KL) {
                             // append mode: the first KL candidates are stored
-                            // unsorted (a few instructions); a full buffer is
-                            // sorted once and the lane switches to list mode
+                            // unsorted; a full buffer is sorted once (stable)
+                            // and the lane switches to list mode
                             lds_put_u64(la + (uint32_t)cnt * 512u, key);
-#ifdef LMI_ABLATION
-                            if (ABL == 7) atomicAdd(&lmi_dbg[2], 1ull);
-                            if (ABL == 7 && cnt + 1 == KL) atomicAdd(&lmi_dbg[4], 1ull);
-#endif
                             if (++cnt == KL) {
                                 uint64_t L[KL];
                                 list_load<KL>(la, L);
-                                list_sort<KL>(L);
+                                list_sort_hi<KL>(L);
                                 list_store<KL>(la, L);
-                                thr = std::min(thr, L[KL - 1]);
+                                thr = std::min(thr, (uint32_t)(L[KL - 1] >> 32));
                             }
                         } else {
-                            // (the list lives in LDS: registers are taken by
-                            // the query fragments)
                             uint64_t L[KL];
                             list_load<KL>(la, L);
-                            if (key < L[KL - 1]) {
-#ifdef LMI_ABLATION
-                                if (ABL == 7) atomicAdd(&lmi_dbg[3], 1ull);
-#endif
-                                list_insert<KL>(L, key);
+                            if (ABL == 64 ? key < L[KL - 1] : (uint32_t)(key >> 32) < (uint32_t)(L[KL - 1] >> 32)) {
+                                if (ABL == 64)
+                                    list_insert<KL>(L, key);
+                                else
+                                    list_insert_hi<KL>(L, key);
                                 list_store<KL>(la, L);
                             }
-                            thr = std::min(thr, L[KL - 1]);
+                            thr = std::min(thr, (uint32_t)(L[KL - 1] >> 32));
                         }
                     }
                 }
+                }
                 // every bound is an upper bound of the pair's k-th key: share it
-                thr = std::min(thr, partner_u64(thr, hh));
+                thr = std::min(thr, partner_u32(thr, hh));
             }
         };
         // The two waves of a SIMD are staggered (MI355X_MICROARCH "two waves
@@ -1622,13 +1783,15 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             // other chunks run concurrently); the returning atomic is consumed
             // in the next epilogue, behind this block's MFMAs
             if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live)
-                xg_carry = std::min<uint64_t>(xg_carry, atomicMin(&a.thr_g[pp], (unsigned long long)thr));
+                xg_carry = std::min(xg_carry, (uint32_t)(atomicMin(&a.thr_g[pp], ((unsigned long long)thr << 32) | 0xffffffffull) >> 32));
+            if (kDmaOnly || !wave_live) {
+                // (no MFMA stream: a branch out of the middle of one would
+                // join its accumulators to a path without the drain)
+                if (more && !kDmaHead)
+                    for (int j = 0; j < NST; ++j) dma_stage(ws0 + j * STAGE, blk + 1, j);
+            } else {
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
-                if (kDmaOnly || !wave_live) {
-                    if (more && !kDmaHead) dma_stage(ws0 + j * STAGE, blk + 1, j);
-                    continue;
-                }
                 const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
 #define LMI_A3(tt) (*reinterpret_cast<const half8*>(rp + 64 * (tt)))
                 half8 af[16];
@@ -1637,8 +1800,9 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
 #pragma unroll
                 for (int tt = 0; tt < 16; ++tt) {
                     if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
-                    acc = (j == 0 && tt == 0) ? mfma_first_v(af[0], qf[0])
-                                              : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
+                    acc = (j == 0 && tt == 0)        ? mfma_first_v(af[0], qf[0])
+                          : (j == NST - 1 && tt == 15 && ABL != 61) ? mfma_last_v(acc, af[tt], qf[j * 16 + tt])
+                                                       : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
                     if (!kDmaHead && tt == (late ? kDmaLate : kDmaTT) && more)
                         dma_stage(ws0 + j * STAGE, blk + 1, j);
                     // keep the A-fragment reads 3 MFMAs ahead, no further
@@ -1646,12 +1810,13 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 }
 #undef LMI_A3
             }
+            }
             if (kNoEpi || !wave_live || defer) continue;
             epilogue(blk);
         }
         if (defer && nblk > 0) epilogue(nblk - 1);
         // lanes still in append mode hold an unsorted (EMPTY-padded) buffer
-        if (__any(cnt < KL)) {
+        if (!kCoop && __any(cnt < KL)) {
             if (cnt < KL) {
                 uint64_t L[KL];
                 list_load<KL>(lbase, L);
@@ -1664,8 +1829,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         // ---- merge the two partial lists of each query (lanes col, col+32) ----
         if (h == 0 && live) {
             uint64_t L[KL], P[KL];
-            list_load<KL>(lbase, L);
-            list_load<KL, 32 * 8>(lbase, P);
+            list_load<KL, 0, ES>(lbase, L);
+            list_load<KL, 32 * LSTR, ES>(lbase, P);
 #pragma unroll
             for (int i = 0; i < KL; ++i) {
                 if (P[i] >= L[KL - 1]) break;
@@ -2002,6 +2167,10 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 51) return launch_scan3_v<KL, 51>(b, s);
     if (abl == 52) return launch_scan3_v<KL, 52>(b, s);
     if (abl == 53) return launch_scan3_v<KL, 53>(b, s);
+    if (abl == 61) return launch_scan3_v<KL, 61>(b, s);
+    if (abl == 62) return launch_scan3_v<KL, 62>(b, s);
+    if (abl == 64) return launch_scan3_v<KL, 64>(b, s);
+    if (abl == 65) return launch_scan3_v<KL, 65>(b, s);
 #endif
     return launch_scan3_v<KL, 0>(b, s);
 }
@@ -2230,8 +2399,14 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         if (!env_config().scan_keep_thr)
 #endif
         LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
-        if (w.use_v3 && LOP)
-            rc = (KL == 10) ? launch_scan3_v<10, 0, true>(b, s) : launch_scan3_v<15, 0, true>(b, s);
+        if (w.use_v3 && LOP) {
+            // the passes' lists are 15 entries on v3 (passes_of)
+            if (KL != 15) {
+                set_error("lower-bound scan passes take 15-entry lists on scan v3");
+                return LMI_E_UNSUPPORTED;
+            }
+            rc = launch_scan3_v<15, 0, true>(b, s);
+        }
         else if (w.use_v3)
             rc = (KL == 10) ? launch_scan3<10>(b, s) : launch_scan3<15>(b, s);
         else

@@ -1,0 +1,115 @@
+"""Code-object guard for the scan kernels (CPU; reads the built liblmi_hip.so).
+
+scan3_kernel issues its MFMAs as VGPR-form inline asm (lmi_scan.hip,
+mfma_acc_v), so the compiler does not see them as matrix instructions and
+inserts no hazard wait states around them.  A register spill of a query
+fragment reloaded between those MFMAs (scratch_load right before the MFMA that
+reads it) is then both a hazard (wrong distances) and a vmcnt(0) stall on the
+in-flight row DMA; a copy of the accumulators placed after the last MFMA
+reads an unfinished result.  This test disassembles the gfx950 code object and
+fails if any scratch access sits inside a scan3 kernel's MFMA stream, or if any
+instruction touches an MFMA's accumulators before the next MFMA or the drain
+(s_nop 7) that ends the stream."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd", "li", "liblmi_hip.so")
+OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
+
+
+def _disassembly(tmp_path):
+    so = tmp_path / "lib.so"
+    shutil.copy(LIB, so)
+    subprocess.run([OBJDUMP, "--offloading", str(so)], cwd=tmp_path, check=True,
+                   capture_output=True)
+    text = []
+    for f in sorted(tmp_path.iterdir()):
+        if "amdgcn" in f.name and "gfx950" in f.name:
+            r = subprocess.run([OBJDUMP, "-d", "--mcpu=gfx950", str(f)], check=True,
+                               capture_output=True, text=True)
+            text.append(r.stdout)
+    return "\n".join(text)
+
+
+def _functions(dis):
+    """{symbol: [instruction lines]} of every disassembled function."""
+    out, name = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            name = m.group(1)
+            out[name] = []
+        elif name is not None and line.strip() and not line.startswith("Disassembly"):
+            out[name].append(line.strip())
+    return out
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)),
+                    reason="needs the built library and llvm-objdump")
+def test_no_spill_inside_scan3_mfma_stream(tmp_path):
+    funcs = _functions(_disassembly(tmp_path))
+    scan3 = {k: v for k, v in funcs.items() if "scan3_kernel" in k}
+    assert scan3, "no scan3_kernel in the code object"
+    for name, ins in scan3.items():
+        mf = [i for i, l in enumerate(ins) if "v_mfma" in l]
+        assert mf, name
+        bad = [i for i, l in enumerate(ins) if "scratch_" in l and
+               (mf[0] <= i <= mf[-1] or any(0 <= m - i <= 12 for m in mf))]
+        assert not bad, f"{name}: scratch access in the MFMA stream: {[ins[i] for i in bad][:4]}"
+        # nothing may touch an MFMA's accumulators on any path from it to the
+        # next MFMA (which takes them as its C operand) or to the drain that
+        # ends the stream (s_nop 7); A/B operand registers may be refilled (the
+        # A-fragment prefetch does that by design)
+        addr = {}
+        for k, l in enumerate(ins):
+            m = re.search(r"//\s*([0-9A-Fa-f]+):", l)
+            if m:
+                addr[int(m.group(1), 16)] = k
+        for i in mf:
+            acc = _regs(ins[i].split("//")[0].split(None, 1)[1].split(",")[0])
+            todo, seen = [i + 1], set()
+            while todo:
+                k = todo.pop()
+                while k < len(ins) and k not in seen:
+                    seen.add(k)
+                    l = ins[k]
+                    if "v_mfma" in l or "s_nop 7" in l:
+                        break
+                    assert not (_regs(l.split("//")[0]) & acc), \
+                        f"{name}: `{l.split('//')[0].strip()}` touches the accumulators of an unfinished MFMA"
+                    op = l.split()[0]
+                    if op.startswith(("s_branch", "s_cbranch")):
+                        tgt = _target(l)
+                        if tgt is not None and tgt in addr:
+                            todo.append(addr[tgt])
+                        if op.startswith("s_branch"):
+                            break
+                    if op.startswith(("s_setpc", "s_endpgm")):
+                        break
+                    k += 1
+
+
+def _target(line):
+    """Branch target address of an s_branch / s_cbranch_* line (SIMM16 dwords
+    relative to the next instruction)."""
+    m = re.match(r"^\s*s_c?branch\S*\s+(-?\d+)\s*//\s*([0-9A-Fa-f]+):", line)
+    if not m:
+        return None
+    simm = int(m.group(1))
+    if simm >= 1 << 15:
+        simm -= 1 << 16
+    return int(m.group(2), 16) + 4 + 4 * simm
+
+
+def _regs(text):
+    """The VGPR numbers an instruction's operand text names."""
+    out = set()
+    for a, b in re.findall(r"\bv\[(\d+):(\d+)\]", text):
+        out.update(range(int(a), int(b) + 1))
+    out.update(int(v) for v in re.findall(r"\bv(\d+)\b", text))
+    return out
