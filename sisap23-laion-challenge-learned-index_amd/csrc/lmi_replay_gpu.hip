@@ -12,10 +12,12 @@
 //     broadcast to the whole group         :192-193
 // and is checked bit for bit against it (tests/test_gpu_replay.py).
 //
+// Before round 0, replay_groups_kernel (C x R workgroups) lays out every
+// round's groups: the queries with classes[q, r] == c in ascending q.
 // Layout of one round r (R rounds run in order on one stream):
 //   replay_thr_kernel    per query: thr = max of the merged row; D_r <- (FILL, -1)
-//   replay_group_kernel  per category c (one workgroup): the queries with
-//                        classes[q, r] == c in ascending q; thresholded rounds
+//   replay_group_kernel  per category c (one workgroup) over its group of
+//                        round r; thresholded rounds
 //                        need U = sorted unique union of the relevant
 //                        positions, but only its smallest kr + kl members
 //                        matter (fillers and the |U| < kr test), found by
@@ -71,7 +73,8 @@ struct RoundArgs {
     int32_t lists_f64;
     const int32_t* lists_p;  // [nq][R][kl]
     const int64_t* bucket_size;
-    int32_t* groups;         // [nq] this round's groups, category c at [g0(c), g1(c))
+    const int32_t* groups;   // [nq] this round's groups, category c at [g0(c), g1(c))
+    const int32_t* gb;       // [C][2] this round's (g0, g1) per category
     int32_t thresholded;
     const double* thr;       // [nq]
     double* dr_d;            // [nq][kr]
@@ -151,6 +154,72 @@ __device__ inline int block_reduce_g(int v, int* sh, bool is_min) {
 __device__ inline int block_sum_g(int v, int* sh) { return block_reduce_g<kTG>(v, sh, false); }
 __device__ inline int block_min_g(int v, int* sh) { return block_reduce_g<kTG>(v, sh, true); }
 
+// The groups of every round at once (grid C x R), before round 0: category c
+// of round r = the queries with classes[q, r] == c in ascending q, placed at
+// [g0, g1) of groups[r] with g0 = #{q : classes[q, r] < c}.
+__global__ __launch_bounds__(kTG) void replay_groups_kernel(const int32_t* __restrict__ classes,
+                                                            int32_t nq, int32_t R, int32_t C,
+                                                            int32_t* __restrict__ groups_all,
+                                                            int32_t* __restrict__ gb_all) {
+    const int c = blockIdx.x, r = blockIdx.y;
+    const int tid = threadIdx.x;
+    int32_t* groups = groups_all + (size_t)r * nq;
+    int32_t* gb = gb_all + ((size_t)r * C + c) * 2;
+    // every wave takes a contiguous segment of the queries, read coalesced,
+    // matches ranked by ballot
+    __shared__ int wc[2][kTG / 64];
+    const int lane = tid & 63, w = tid >> 6;
+    const int seg = ((nq + kTG / 64 - 1) / (kTG / 64) + 63) & ~63;
+    const int qa = min(nq, w * seg), qb = min(nq, qa + seg);
+    constexpr int kU = 8;  // loads in flight per lane (each pass is latency-bound)
+    int n_eq = 0, n_lt = 0;
+    for (int q0 = qa; q0 < qb; q0 += kU * 64) {
+        int v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int q = q0 + 64 * u + lane;
+            v[u] = q < qb ? classes[(size_t)q * R + r] : INT32_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            n_eq += __popcll(__ballot(v[u] == c));
+            n_lt += __popcll(__ballot(v[u] < c));
+        }
+    }
+    if (lane == 0) {
+        wc[0][w] = n_eq;
+        wc[1][w] = n_lt;
+    }
+    __syncthreads();
+    int before = 0, n_g = 0, lt = 0;
+    for (int i = 0; i < kTG / 64; ++i) {
+        before += (i < w) ? wc[0][i] : 0;
+        n_g += wc[0][i];
+        lt += wc[1][i];
+    }
+    if (tid == 0) {
+        gb[0] = lt;
+        gb[1] = lt + n_g;
+    }
+    if (n_g == 0) return;
+    int o = lt + before;
+    const uint64_t lanes_lt = (1ull << lane) - 1ull;
+    for (int q0 = qa; q0 < qb; q0 += kU * 64) {
+        int v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int q = q0 + 64 * u + lane;
+            v[u] = q < qb ? classes[(size_t)q * R + r] : INT32_MAX;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t m = __ballot(v[u] == c);
+            if (v[u] == c) groups[o + __popcll(m & lanes_lt)] = q0 + 64 * u + lane;
+            o += __popcll(m);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
     __shared__ int sh[kTG / 64];
     __shared__ int32_t S[2 * kMaxKr + 16];  // smallest members of U, ascending
@@ -163,61 +232,8 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
     if (a.bucket_size[c] <= 0) return;  // groupby visits non-empty categories only
     // the group: queries with classes[q, r] == c in ascending q, placed at
     // [g0, g1) with g0 = #{q : classes[q, r] < c} (disjoint across categories)
-    int g0, g1;
-    {
-        // every wave takes a contiguous segment of the queries, read
-        // coalesced, matches ranked by ballot
-        __shared__ int wc[2][kTG / 64];
-        const int lane = tid & 63, w = tid >> 6;
-        const int seg = ((a.nq + kTG / 64 - 1) / (kTG / 64) + 63) & ~63;
-        const int qa = min(a.nq, w * seg), qb = min(a.nq, qa + seg);
-        constexpr int kU = 8;  // loads in flight per lane (each pass is latency-bound)
-        int n_eq = 0, n_lt = 0;
-        for (int q0 = qa; q0 < qb; q0 += kU * 64) {
-            int v[kU];
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int q = q0 + 64 * u + lane;
-                v[u] = q < qb ? a.classes[(size_t)q * a.R + a.r] : INT32_MAX;
-            }
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                n_eq += __popcll(__ballot(v[u] == c));
-                n_lt += __popcll(__ballot(v[u] < c));
-            }
-        }
-        if (lane == 0) {
-            wc[0][w] = n_eq;
-            wc[1][w] = n_lt;
-        }
-        __syncthreads();
-        int before = 0, n_g = 0, lt = 0;
-        for (int i = 0; i < kTG / 64; ++i) {
-            before += (i < w) ? wc[0][i] : 0;
-            n_g += wc[0][i];
-            lt += wc[1][i];
-        }
-        if (n_g == 0) return;
-        g0 = lt;
-        g1 = lt + n_g;
-        int o = g0 + before;
-        const uint64_t lanes_lt = (1ull << lane) - 1ull;
-        for (int q0 = qa; q0 < qb; q0 += kU * 64) {
-            int v[kU];
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int q = q0 + 64 * u + lane;
-                v[u] = q < qb ? a.classes[(size_t)q * a.R + a.r] : INT32_MAX;
-            }
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const uint64_t m = __ballot(v[u] == c);
-                if (v[u] == c) a.groups[o + __popcll(m & lanes_lt)] = q0 + 64 * u + lane;
-                o += __popcll(m);
-            }
-        }
-        __syncthreads();
-    }
+    const int g0 = a.gb[2 * c], g1 = a.gb[2 * c + 1];  // (replay_groups_kernel)
+    if (g1 <= g0) return;
 #ifdef LMI_ABLATION
     if (a.abl == 1) return;
 #endif
@@ -534,7 +550,7 @@ __global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, i
 }
 
 struct ReplayWs {
-    size_t groups, Fd[2], Fp[2], drd[2], drp[2], thr, uraw, total;
+    size_t groups, gb, Fd[2], Fp[2], drd[2], drp[2], thr, uraw, total;
 };
 
 ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
@@ -546,7 +562,8 @@ ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
         return at;
     };
     const int fs = std::max(kr, w);
-    s.groups = take((size_t)nq * 4);
+    s.groups = take((size_t)R * nq * 4);
+    s.gb = take((size_t)R * C * 2 * 4);
     for (int b = 0; b < 2; ++b) {
         s.Fd[b] = take((size_t)nq * fs * 8);
         s.Fp[b] = take((size_t)nq * fs * 4);
@@ -642,7 +659,11 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
     const int C = n_buckets;
     const int fs = std::max(k_round, w);
     int32_t* groups = (int32_t*)(ws + s.groups);
+    int32_t* gb = (int32_t*)(ws + s.gb);
     const dim3 qgrid((unsigned)((nq + kT - 1) / kT));
+    // every round's groups in one launch (C x R workgroups)
+    hipLaunchKernelGGL(replay_groups_kernel, dim3(C, R), dim3(kTG), 0, st, classes, nq, R, C, groups, gb);
+    LMI_LAUNCH_CHECK("replay_groups_kernel");
     int cur = 0;  // F lives in buffer cur; the merge writes the other one
     int wF = 0;
     for (int r = 0; r < R; ++r) {
@@ -669,7 +690,8 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         a.lists_f64 = lists_f64;
         a.lists_p = lists_pos;
         a.bucket_size = bucket_size;
-        a.groups = groups;
+        a.groups = groups + (size_t)r * nq;
+        a.gb = gb + (size_t)r * C * 2;
         a.thresholded = thresholded ? 1 : 0;
         a.thr = (const double*)(ws + s.thr);
         a.dr_d = drd;
