@@ -34,7 +34,7 @@ EnvConfig read_env() {
     e.scan_v2 = env_b("LMI_SCAN_V2");
     e.scan_abl = env_i("LMI_SCAN_ABL", 0);
     e.scan_groups = env_i("LMI_SCAN_GROUPS", 0);
-    e.scan_order = env_i("LMI_SCAN_ORDER", 1);
+    e.scan_order = env_i("LMI_SCAN_ORDER", 0);
     e.scan_lag = env_i("LMI_SCAN_LAG", 0);
     e.scan_no_pref = env_b("LMI_SCAN_NO_PREF");
     e.scan_keep_thr = env_b("LMI_SCAN_KEEP_THR");

@@ -13,7 +13,7 @@ struct EnvConfig {
     bool scan_v2;        // LMI_SCAN_V2: force the 4-wave ring
     int scan_abl;        // LMI_SCAN_ABL (diagnostic builds)
     int scan_groups;     // LMI_SCAN_GROUPS: tile queues (power of two <= 8), 0 = default
-    int scan_order;      // LMI_SCAN_ORDER: heavy-first tile order (default 1)
+    int scan_order;      // LMI_SCAN_ORDER: 0 plan order (default), 1 heavy-first per tile, 2 per chunk
     int scan_lag;        // LMI_SCAN_LAG
     bool scan_no_pref;   // LMI_SCAN_NO_PREF
     bool scan_keep_thr;  // LMI_SCAN_KEEP_THR (diagnostic builds)

@@ -299,15 +299,22 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
     }
 }
 
-// Tail balance: in every group queue the tiles after the seeds are stably
-// partitioned, heavy first, so the light ones (a partial chunk or a partial
-// query block: under half a full tile's rows x waves) run last, when the CUs
-// start to run dry.  Only the order changes (results are order-independent).
+// Optional (LMI_SCAN_ORDER=1|2; default off since round 2): in every group
+// queue the tiles after the seeds are stably partitioned, heavy first, so the
+// light ones (a partial chunk or a partial query block: under half a full
+// tile's rows x waves) run last.  Measured slower than the plan order once
+// the epilogue was reworked (7.17-7.22 vs 7.07-7.10 ms at 10M, same box,
+// profiles/r02_tile_order.txt): with the light, DMA-bound tiles all at the
+// end, the chip's HBM demand and MFMA power are uneven over the launch; the
+// plan order mixes them throughout.  Only the order changes (results are
+// order-independent).
 __global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ tiles,
                                                           Tile* __restrict__ tmp,
                                                           const int32_t* __restrict__ meta,
                                                           const int64_t* __restrict__ bucket_off,
-                                                          int32_t chunk_rows, int32_t QB) {
+                                                          int32_t chunk_rows, int32_t QB,
+                                                          const int32_t* __restrict__ counts,
+                                                          int32_t by_chunk) {
     __shared__ int wc[16];
     const int x = blockIdx.x;
     const int seeds = meta[2 * kGroups + 1 + x];
@@ -325,7 +332,11 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ til
             t = tiles[base + i];
             const int64_t r0 = bucket_off[t.c] + (int64_t)t.chunk * chunk_rows;
             const int64_t rows = min((int64_t)chunk_rows, bucket_off[t.c + 1] - r0);
-            heavy = 2 * rows * ((t.np + 31) / 32) >= full;
+            // by_chunk: the chunk's first query block decides for all its
+            // tiles, so the sibling tiles of a chunk stay adjacent in the
+            // queue (dequeued together: their row streams can meet in L2)
+            const int np = by_chunk ? min(QB, counts[t.c]) : t.np;
+            heavy = 2 * rows * ((np + 31) / 32) >= full;
         }
         const uint64_t mh = __ballot(i < n && heavy), ml = __ballot(i < n && !heavy);
         if (lane == 0) wc[w] = __popcll(mh);
@@ -2334,7 +2345,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
     if (!nearest_first && env_config().scan_order != 0) {
         hipLaunchKernelGGL(tile_order_kernel, dim3(ng), dim3(1024), 0, s, tiles, (Tile*)(ws + w.tiles_tmp),
-                           meta, idx->bucket_off, idx->chunk_rows, QB);
+                           meta, idx->bucket_off, idx->chunk_rows, QB, counts,
+                           env_config().scan_order == 2 ? 1 : 0);
         LMI_LAUNCH_CHECK("tile_order_kernel");
     }
     if (nearest_first) {
