@@ -292,10 +292,6 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager step (every launch from the host) instead of the "
                          "HIP-graph replay of the captured step")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="replay one graph per step and wait for each answer before the next "
-                         "(default: two graphs in turn, each answer's D2H on a copy stream while "
-                         "the next batch's kernels run; Searcher.pipeline)")
     ap.add_argument("--dist", default="f32", choices=["f32", "f64"],
                     help="distance arithmetic of the headline line: f32 = the reference's on "
                          "float32 DataFrames (the synthetic corpus is float32 holding fp16-exact "
@@ -318,7 +314,6 @@ def main():
     lib = _lib.load()
 
     use_graph = not args.no_graph and (world == 1 or torch.distributed.get_backend() == "nccl")
-    serial_ms = {}
 
     def timed_graph(dist):
         """The step captured once as a HIP graph (Searcher.graph) and replayed:
@@ -327,57 +322,26 @@ def main():
         kernel's duration comes from HIP events around the same launches in K
         eager steps right after (outside the timed region; a kernel runs the
         same whichever way it is launched)."""
-        def clock(run_steps):
-            if world > 1:
-                torch.distributed.barrier()
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            o = run_steps()
-            torch.cuda.synchronize()
-            if world > 1:
-                torch.distributed.barrier()
-            e = time.perf_counter() - t0
-            if world > 1:
-                t = torch.tensor([e], dtype=torch.float64, device=device)
-                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-                e = float(t.item())
-            return e, (o[0].copy(), o[1].copy())
-
-        # serial: one graph, each answer waited for before the next replay
         gs = searcher.graph(qn, q, args.R, k=args.k, dist=dist)
+        out = None
         for _ in range(args.warmup):
-            gs.run()
-
-        def serial():
-            o = None
-            for _ in range(args.steps):
-                o = gs.run()
-            return o
-
-        el_serial, out = clock(serial)
+            out = gs.run()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = gs.run()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        out = (out[0].copy(), out[1].copy())
         del gs
-        el = el_serial
-        if not args.no_pipeline:
-            # pipelined: K batches in flight two at a time (every answer
-            # collected on the host inside the timed region)
-            pl = searcher.pipeline(qn, q, args.R, k=args.k, dist=dist, depth=2)
-            for _ in range(args.warmup):
-                pl.result(pl.submit())
-
-            def pipelined():
-                o = None
-                first = pl.n
-                for i in range(args.steps):
-                    if i >= 2:
-                        o = pl.result(first + i - 2)
-                    pl.submit()
-                for j in range(max(0, args.steps - 2), args.steps):
-                    o = pl.result(first + j)
-                return o
-
-            el, out = clock(pipelined)
-            del pl
-        serial_ms[dist] = el_serial / args.steps * 1e3
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
         lib.lmi_timing_read(None, 0)
         lib.lmi_timing_enable(1)
         for _ in range(args.steps):
@@ -491,10 +455,7 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
         "recall_sample": sample, "breakdown_ms": breakdown,
-        "dist": args.dist,
-        "step": ("eager launches" if not use_graph else "hip-graph replay" if args.no_pipeline else
-                 "hip-graph replays, 2 batches in flight (answer D2H on a copy stream)"),
-        "ms_per_step_serial": round(serial_ms[args.dist], 3) if args.dist in serial_ms else None,
+        "dist": args.dist, "step": "hip-graph replay" if use_graph else "eager launches",
         "other_dist": {"dist": other, "value": round(args.nq / (el_o / args.steps), 1),
                        "ms_per_step": round(el_o / args.steps * 1e3, 3),
                        "scan_kernel_ms": round(scan_ms_o, 4),

@@ -26,6 +26,8 @@
 // followed by replay_out_kernel (ids through pos_to_id, uint32).
 #include "lmi_common.hpp"
 
+#include <type_traits>
+
 namespace lmi {
 namespace {
 
@@ -247,15 +249,37 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
         int32_t* U = nU <= kUCap ? Ul : a.uraw + (size_t)g0 * kl_use;
         // entry-parallel: a list is sorted by distance with its empty entries
         // last, so "leading entries with d < thr" is a per-entry test
+        // (a popular category's group holds ~10^3 queries: kUL entries per
+        // lane with their dependent loads in flight together, not one
+        // latency chain per entry)
+        constexpr int kUL = 8;
         int nb_tot = 0;
-        for (int e = tid; e < nU; e += kTG) {
-            const int gi = g0 + e / kl_use, j = e - (e / kl_use) * kl_use;
-            const int q = G[gi];
-            const size_t o = ((size_t)q * a.R + a.r) * a.kl + j;
-            const int32_t pos = a.lists_p[o];
-            const bool rel = pos >= 0 && list_d(a, o) < a.thr[q];
-            U[e] = rel ? pos : INT32_MAX;
-            nb_tot += rel ? 1 : 0;
+        for (int e0 = tid; e0 < nU; e0 += kUL * kTG) {
+            int qv[kUL];
+            size_t ov[kUL];
+#pragma unroll
+            for (int u = 0; u < kUL; ++u) {
+                const int e = e0 + u * kTG;
+                const int gi = g0 + e / kl_use, j = e - (e / kl_use) * kl_use;
+                qv[u] = e < nU ? G[gi] : 0;
+                ov[u] = ((size_t)qv[u] * a.R + a.r) * a.kl + j;
+            }
+            int32_t pv[kUL];
+            double dv[kUL], tv[kUL];
+#pragma unroll
+            for (int u = 0; u < kUL; ++u) {
+                const bool in = e0 + u * kTG < nU;
+                pv[u] = in ? a.lists_p[ov[u]] : -1;
+                dv[u] = in ? list_d(a, ov[u]) : 0.0;
+                tv[u] = in ? a.thr[qv[u]] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kUL; ++u) {
+                const int e = e0 + u * kTG;
+                const bool rel = pv[u] >= 0 && dv[u] < tv[u];
+                if (e < nU) U[e] = rel ? pv[u] : INT32_MAX;
+                nb_tot += rel ? 1 : 0;
+            }
         }
         nb_tot = block_sum_g(nb_tot, sh);  // (its barriers publish U)
         if (nb_tot == 0) return;  // LearnedIndex.py:157-159
@@ -268,25 +292,37 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
         // (a global member among the smallest `want` is among its share's)
         const int lane = tid & 63, wv = tid >> 6;
         int prev = -1, cnt = 0;
-        constexpr int kUReg = kUCap / kTG;  // share entries a lane keeps in registers
-        if (nU <= kUReg * kTG) {
-            // the lane's share read once; the `want` rounds then run on registers
-            int uc[kUReg];
+        // the lane's share (<= NR entries) read once into registers, then the
+        // `want` rounds run on them; NR by the group's size (the compares of
+        // a round scale with it: 2 at the bench's groups of <= 253 queries,
+        // up to 16 for a popular category's 10^3 queries past the LDS staging)
+        auto sel = [&](auto nr) {
+            constexpr int NR = decltype(nr)::value;
+            int uc[NR];
 #pragma unroll
-            for (int i = 0; i < kUReg; ++i) {
+            for (int i = 0; i < NR; ++i) {
                 const int e = wv * 64 + lane + i * kTG;
                 uc[i] = e < nU ? U[e] : INT32_MAX;
             }
             for (; cnt < want; ++cnt) {
                 int m = INT32_MAX;
 #pragma unroll
-                for (int i = 0; i < kUReg; ++i)
+                for (int i = 0; i < NR; ++i)
                     if (uc[i] > prev && uc[i] < m) m = uc[i];
                 m = wave_min_i(m);
                 if (m == INT32_MAX) break;
                 if (lane == 0) Sw[wv][cnt] = m;
                 prev = m;
             }
+        };
+        if (nU <= 2 * kTG) {
+            sel(std::integral_constant<int, 2>{});
+        } else if (nU <= 4 * kTG) {
+            sel(std::integral_constant<int, 4>{});
+        } else if (nU <= 8 * kTG) {
+            sel(std::integral_constant<int, 8>{});
+        } else if (nU <= 16 * kTG) {
+            sel(std::integral_constant<int, 16>{});
         } else {
             for (; cnt < want; ++cnt) {
                 int m = INT32_MAX;
@@ -303,25 +339,36 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
         if (lane == 0) nsw[wv] = cnt;
         __syncthreads();
         if (wv == 0) {
-            constexpr int NV = (kTG / 64) * (2 * kMaxKr) / 64;
-            int v[NV];
+            // the 16 wave lists (<= want entries each) packed want-major over
+            // the lanes: NV registers per lane for 16 * want entries
+            auto mrg = [&](auto nv) {
+                constexpr int NV = decltype(nv)::value;
+                int v[NV];
 #pragma unroll
-            for (int t = 0; t < NV; ++t) {
-                const int e = lane + 64 * t, w = e / (2 * kMaxKr), i = e % (2 * kMaxKr);
-                v[t] = (i < nsw[w]) ? Sw[w][i] : INT32_MAX;
-            }
-            int pv = -1, n = 0;
-            for (; n < want; ++n) {
-                int m = INT32_MAX;
+                for (int t = 0; t < NV; ++t) {
+                    const int e = lane + 64 * t, w = e / want, i = e - w * want;
+                    v[t] = (w < kTG / 64 && i < nsw[w]) ? Sw[w][i] : INT32_MAX;
+                }
+                int pv = -1, n = 0;
+                for (; n < want; ++n) {
+                    int m = INT32_MAX;
 #pragma unroll
-                for (int t = 0; t < NV; ++t)
-                    if (v[t] > pv && v[t] < m) m = v[t];
-                m = wave_min_i(m);
-                if (m == INT32_MAX) break;
-                if (lane == 0) S[n] = m;
-                pv = m;
-            }
-            if (lane == 0) nsw[kTG / 64] = n;
+                    for (int t = 0; t < NV; ++t)
+                        if (v[t] > pv && v[t] < m) m = v[t];
+                    m = wave_min_i(m);
+                    if (m == INT32_MAX) break;
+                    if (lane == 0) S[n] = m;
+                    pv = m;
+                }
+                if (lane == 0) nsw[kTG / 64] = n;
+            };
+            static_assert((kTG / 64) * (2 * kMaxKr) <= 16 * 64, "merge registers");
+            if ((kTG / 64) * want <= 4 * 64)
+                mrg(std::integral_constant<int, 4>{});
+            else if ((kTG / 64) * want <= 8 * 64)
+                mrg(std::integral_constant<int, 8>{});
+            else
+                mrg(std::integral_constant<int, 16>{});
         }
         __syncthreads();
         const int ns = nsw[kTG / 64];
@@ -333,13 +380,31 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
             // normal case: B_q then the smallest members of U not in B_q;
             // B_q entry-parallel (U holds its positions), then per query the
             // fillers, membership tested against its U row
-            for (int e = tid; e < nU; e += kTG) {
-                const int32_t p = U[e];
-                if (p == INT32_MAX) continue;
-                const int gi = g0 + e / kl_use, j = e - (e / kl_use) * kl_use;
-                const int q = G[gi];
-                a.dr_d[(size_t)q * kr + j] = list_d(a, ((size_t)q * a.R + a.r) * a.kl + j);
-                a.dr_p[(size_t)q * kr + j] = p;
+            for (int e0 = tid; e0 < nU; e0 += kUL * kTG) {
+                int32_t pv[kUL];
+                int qv[kUL];
+#pragma unroll
+                for (int u = 0; u < kUL; ++u) {
+                    const int e = e0 + u * kTG;
+                    pv[u] = e < nU ? U[e] : INT32_MAX;
+                    const int gi = g0 + e / kl_use;
+                    qv[u] = pv[u] != INT32_MAX ? G[gi] : 0;
+                }
+                double dv[kUL];
+#pragma unroll
+                for (int u = 0; u < kUL; ++u) {
+                    const int e = e0 + u * kTG;
+                    const int j = e - (e / kl_use) * kl_use;
+                    dv[u] = pv[u] != INT32_MAX ? list_d(a, ((size_t)qv[u] * a.R + a.r) * a.kl + j) : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kUL; ++u) {
+                    if (pv[u] == INT32_MAX) continue;
+                    const int e = e0 + u * kTG;
+                    const int j = e - (e / kl_use) * kl_use;
+                    a.dr_d[(size_t)qv[u] * kr + j] = dv[u];
+                    a.dr_p[(size_t)qv[u] * kr + j] = pv[u];
+                }
             }
             for (int gi = g0 + tid; gi < g1; gi += kTG) {
                 const int q = G[gi];
@@ -400,12 +465,21 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
         if (n >= kr) {
             for (int gi = g0 + tid; gi < g1; gi += kTG) {
                 const int q = G[gi];
-                for (int j = 0; j < kr; ++j) {
-                    double d;
-                    int32_t pos;
-                    list_at(a, q, j, d, pos);
-                    a.dr_d[(size_t)q * kr + j] = d;
-                    a.dr_p[(size_t)q * kr + j] = pos;
+                // 8 entries' loads in flight before their stores (the stores
+                // may alias the lists for the compiler: one chain per entry)
+                for (int j0 = 0; j0 < kr; j0 += 8) {
+                    double dv[8];
+                    int32_t pv[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (j0 + u < kr) list_at(a, q, j0 + u, dv[u], pv[u]);
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        if (j0 + u < kr) {
+                            a.dr_d[(size_t)q * kr + j0 + u] = dv[u];
+                            a.dr_p[(size_t)q * kr + j0 + u] = pv[u];
+                        }
+                    }
                 }
             }
         } else {

@@ -81,7 +81,11 @@ struct ScanArgs {
 // ---------------------------------------------------------------------------
 // prep
 // ---------------------------------------------------------------------------
-template <bool F16>
+// One wave per query (4 per workgroup: a latency-bound pass over 30 MB at
+// 10k queries; round 1's 256-thread workgroup per query took 19 us, most of
+// it workgroup launch and block reductions): each lane takes runs of 4
+// consecutive elements, float4 loads when the rows allow (VEC).
+template <bool F16, bool VEC>
 __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict__ q, int32_t nq,
                                                         int32_t ldq, int32_t d, int32_t d_pad,
                                                         void* __restrict__ qbuf,
@@ -91,38 +95,49 @@ __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict_
                                                         int32_t* __restrict__ out_pos,
                                                         int32_t* __restrict__ out_row,
                                                         int32_t out_per_q) {
-    __shared__ float red[kThreads / 64];
-    const int row = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= nq) return;  // (wave-uniform; no block-wide barrier below)
     const float* src = q + (size_t)row * ldq;
     float ss = 0.0f;
     bool inexact = false;
-    for (int c = tid; c < d_pad; c += kThreads) {
-        const float v = (c < d) ? src[c] : 0.0f;
-        ss = fmaf(v, v, ss);
-        if constexpr (F16) {
-            const _Float16 h = (_Float16)v;
-            inexact |= ((float)h != v);
-            reinterpret_cast<_Float16*>(qbuf)[(size_t)row * d_pad + c] = h;
+    for (int c0 = 4 * lane; c0 < d_pad; c0 += 256) {  // d_pad is a multiple of 32
+        float v[4];
+        if (VEC && c0 + 3 < d) {
+            const float4 f = *reinterpret_cast<const float4*>(src + c0);
+            v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
         } else {
-            reinterpret_cast<float*>(qbuf)[(size_t)row * d_pad + c] = v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (c0 + e < d) ? src[c0 + e] : 0.0f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ss = fmaf(v[e], v[e], ss);
+        if constexpr (F16) {
+            _Float16 h[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                h[e] = (_Float16)v[e];
+                inexact |= ((float)h[e] != v[e]);
+            }
+            uint2 pk;
+            pk.x = (uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16);
+            pk.y = (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16);
+            *reinterpret_cast<uint2*>(reinterpret_cast<_Float16*>(qbuf) + (size_t)row * d_pad + c0) = pk;
+        } else {
+            *reinterpret_cast<float4*>(reinterpret_cast<float*>(qbuf) + (size_t)row * d_pad + c0) =
+                make_float4(v[0], v[1], v[2], v[3]);
         }
     }
-    // wave + block reduction of the squared norm
     for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-    if ((tid & 63) == 0) red[tid >> 6] = ss;
     if constexpr (F16) {
-        if (__any(inexact) && (tid & 63) == 0) atomicOr(status, LMI_STATUS_QUERY_NOT_F16);
+        if (__any(inexact) && lane == 0) atomicOr(status, LMI_STATUS_QUERY_NOT_F16);
     }
-    __syncthreads();
-    if (tid == 0) {
-        float t = 0.0f;
-        for (int w = 0; w < kThreads / 64; ++w) t += red[w];
-        const float n = sqrtf(t);
+    if (lane == 0) {
+        const float n = sqrtf(ss);
         // sklearn _handle_zeros_in_scale: norms < 10*eps are replaced by 1
         invq[row] = (n < 10.0f * 1.1920929e-07f) ? 1.0f : 1.0f / n;
     }
-    for (int e = tid; e < out_per_q; e += kThreads) {
+    for (int e = lane; e < out_per_q; e += 64) {
         out_d[(size_t)row * out_per_q + e] = __builtin_inff();
         out_pos[(size_t)row * out_per_q + e] = -1;
         if (out_row) out_row[(size_t)row * out_per_q + e] = -1;
@@ -1005,6 +1020,8 @@ __global__ __launch_bounds__(kThreads, 1) void scan2_kernel(Scan2Args a) {
         {
             const int q = live ? a.pair_q[pp] / a.R : 0;
             const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
+            // (dead columns keep query 0's fragments here: zeroing them as
+            // scan v3 does broke this kernel's KL = 16 lists on gfx950)
 #pragma unroll
             for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
         }
@@ -1540,8 +1557,13 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 }
             }
             const half8* qrow = reinterpret_cast<const half8*>(a.qbuf + (size_t)q * D) + h;
+            // dead columns of a partial wave multiply zeros: their results
+            // are never read, and zero operands draw less MFMA power (the
+            // chip holds a power-limited clock under this kernel; diagnostic
+            // ABL 57: query 0's fragments, round 1's)
+            const half8 z{};
 #pragma unroll
-            for (int s = 0; s < NQF; ++s) qf[s] = qrow[2 * s];
+            for (int s = 0; s < NQF; ++s) qf[s] = (live || ABL == 57) ? qrow[2 * s] : z;
             // dead slots (and exhausted pairs) reject everything
             thr = live && !done ? (uint32_t)(a.thr_g[pp] >> 32) : 0u;
             my_invq = live ? a.invq[q] : 0.0f;
@@ -1894,11 +1916,23 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     // ascending global position (the index layout guarantees it), so mapping
     // each key to (distance, global position) keeps the list ordered, and the
     // merge across chunks is by the reference's (distance, g.index) order.
+    // (software-pipelined: chunk j+1's keys load while chunk j's positions
+    // are gathered, one memory latency per chunk instead of two)
+    uint64_t Kn[KL];
+    {
+        const uint64_t* src = partial + (size_t)pp * max_chunks * KL;
+#pragma unroll
+        for (int i = 0; i < KL; ++i) Kn[i] = nch > 0 ? src[i] : kEmptyKey;
+    }
     for (int j = 0; j < nch; ++j) {
-        const uint64_t* src = partial + ((size_t)pp * max_chunks + j) * KL;
         uint64_t K[KL];
 #pragma unroll
-        for (int i = 0; i < KL; ++i) K[i] = src[i];
+        for (int i = 0; i < KL; ++i) K[i] = Kn[i];
+        if (j + 1 < nch) {
+            const uint64_t* src = partial + ((size_t)pp * max_chunks + j + 1) * KL;
+#pragma unroll
+            for (int i = 0; i < KL; ++i) Kn[i] = src[i];
+        }
         int32_t g[KL];
 #pragma unroll
         for (int i = 0; i < KL; ++i) {
@@ -2178,6 +2212,7 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 51) return launch_scan3_v<KL, 51>(b, s);
     if (abl == 52) return launch_scan3_v<KL, 52>(b, s);
     if (abl == 53) return launch_scan3_v<KL, 53>(b, s);
+    if (abl == 57) return launch_scan3_v<KL, 57>(b, s);
     if (abl == 61) return launch_scan3_v<KL, 61>(b, s);
     if (abl == 62) return launch_scan3_v<KL, 62>(b, s);
     if (abl == 64) return launch_scan3_v<KL, 64>(b, s);
@@ -2313,14 +2348,14 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const int P = nq * R;
     const int KL = pick_kl(idx, qmode, k);
 
-    if (f16math) {
-        hipLaunchKernelGGL(prep_kernel<true>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
-                           idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
-                           out_pos, out_row, prefill ? R * ldo : 0);
-    } else {
-        hipLaunchKernelGGL(prep_kernel<false>, dim3(nq), dim3(kThreads), 0, s, q, nq, ldq, idx->d,
-                           idx->d_pad, (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d,
-                           out_pos, out_row, prefill ? R * ldo : 0);
+    {
+        const dim3 pg((nq + kThreads / 64 - 1) / (kThreads / 64));
+        const bool vec = ((uintptr_t)q % 16 == 0) && (ldq % 4 == 0);
+        auto* kp = f16math ? (vec ? prep_kernel<true, true> : prep_kernel<true, false>)
+                           : (vec ? prep_kernel<false, true> : prep_kernel<false, false>);
+        hipLaunchKernelGGL(kp, pg, dim3(kThreads), 0, s, q, nq, ldq, idx->d, idx->d_pad,
+                           (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d, out_pos,
+                           out_row, prefill ? R * ldo : 0);
     }
     LMI_LAUNCH_CHECK("prep_kernel");
     if (idx->n_rows == 0) return LMI_OK;

@@ -610,12 +610,6 @@ class Searcher:
         search(..., semantics="reference", replay_on="device")."""
         return GraphedSearch(self, q_nav, q_search, R, k, **kw)
 
-    def pipeline(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "PipelinedSearch":
-        """Batches streamed through `depth` (default 2) captured step graphs,
-        each answer's D2H overlapping the next batch's kernels
-        (PipelinedSearch)."""
-        return PipelinedSearch(self, q_nav, q_search, R, k, **kw)
-
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
                use_threshold: bool = True, classes: Optional[torch.Tensor] = None,
                timings: Optional[dict] = None, replay_on: str = "device",
@@ -788,8 +782,7 @@ class GraphedSearch:
     until the next run (copy them to keep them)."""
 
     def __init__(self, searcher: "Searcher", q_nav: torch.Tensor, q_search: torch.Tensor, R: int,
-                 k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 d2h: bool = True):
+                 k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32"):
         s = searcher
         dev = s.index.device
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
@@ -820,28 +813,21 @@ class GraphedSearch:
                 rd, ra, st, rst = step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        self.d2h = d2h
-        if d2h:
-            self.h_d = torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True)
-            self.h_a = torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True)
-            self.h_st = torch.zeros((2,), dtype=torch.int32, pin_memory=True)
+        self.h_d = torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True)
+        self.h_a = torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True)
+        self.h_st = torch.zeros((2,), dtype=torch.int32, pin_memory=True)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             rd, ra, st, rst = step()
-            if d2h:
-                self.h_d.copy_(rd, non_blocking=True)
-                self.h_a.copy_(ra, non_blocking=True)
-                self.h_st[0:1].copy_(st, non_blocking=True)
-                self.h_st[1:2].copy_(rst, non_blocking=True)
-        # the graph's device outputs (its private pool keeps them at these
-        # addresses for every replay)
+            self.h_d.copy_(rd, non_blocking=True)
+            self.h_a.copy_(ra, non_blocking=True)
+            self.h_st[0:1].copy_(st, non_blocking=True)
+            self.h_st[1:2].copy_(rst, non_blocking=True)
         self._keep = (rd, ra, st, rst)
         torch.cuda.synchronize(dev)
 
     def run(self):
         """Replay the step -> (dists f64 [nq, w], anns uint32 [nq, w])."""
-        if not self.d2h:
-            raise ValueError("captured without the D2H (d2h=False): use PipelinedSearch")
         dev = self.searcher.index.device
         self.graph.replay()
         torch.cuda.current_stream(dev).synchronize()
@@ -855,89 +841,3 @@ class GraphedSearch:
                                         k_round=self.k_round, use_threshold=self.use_threshold,
                                         dist=self.dist)
         return self.h_d.numpy(), self.h_a.numpy().view(np.uint32)
-
-
-class PipelinedSearch:
-    """A stream of query batches through the captured step, pipelined: `depth`
-    step graphs (GraphedSearch without the D2H, each with its own device
-    outputs) replayed in turn on the compute stream, each answer's D2H on a
-    copy stream of its own.  Batch i+1's kernels start while batch i's answer
-    crosses PCIe and while the host collects it, so neither the copy nor the
-    host's turn-around sits between two steps' kernels.  Every collective
-    (G > 1) stays on the one compute stream, in the same order on every rank.
-
-        p = searcher.pipeline(q_nav, q_search, R)
-        t0 = p.submit(); t1 = p.submit(); d, a = p.result(t0); ...
-
-    A ticket's arrays are views of pinned buffers, valid until `depth` more
-    batches have been submitted (copy them to keep them).  The graphs read the
-    query tensors they were captured with: write the next batch into `q_nav` /
-    `q_search` (on the compute stream) before its submit.  A batch that is not
-    fp16-exact under an fp16 capture, or an internal status, is reported by
-    `result` as GraphedSearch.run reports it (the eager path answers the
-    former)."""
-
-    def __init__(self, searcher: "Searcher", q_nav, q_search, R: int, k: int = 10, *,
-                 k_round: int = 10, use_threshold: bool = True, dist: str = "f32", depth: int = 2):
-        if depth < 1:
-            raise ValueError("depth must be >= 1")
-        dev = searcher.index.device
-        self.searcher, self.R, self.k, self.k_round = searcher, R, k, k_round
-        self.use_threshold, self.dist = use_threshold, dist
-        g0 = GraphedSearch(searcher, q_nav, q_search, R, k, k_round=k_round,
-                           use_threshold=use_threshold, dist=dist, d2h=False)
-        self.q_nav, self.q_search = g0.q_nav, g0.q_search
-        self.graphs = [g0] + [GraphedSearch(searcher, self.q_nav, self.q_search, R, k, k_round=k_round,
-                                            use_threshold=use_threshold, dist=dist, d2h=False)
-                              for _ in range(depth - 1)]
-        rd, ra = g0._keep[0], g0._keep[1]
-        self.h_d = [torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True) for _ in range(depth)]
-        self.h_a = [torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True) for _ in range(depth)]
-        self.h_st = [torch.zeros((2,), dtype=torch.int32, pin_memory=True) for _ in range(depth)]
-        self.copy_stream = torch.cuda.Stream(dev)
-        self.ready = [torch.cuda.Event() for _ in range(depth)]
-        self.copied = [torch.cuda.Event() for _ in range(depth)]
-        self.n = 0
-        self.done = 0
-
-    def submit(self) -> int:
-        """Enqueue one step (no host wait unless a slot's previous answer has
-        not been collected) -> its ticket."""
-        t = self.n
-        slot = t % len(self.graphs)
-        if t - self.done >= len(self.graphs):
-            raise RuntimeError("pipeline full: collect the oldest ticket with result() first")
-        dev = self.searcher.index.device
-        main = torch.cuda.current_stream(dev)
-        g = self.graphs[slot]
-        main.wait_event(self.copied[slot])  # the slot's previous answer has left its buffers
-        g.graph.replay()
-        self.ready[slot].record(main)
-        rd, ra, st, rst = g._keep
-        self.copy_stream.wait_event(self.ready[slot])
-        with torch.cuda.stream(self.copy_stream):
-            self.h_d[slot].copy_(rd, non_blocking=True)
-            self.h_a[slot].copy_(ra, non_blocking=True)
-            self.h_st[slot][0:1].copy_(st, non_blocking=True)
-            self.h_st[slot][1:2].copy_(rst, non_blocking=True)
-        self.copied[slot].record(self.copy_stream)
-        self.n += 1
-        return t
-
-    def result(self, ticket: int):
-        """Wait for a ticket's answer -> (dists f64 [nq, w], anns uint32 [nq, w]).
-        Tickets are collected in submission order."""
-        if ticket != self.done:
-            raise ValueError(f"collect tickets in order (next is {self.done})")
-        slot = ticket % len(self.graphs)
-        self.copied[slot].synchronize()
-        self.done += 1
-        st, rst = int(self.h_st[slot][0]), int(self.h_st[slot][1])
-        if st & _lib.LMI_STATUS_INTERNAL or rst:
-            raise RuntimeError(f"search: internal status {st}/{rst}")
-        if st & _lib.LMI_STATUS_QUERY_NOT_F16:
-            self.searcher._qcheck = None
-            return self.searcher.search(self.q_nav, self.q_search, self.R, k=self.k,
-                                        k_round=self.k_round, use_threshold=self.use_threshold,
-                                        dist=self.dist)
-        return self.h_d[slot].numpy(), self.h_a[slot].numpy().view(np.uint32)

@@ -51,50 +51,3 @@ def test_graph_new_batch_and_inexact_queries(setup):
     d3, a3 = s.search(g.q_nav, g.q_search, 4, k=10)
     np.testing.assert_array_equal(d2, d3)
     np.testing.assert_array_equal(a2, a3)
-
-
-@pytest.mark.parametrize("dist,depth", [("f32", 2), ("f64", 2), ("f32", 3)])
-def test_pipeline_batches_in_flight(setup, dist, depth):
-    """PipelinedSearch: several batches in flight (different queries per
-    batch, written into the capture's query buffers on the compute stream
-    between submits); every ticket's answer equals the eager search of its
-    own batch."""
-    w, s = setup
-    qn = torch.from_numpy(w["qn"]).cuda()
-    q = torch.from_numpy(w["q"]).cuda()
-    p = s.pipeline(qn.clone(), q.clone(), 4, k=10, dist=dist, depth=depth)
-    g = torch.Generator().manual_seed(3)
-    perms = [torch.randperm(q.shape[0], generator=g).cuda() for _ in range(7)]
-    want = [s.search(qn[pm], q[pm], 4, k=10, dist=dist) for pm in perms]
-    got, tickets = [], []
-    for i, pm in enumerate(perms):
-        if i >= depth:
-            t = tickets.pop(0)
-            d, a = p.result(t)
-            got.append((d.copy(), a.copy()))
-        p.q_nav.copy_(qn[pm])
-        p.q_search.copy_(q[pm])
-        tickets.append(p.submit())
-    for t in tickets:
-        d, a = p.result(t)
-        got.append((d.copy(), a.copy()))
-    assert len(got) == len(want)
-    for (d1, a1), (d0, a0) in zip(got, want):
-        np.testing.assert_array_equal(d1, d0)
-        np.testing.assert_array_equal(a1, a0)
-
-
-def test_pipeline_order_and_capacity(setup):
-    w, s = setup
-    qn = torch.from_numpy(w["qn"]).cuda()
-    q = torch.from_numpy(w["q"]).cuda()
-    p = s.pipeline(qn, q, 4, k=10, depth=2)
-    t0, t1 = p.submit(), p.submit()
-    with pytest.raises(RuntimeError):
-        p.submit()  # both slots hold uncollected answers
-    with pytest.raises(ValueError):
-        p.result(t1)  # out of order
-    d0, a0 = p.result(t0)
-    d1, a1 = p.result(t1)
-    np.testing.assert_array_equal(d0, d1)
-    np.testing.assert_array_equal(a0, a1)

@@ -103,14 +103,17 @@ def test_device_replay_on_real_lists_reaches_every_branch(seed):
 
 
 @pytest.mark.parametrize("use_threshold", [True, False])
-def test_device_replay_large_groups(use_threshold):
+@pytest.mark.parametrize("nq,C", [(6000, 5), (2500, 4), (12000, 3)])
+def test_device_replay_large_groups(use_threshold, nq, C):
     """Groups whose relevant positions exceed the kernel's LDS staging
     (kUCap = 8192 entries) take the global-scratch path; small ones in the
-    same launch stay in LDS."""
-    classes, d, pos, size, ids = _random_lists(21, nq=6000, R=3, C=5, kl=10, tiny=(4,))
+    same launch stay in LDS.  Selection runs from registers up to 16384
+    entries (thresholded rounds of nq=2500, C=4: 9.4K-14.4K), from the
+    global share beyond (nq=6000, C=5: 19K-25K; nq=12000, C=3: up to 74K)."""
+    classes, d, pos, size, ids = _random_lists(21, nq=nq, R=3, C=C, kl=10, tiny=(C - 1,))
     ref_d, ref_a = replay(classes, d, pos, k_round=10, k_final=10, bucket_size=size,
                           pos_to_id=ids, use_threshold=use_threshold)
-    assert np.bincount(classes[:, 1], minlength=5).max() * 10 > 8192
+    assert np.bincount(classes[:, 1], minlength=C).max() * 10 > 8192
     dev = torch.device("cuda")
     dd, aa, st = replay_device(torch.from_numpy(classes).to(dev), torch.from_numpy(d).to(dev),
                                torch.from_numpy(pos).to(dev), k_round=10, k_final=10,

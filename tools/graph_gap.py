@@ -25,8 +25,6 @@ ap.add_argument("--R", type=int, default=4)
 ap.add_argument("--steps", type=int, default=30)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--trace", default=None)
-ap.add_argument("--pipeline", type=int, default=0,
-                help="batches in flight (Searcher.pipeline depth); 0 = one graph, synchronised per step")
 a = ap.parse_args()
 
 if a.trace:
@@ -63,18 +61,8 @@ labels = router.argmax(xn)
 del xn
 ix = DeviceIndex(x, labels, 122, chunk_rows=8192)
 del x
-if a.pipeline:
-    pl = Searcher(ix, router).pipeline(qn, q, a.R, k=10, depth=a.pipeline)
-    n = a.warmup + a.steps
-    for i in range(n):
-        if i >= a.pipeline:
-            pl.result(i - a.pipeline)
-        pl.submit()
-    for j in range(max(0, n - a.pipeline), n):
-        pl.result(j)
-else:
-    gs = Searcher(ix, router).graph(qn, q, a.R, k=10)
-    for _ in range(a.warmup + a.steps):
-        gs.run()
+gs = Searcher(ix, router).graph(qn, q, a.R, k=10)
+for _ in range(a.warmup + a.steps):
+    gs.run()
 torch.cuda.synchronize()
 print("done", flush=True)

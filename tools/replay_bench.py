@@ -33,10 +33,31 @@ def _random_lists(seed, nq, R, C, kl):
     return classes, d, pos, size, ids
 
 
-classes, d, pos, size, ids = _random_lists(3, nq=10000, R=4, C=122, kl=10)
 dev = torch.device("cuda")
-args = [torch.from_numpy(x).to(dev) for x in (classes, d, pos)]
-bsz, p2id = torch.from_numpy(size).to(dev), torch.from_numpy(ids).to(dev)
+if "--bench-lists" in sys.argv:
+    # the bench's own 10M workload: its router classes and K2 lists
+    from li import synth
+    from li.index import DeviceIndex, DeviceRouter, bucket_topk
+    x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
+    router = DeviceRouter(layers)
+    labels = router.argmax(xn)
+    del xn
+    ix = DeviceIndex(x, labels, 122, chunk_rows=8192)
+    del x
+    cls_t, _ = router.topr(qn, 4)
+    ld, lp, _ = bucket_topk(ix, q, cls_t, 10)
+    args = [cls_t, ld, lp]
+    bsz = torch.from_numpy(np.ascontiguousarray(ix.bucket_size, dtype=np.int64)).to(dev)
+    p2id = torch.from_numpy(np.ascontiguousarray(ix.pos_to_id, dtype=np.int64)).to(dev)
+    cl = cls_t.cpu().numpy()
+    for r in range(cl.shape[1]):
+        bc = np.bincount(cl[:, r], minlength=122)
+        print(f"round {r}: group sizes max {bc.max()} p99 {np.percentile(bc, 99):.0f} "
+              f"median {np.median(bc):.0f}; groups > 819 queries: {(bc > 819).sum()}", flush=True)
+else:
+    classes, d, pos, size, ids = _random_lists(3, nq=10000, R=4, C=122, kl=10)
+    args = [torch.from_numpy(x).to(dev) for x in (classes, d, pos)]
+    bsz, p2id = torch.from_numpy(size).to(dev), torch.from_numpy(ids).to(dev)
 for abl in (os.environ.get("ABLS", "0").split(",")):
     os.environ["LMI_REPLAY_ABL"] = abl
     _lib.load().lmi_config_reload()
