@@ -1252,6 +1252,10 @@ __device__ __forceinline__ f32x16 mfma_last_v(const f32x16& c, const half8& a, c
                  : "+v"(d) : "v"(a), "v"(b));
     return d;
 }
+// (diagnostic ABL 66 / 68: the 16x16x32 shape, timing only)
+__device__ __forceinline__ void mfma16_v(f32x4& c, const half8& a, const half8& b) {
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+}
 // (diagnostic ABL 61: the wait at the epilogue instead)
 __device__ __forceinline__ f32x16 mfma_drain_v(const f32x16& c) {
     f32x16 d = c;
@@ -1443,10 +1447,14 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     constexpr int kAux = ABL == 33 ? 2 : 0;
     constexpr bool kDmaOnly = ABL == 2 || ABL == 32;
     constexpr bool kL2Src = ABL == 31 || ABL == 32;
-    constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6;
-    constexpr bool kNoEpi = kDmaOnly || ABL == 5 || ABL == 6;
+    // 66 = 6 with v_mfma_f32_16x16x32_f16 (same operand registers, same LDS
+    // bytes, 96 MFMAs of 16 cycles per wave-block: timing of the shape only),
+    // 67 = the full kernel without the epilogue, 68 = 67 with 16x16x32
+    constexpr bool kM16 = ABL == 66 || ABL == 68;
+    constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6 || ABL == 66;
+    constexpr bool kNoEpi = kDmaOnly || ABL == 5 || ABL == 6 || ABL == 66 || ABL == 67 || ABL == 68;
     constexpr bool kNoIns = ABL == 1 || ABL == 4;
-    constexpr bool kNoBar = ABL == 6 || ABL == 21;
+    constexpr bool kNoBar = ABL == 6 || ABL == 66 || ABL == 21;
     // bound exchange period in blocks (diagnostic: 40 none, 41 every 4, 42 every 8, 43 every 16)
     constexpr int kXch = ABL == 40 ? 0 : ABL == 41 ? 4 : ABL == 42 ? 8 : ABL == 43 ? 16 : 32;
     // (ABL 53, round 1's placement: an LDS-DMA issue holds its wave for ~45-60
@@ -1613,6 +1621,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         const uint32_t lane_off = (uint32_t)(((lane >> 1) & 15) * PIECEP + (lane & 1) * 16 + (lane >> 5) * 32);
 
         f32x16 acc;
+        f32x4 acc4[4] = {};  // (diagnostic 66 / 68 only)
         uint32_t xg_carry = 0xffffffffu;  // global bound fetched, not yet applied
         // ---- epilogue of block eb (accumulators of its 48 MFMAs in acc) ------
         auto epilogue = [&](int eb) {
@@ -1823,6 +1832,23 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 if (more && !kDmaHead)
                     for (int j = 0; j < NST; ++j) dma_stage(ws0 + j * STAGE, blk + 1, j);
             } else {
+            if constexpr (kM16) {
+#pragma unroll
+                for (int j = 0; j < NST; ++j) {
+                    const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
+#pragma unroll
+                    for (int kk = 0; kk < 8; ++kk) {
+                        const half8 a0 = *reinterpret_cast<const half8*>(rp + 64 * (2 * kk));
+                        const half8 a1 = *reinterpret_cast<const half8*>(rp + 64 * (2 * kk + 1));
+#pragma unroll
+                        for (int qt = 0; qt < 2; ++qt) {
+                            mfma16_v(acc4[2 * qt], a0, qf[j * 16 + 2 * kk + qt]);
+                            mfma16_v(acc4[2 * qt + 1], a1, qf[j * 16 + 2 * kk + qt]);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            } else
 #pragma unroll
             for (int j = 0; j < NST; ++j) {
                 const unsigned char* rp = ring + rs0 + j * STAGE + opaque_u(lane_off);
@@ -2213,6 +2239,9 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 52) return launch_scan3_v<KL, 52>(b, s);
     if (abl == 53) return launch_scan3_v<KL, 53>(b, s);
     if (abl == 57) return launch_scan3_v<KL, 57>(b, s);
+    if (abl == 66) return launch_scan3_v<KL, 66>(b, s);
+    if (abl == 67) return launch_scan3_v<KL, 67>(b, s);
+    if (abl == 68) return launch_scan3_v<KL, 68>(b, s);
     if (abl == 61) return launch_scan3_v<KL, 61>(b, s);
     if (abl == 62) return launch_scan3_v<KL, 62>(b, s);
     if (abl == 64) return launch_scan3_v<KL, 64>(b, s);
