@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 4
+#define LMI_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -183,6 +183,21 @@ int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx, 
 /* K3 on float64 lists: order (d64, pos). */
 int lmi_merge_topk_f64(const double* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
                        int32_t k, double* out_d, int32_t* out_pos, void* stream);
+
+/* ---- K3 over the all-gathered buffer, in place (ABI 5) ------------------ */
+/* A G-GPU search all-gathers one packed int32 buffer per rank instead of
+ * separate lists (li/dist.py): rank g's words start at gathered + g *
+ * rank_words and hold [distances: rows*k f32, or rows*k f64 as 2 words each]
+ * [positions: rows*k int32][the rank's lmi_bucket_topk status word], padded
+ * to rank_words (even, >= lmi_packed_rank_words; the buffer 8-byte aligned).
+ * lmi_merge_topk_packed merges the G lists as lmi_merge_topk(_f64) does and
+ * writes the OR of the G status words to out_status (device int32), so every
+ * rank sees every rank's bits; out_d is f32 or f64 [rows][k] by dist_f64.
+ * One launch replaces the unpacking copies and the per-rank status ORs. */
+int64_t lmi_packed_rank_words(int64_t rows, int32_t k, int32_t dist_f64);
+int lmi_merge_topk_packed(const int32_t* gathered, int32_t G, int64_t rank_words, int64_t rows,
+                          int32_t k, int32_t dist_f64, void* out_d, int32_t* out_pos,
+                          int32_t* out_status, void* stream);
 
 /* ---- host replay of the reference's multi-round merge ----------------- */
 /* Reproduces LearnedIndex.search (LearnedIndex.py:22-101) and search_single

@@ -8,26 +8,45 @@
 // identical for any G.
 #include "lmi_common.hpp"
 
+#include <algorithm>
+
 namespace lmi {
 namespace {
 
 constexpr int kThreads = 256;
 
+// Rank g's lists start at d_in + g * gs_d and pos_in + g * gs_p (elements):
+// [G][rows][k] arrays (gs = rows * k), or the all-gathered packed buffer of
+// lmi_merge_topk_packed read in place.  With st_in, thread 0 also writes the
+// OR of the G status words (rank g's at st_in + g * gs_st) to st_out.
+__device__ inline void or_status(const int32_t* st_in, int64_t gs_st, int32_t G,
+                                 int32_t* st_out) {
+    if (st_in == nullptr || blockIdx.x != 0 || threadIdx.x != 0) return;
+    int32_t v = 0;
+    for (int g = 0; g < G; ++g) v |= st_in[(size_t)g * gs_st];
+    *st_out = v;
+}
+
 template <int KL>
 __global__ __launch_bounds__(kThreads) void merge_kernel(const float* __restrict__ d_in,
                                                          const int32_t* __restrict__ pos_in,
                                                          int32_t G, int64_t rows, int32_t k,
+                                                         int64_t gs_d, int64_t gs_p,
+                                                         const int32_t* __restrict__ st_in,
+                                                         int64_t gs_st, int32_t* __restrict__ st_out,
                                                          float* __restrict__ out_d,
                                                          int32_t* __restrict__ out_pos) {
+    or_status(st_in, gs_st, G, st_out);
     const int64_t row = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (row >= rows) return;
     uint64_t M[KL];
     list_clear<KL>(M);
     for (int g = 0; g < G; ++g) {
-        const size_t base = ((size_t)g * rows + row) * k;
+        const float* dg = d_in + (size_t)g * gs_d + (size_t)row * k;
+        const int32_t* pg = pos_in + (size_t)g * gs_p + (size_t)row * k;
         for (int i = 0; i < k; ++i) {
-            const int32_t p = pos_in[base + i];
-            const uint64_t key = (p < 0) ? kEmptyKey : make_key(d_in[base + i], (uint32_t)p);
+            const int32_t p = pg[i];
+            const uint64_t key = (p < 0) ? kEmptyKey : make_key(dg[i], (uint32_t)p);
             if (key >= M[KL - 1]) break;  // each input list is ascending
             list_insert<KL>(M, key);
         }
@@ -47,8 +66,13 @@ template <int KL>
 __global__ __launch_bounds__(kThreads) void merge_f64_kernel(const double* __restrict__ d_in,
                                                              const int32_t* __restrict__ pos_in,
                                                              int32_t G, int64_t rows, int32_t k,
+                                                             int64_t gs_d, int64_t gs_p,
+                                                             const int32_t* __restrict__ st_in,
+                                                             int64_t gs_st,
+                                                             int32_t* __restrict__ st_out,
                                                              double* __restrict__ out_d,
                                                              int32_t* __restrict__ out_pos) {
+    or_status(st_in, gs_st, G, st_out);
     const int64_t row = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (row >= rows) return;
     double M[KL];
@@ -62,11 +86,12 @@ __global__ __launch_bounds__(kThreads) void merge_f64_kernel(const double* __res
         return a < b || (a == b && pa < pb);
     };
     for (int g = 0; g < G; ++g) {
-        const size_t base = ((size_t)g * rows + row) * k;
+        const double* dg = d_in + (size_t)g * gs_d + (size_t)row * k;
+        const int32_t* pg = pos_in + (size_t)g * gs_p + (size_t)row * k;
         for (int i = 0; i < k; ++i) {
-            const int32_t p = pos_in[base + i];
+            const int32_t p = pg[i];
             if (p < 0) break;  // each input list is ascending, empties last
-            const double x = d_in[base + i];
+            const double x = dg[i];
             const uint32_t u = (uint32_t)p;
             if (!lt(x, u, M[KL - 1], Q[KL - 1])) break;
 #pragma unroll
@@ -95,6 +120,28 @@ __global__ __launch_bounds__(kThreads) void merge_f64_kernel(const double* __res
 }  // namespace
 }  // namespace lmi
 
+namespace lmi {
+namespace {
+int launch_merge(const void* d_in, const int32_t* pos_in, int32_t G, int64_t rows, int32_t k,
+                 bool f64, int64_t gs_d, int64_t gs_p, const int32_t* st_in, int64_t gs_st,
+                 int32_t* st_out, void* out_d, int32_t* out_pos, hipStream_t s) {
+    const dim3 grid((unsigned)std::max<int64_t>(1, (rows + kThreads - 1) / kThreads));
+    if (f64) {
+        auto* kp = k <= 10 ? merge_f64_kernel<10> : merge_f64_kernel<16>;
+        hipLaunchKernelGGL(kp, grid, dim3(kThreads), 0, s, (const double*)d_in, pos_in, G, rows, k,
+                           gs_d, gs_p, st_in, gs_st, st_out, (double*)out_d, out_pos);
+        LMI_LAUNCH_CHECK("merge_f64_kernel");
+    } else {
+        auto* kp = k <= 10 ? merge_kernel<10> : merge_kernel<16>;
+        hipLaunchKernelGGL(kp, grid, dim3(kThreads), 0, s, (const float*)d_in, pos_in, G, rows, k,
+                           gs_d, gs_p, st_in, gs_st, st_out, (float*)out_d, out_pos);
+        LMI_LAUNCH_CHECK("merge_kernel");
+    }
+    return LMI_OK;
+}
+}  // namespace
+}  // namespace lmi
+
 extern "C" int lmi_merge_topk_f64(const double* d_in, const int32_t* pos_in, int32_t G,
                                   int64_t rows, int32_t k, double* out_d, int32_t* out_pos,
                                   void* stream) {
@@ -103,16 +150,8 @@ extern "C" int lmi_merge_topk_f64(const double* d_in, const int32_t* pos_in, int
     LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
     if (rows == 0) return LMI_OK;
     LMI_CHECK_ARG(d_in && pos_in && out_d && out_pos, "null pointer");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid((unsigned)((rows + kThreads - 1) / kThreads));
-    if (k <= 10)
-        hipLaunchKernelGGL(merge_f64_kernel<10>, grid, dim3(kThreads), 0, s, d_in, pos_in, G, rows,
-                           k, out_d, out_pos);
-    else
-        hipLaunchKernelGGL(merge_f64_kernel<16>, grid, dim3(kThreads), 0, s, d_in, pos_in, G, rows,
-                           k, out_d, out_pos);
-    LMI_LAUNCH_CHECK("merge_f64_kernel");
-    return LMI_OK;
+    return launch_merge(d_in, pos_in, G, rows, k, true, rows * k, rows * k, nullptr, 0, nullptr,
+                        out_d, out_pos, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
@@ -122,14 +161,28 @@ extern "C" int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t 
     LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
     if (rows == 0) return LMI_OK;
     LMI_CHECK_ARG(d_in && pos_in && out_d && out_pos, "null pointer");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid((unsigned)((rows + kThreads - 1) / kThreads));
-    if (k <= 10)
-        hipLaunchKernelGGL(merge_kernel<10>, grid, dim3(kThreads), 0, s, d_in, pos_in, G, rows, k,
-                           out_d, out_pos);
-    else
-        hipLaunchKernelGGL(merge_kernel<16>, grid, dim3(kThreads), 0, s, d_in, pos_in, G, rows, k,
-                           out_d, out_pos);
-    LMI_LAUNCH_CHECK("merge_kernel");
-    return LMI_OK;
+    return launch_merge(d_in, pos_in, G, rows, k, false, rows * k, rows * k, nullptr, 0, nullptr,
+                        out_d, out_pos, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int64_t lmi_packed_rank_words(int64_t rows, int32_t k, int32_t dist_f64) {
+    const int64_t n = rows * k * (dist_f64 ? 3 : 2) + 1;
+    return (n + 1) & ~(int64_t)1;
+}
+
+extern "C" int lmi_merge_topk_packed(const int32_t* gathered, int32_t G, int64_t rank_words,
+                                     int64_t rows, int32_t k, int32_t dist_f64, void* out_d,
+                                     int32_t* out_pos, int32_t* out_status, void* stream) {
+    using namespace lmi;
+    LMI_CHECK_ARG(G >= 1 && rows >= 0, "bad G/rows");
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(rank_words >= lmi_packed_rank_words(rows, k, dist_f64) && rank_words % 2 == 0,
+                  "rank_words %lld < lmi_packed_rank_words() or odd", (long long)rank_words);
+    LMI_CHECK_ARG(gathered && out_status && (rows == 0 || (out_d && out_pos)), "null pointer");
+    LMI_CHECK_ARG(((uintptr_t)gathered & 7) == 0, "gathered buffer not 8-byte aligned");
+    const int64_t nd = rows * k * (dist_f64 ? 2 : 1);  // distance words per rank
+    return launch_merge(gathered, gathered + nd, G, rows, k, dist_f64 != 0,
+                        dist_f64 ? rank_words / 2 : rank_words, rank_words,
+                        gathered + nd + rows * k, rank_words, out_status, out_d, out_pos,
+                        reinterpret_cast<hipStream_t>(stream));
 }

@@ -54,6 +54,8 @@ EXPORTS = (
     "lmi_bucket_topk_f64",
     "lmi_refine_fallback_count",
     "lmi_merge_topk_f64",
+    "lmi_packed_rank_words",
+    "lmi_merge_topk_packed",
     "lmi_replay",
     "lmi_replay_f64",
     "lmi_replay_device_workspace_bytes",
@@ -89,7 +91,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class IndexDesc(C.Structure):
@@ -128,6 +130,8 @@ _SIGNATURES = {
     "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,
                                             _P]),
     "lmi_merge_topk_f64": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),
+    "lmi_packed_rank_words": (C.c_int64, [_I64, _I32, _I32]),
+    "lmi_merge_topk_packed": (C.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _P, _P, _P]),
     "lmi_replay": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64, _I32,
                              _P, _P, _P, _P]),
     "lmi_replay_f64": (C.c_int, [_P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32, _P, _I64,

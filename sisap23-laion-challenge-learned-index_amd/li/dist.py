@@ -6,8 +6,11 @@ and the per-(query, probe) top-k is recovered exactly by merging the G
 per-shard lists: top-k(union of shards) = top-k(union of per-shard top-k).
 The one exchange step is an all-gather of the lists (nq*R*k*8 bytes per rank,
 ~3.2 MB at 10k queries, R=4: latency-bound on xGMI), over RCCL
-(torch.distributed backend "nccl"), followed by K3 (lmi_merge_topk) on every
-rank.  Every rank ends up with the same classes.  Results are bitwise identical
+(torch.distributed backend "nccl"), followed by K3 on every rank.  The product
+path (Searcher) has K2 write each rank's lists and status word straight into
+one packed send buffer (packed_lists) and K3 read the gathered buffer in place
+(gather_merge_packed: lmi_merge_topk_packed); gather_merge is the general form
+(any merge callable, the CPU gloo tests).  Every rank ends up with the same classes.  Results are bitwise identical
 for any G because every list is ordered by (distance, global position).
 The router is sharded by queries (route_sharded): each rank routes nq/G queries
 and the classes are all-gathered (nq*R*4 bytes), so its cost shrinks with G;
@@ -96,6 +99,44 @@ def gather_merge(d: torch.Tensor, pos: torch.Tensor, k: int, group=None,
     st = got[2][0:1].clone()
     for g in range(1, got[2].shape[0]):
         st = torch.bitwise_or(st, got[2][g:g + 1])
+    return md, mp, st
+
+
+def packed_lists(rows: int, k: int, f64: bool, device):
+    """This rank's send buffer for gather_merge_packed and views of it:
+    (buf int32 [W], d [rows*k] f32/f64, pos [rows*k] int32, status [1] int32,
+    zeroed).  K2 writes its lists and status word straight into the views,
+    so the all-gather sends the buffer as it is (W = lmi_packed_rank_words)."""
+    from . import _lib
+    W = int(_lib.load().lmi_packed_rank_words(rows, k, int(bool(f64))))
+    buf = torch.empty((W,), dtype=torch.int32, device=device)
+    n = rows * k
+    nd = n * (2 if f64 else 1)
+    d = buf[:nd].view(torch.float64 if f64 else torch.float32)
+    pos = buf[nd:nd + n]
+    status = buf[nd + n:nd + n + 1]
+    status.zero_()
+    return buf, d, pos, status
+
+
+def gather_merge_packed(buf: torch.Tensor, rows: int, k: int, f64: bool, group=None):
+    """All-gather every rank's packed buffer (packed_lists) in one collective,
+    then K3 over the gathered buffer in place (lmi_merge_topk_packed): the
+    merged lists [rows, k] and the OR of every rank's status word, so all
+    ranks fail together.  Two launches at any G (gather_merge's unpacking
+    copies and per-rank status ORs are ~10 small kernels at G = 8)."""
+    from . import _lib
+    from .index import check, ptr
+    G = dist.get_world_size(group)
+    W = buf.numel()
+    out = torch.empty((G * W,), dtype=torch.int32, device=buf.device)
+    _all_gather(out, buf, group)
+    md = torch.empty((rows, k), dtype=torch.float64 if f64 else torch.float32, device=buf.device)
+    mp = torch.empty((rows, k), dtype=torch.int32, device=buf.device)
+    st = torch.empty((1,), dtype=torch.int32, device=buf.device)
+    check("lmi_merge_topk_packed", _lib.load().lmi_merge_topk_packed(
+        ptr(out), G, W, rows, k, int(bool(f64)), ptr(md), ptr(mp), ptr(st),
+        _lib.stream_handle(buf.device)))
     return md, mp, st
 
 

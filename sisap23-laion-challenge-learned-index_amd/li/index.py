@@ -384,8 +384,9 @@ class DeviceRouter:
 # scan / merge / replay
 # ---------------------------------------------------------------------------
 def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
-                qmode: Optional[int] = None, stream=None):
-    """K2 on one shard.  Returns (d [nq,R,k] f32, pos [nq,R,k] int32, status int32 tensor)."""
+                qmode: Optional[int] = None, stream=None, out=None):
+    """K2 on one shard.  Returns (d [nq,R,k] f32, pos [nq,R,k] int32, status int32 tensor);
+    `out` = such a triple to write into (the status word zeroed by the caller)."""
     lib = _lib.load()
     q = _as_torch(q, index.device, torch.float32)
     classes = _as_torch(classes, index.device, torch.int32)
@@ -394,9 +395,12 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
         raise ValueError("query shape does not match the index")
     if qmode is None:
         qmode = _lib.LMI_Q_F16 if index.storage == "f16" else _lib.LMI_Q_F32
-    out_d = torch.empty((nq, R, k), dtype=torch.float32, device=index.device)
-    out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
-    status = torch.zeros((1,), dtype=torch.int32, device=index.device)
+    if out is None:
+        out_d = torch.empty((nq, R, k), dtype=torch.float32, device=index.device)
+        out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
+        status = torch.zeros((1,), dtype=torch.int32, device=index.device)
+    else:
+        out_d, out_pos, status = out
     ws = index.workspace(nq, R, k, qmode)
     s = stream if stream is not None else _lib.stream_handle(index.device)
     check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(index.desc), ptr(q), nq, q.stride(0),
@@ -407,7 +411,7 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
 
 def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
                     qmode: Optional[int] = None, eps: float = _lib.LMI_REFINE_EPS, stream=None,
-                    fallback_count: bool = False):
+                    fallback_count: bool = False, out=None):
     """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
     arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
     (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback])."""
@@ -419,9 +423,12 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
         raise ValueError("query shape does not match the index")
     if qmode is None:
         qmode = _lib.LMI_Q_F16 if index.storage == "f16" else _lib.LMI_Q_F32
-    out_d = torch.empty((nq, R, k), dtype=torch.float64, device=index.device)
-    out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
-    status = torch.zeros((1,), dtype=torch.int32, device=index.device)
+    if out is None:
+        out_d = torch.empty((nq, R, k), dtype=torch.float64, device=index.device)
+        out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
+        status = torch.zeros((1,), dtype=torch.int32, device=index.device)
+    else:
+        out_d, out_pos, status = out
     need = lib.lmi_scan_f64_workspace_bytes(C.byref(index.desc), nq, R, k, qmode)
     ws = index._ws.get("f64")
     if ws is None or ws.numel() < need:
@@ -564,15 +571,25 @@ class Searcher:
         """K2 on this shard (+ all-gather and K3 for G > 1 ranks, the status
         words riding along so every rank sees every rank's bits).  `lap`
         (measurement only) is called after the scan and after the exchange."""
+        out = None
+        if self.index.world > 1:
+            # the lists and the status word land in this rank's slice of the
+            # all-gather's packed send buffer (li.dist.packed_lists)
+            from .dist import packed_lists
+            nq, R = classes.shape
+            buf, dv, pv, sv = packed_lists(nq * R, k_list, f64, self.index.device)
+            out = (dv.view(nq, R, k_list), pv.view(nq, R, k_list), sv)
         if f64:
-            d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode)
+            d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode,
+                                             out=out)
         else:
-            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode)
+            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode, out=out)
         if lap:
             lap("scan")
         if self.index.world > 1:
-            from .dist import gather_merge
-            d, pos, status = gather_merge(d, pos, k_list, self.group, status=status)
+            from .dist import gather_merge_packed
+            d, pos, status = gather_merge_packed(buf, nq * R, k_list, f64, self.group)
+            d, pos = d.view(nq, R, k_list), pos.view(nq, R, k_list)
             if lap:
                 lap("allgather")
         return d, pos, status

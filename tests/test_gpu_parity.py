@@ -84,6 +84,49 @@ def test_shard_merge_equals_single_gpu():
         assert torch.equal(dm, d1) and torch.equal(pm, p1)
 
 
+@pytest.mark.parametrize("f64", [False, True])
+@pytest.mark.parametrize("k", [10, 16])
+def test_packed_merge_equals_single_gpu(f64, k):
+    """The G > 1 product path: every shard's K2 writes its lists and status word
+    into its packed send buffer (li.dist.packed_lists), the buffers are
+    gathered (here by concatenation, as all_gather_into_tensor lays them out)
+    and K3 merges them in place (lmi_merge_topk_packed): bitwise the
+    single-shard lists, and the OR of the ranks' status words."""
+    from li import _lib
+    from li.dist import packed_lists
+    from li.index import bucket_topk_f64, check, ptr
+    if f64 and k > 10:
+        pytest.skip("float64 lists of k <= 10 here (k = 16 is the float32 K3 width)")
+    w = workloads.clustered(n=5000, nq=150, C=16, seed=3, label_mode="skewed")
+    R = 3
+    classes = torch.from_numpy(
+        O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R].astype(np.int32)).cuda()
+    q = torch.from_numpy(w["q"]).cuda()
+    scan = bucket_topk_f64 if f64 else bucket_topk
+    d1, p1, _ = scan(DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=256), q, classes, k)
+    nq = q.shape[0]
+    rows = nq * R
+    lib = _lib.load()
+    for G in (2, 3, 8):
+        bufs = []
+        for g in range(G):
+            buf, dv, pv, sv = packed_lists(rows, k, f64, q.device)
+            ix = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=256, rank=g, world=G)
+            scan(ix, q, classes, k, out=(dv.view(nq, R, k), pv.view(nq, R, k), sv))
+            if g == 1:
+                sv.fill_(4)  # a status bit on one rank reaches every rank's result
+            bufs.append(buf)
+        W = bufs[0].numel()
+        gathered = torch.cat(bufs)
+        md = torch.empty((rows, k), dtype=torch.float64 if f64 else torch.float32, device=q.device)
+        mp = torch.empty((rows, k), dtype=torch.int32, device=q.device)
+        st = torch.full((1,), -1, dtype=torch.int32, device=q.device)
+        check("lmi_merge_topk_packed", lib.lmi_merge_topk_packed(
+            ptr(gathered), G, W, rows, k, int(f64), ptr(md), ptr(mp), ptr(st), _lib.stream_handle(q.device)))
+        assert torch.equal(md.view(nq, R, k), d1) and torch.equal(mp.view(nq, R, k), p1)
+        assert int(st.item()) == 4
+
+
 @pytest.mark.parametrize("use_threshold", [True, False])
 @pytest.mark.parametrize("R", [1, 4])
 def test_full_search_matches_direct_oracle(use_threshold, R):

@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 5
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
@@ -44,6 +44,15 @@ def test_invalid_arguments_fail_loudly_without_a_device():
     assert rc == _lib.LMI_E_INVALID and b"d=2048" in lib.lmi_last_error()
     rc = lib.lmi_merge_topk_f64(None, None, 2, 10, 0, None, None, None)
     assert rc == _lib.LMI_E_INVALID and b"k=0" in lib.lmi_last_error()
+    # packed K3: rank stride of 10 rows x k 10 = 201 words (f32) -> 202; 301 -> 302 (f64)
+    assert lib.lmi_packed_rank_words(10, 10, 0) == 202
+    assert lib.lmi_packed_rank_words(10, 10, 1) == 302
+    rc = lib.lmi_merge_topk_packed(None, 2, 200, 10, 10, 0, None, None, None, None)
+    assert rc == _lib.LMI_E_INVALID and b"rank_words" in lib.lmi_last_error()
+    rc = lib.lmi_merge_topk_packed(None, 2, 203, 10, 10, 0, None, None, None, None)
+    assert rc == _lib.LMI_E_INVALID and b"odd" in lib.lmi_last_error()
+    rc = lib.lmi_merge_topk_packed(None, 2, 302, 10, 10, 1, None, None, None, None)
+    assert rc == _lib.LMI_E_INVALID and b"null pointer" in lib.lmi_last_error()
 
 
 def test_plan_chunks():
