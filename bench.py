@@ -314,6 +314,7 @@ def main():
     lib = _lib.load()
 
     use_graph = not args.no_graph and (world == 1 or torch.distributed.get_backend() == "nccl")
+    graph_failed = []
 
     def timed_graph(dist):
         """The step captured once as a HIP graph (Searcher.graph) and replayed:
@@ -322,7 +323,25 @@ def main():
         kernel's duration comes from HIP events around the same launches in K
         eager steps right after (outside the timed region; a kernel runs the
         same whichever way it is launched)."""
-        gs = searcher.graph(qn, q, args.R, k=args.k, dist=dist)
+        # a capture that fails on any rank (e.g. a collective the runtime
+        # cannot capture) sends every rank to the eager step: collectives
+        # are only recorded during capture, so no rank waits on a failed one
+        try:
+            gs = searcher.graph(qn, q, args.R, k=args.k, dist=dist)
+            ok = 1
+        except Exception as e:  # noqa: BLE001 (reported in the JSON line)
+            log(f"[bench] graph capture failed ({e!r}); timing eager launches")
+            graph_failed.append(repr(e)[:200])
+            gs, ok = None, 0
+        if world > 1:
+            t = torch.tensor([ok], dtype=torch.int32, device=device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+            ok = int(t.item())
+        if not ok:
+            if not graph_failed:
+                graph_failed.append("capture failed on another rank")
+            del gs
+            return timed_eager(dist)
         out = None
         for _ in range(args.warmup):
             out = gs.run()
@@ -359,6 +378,9 @@ def main():
         the last step's output)."""
         if use_graph:
             return timed_graph(dist)
+        return timed_eager(dist)
+
+    def timed_eager(dist):
         out = None
         for _ in range(args.warmup):
             out = searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
@@ -455,7 +477,9 @@ def main():
         "roofline": roof, "cpu_baseline": cpu,
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
         "recall_sample": sample, "breakdown_ms": breakdown,
-        "dist": args.dist, "step": "hip-graph replay" if use_graph else "eager launches",
+        "dist": args.dist,
+        "step": ("hip-graph replay" if use_graph and not graph_failed else
+                 "eager launches" + (f" (graph capture failed: {graph_failed[0]})" if graph_failed else "")),
         "other_dist": {"dist": other, "value": round(args.nq / (el_o / args.steps), 1),
                        "ms_per_step": round(el_o / args.steps * 1e3, 3),
                        "scan_kernel_ms": round(scan_ms_o, 4),
