@@ -1533,6 +1533,43 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         const bool live = 32 * slot + col < np;
         const int pp = tile.pp0 + 32 * slot + col;
 
+        // Block 0's DMA goes out before the query fragments are loaded, so
+        // the two memory latencies of a tile's start overlap (the ring is
+        // free: the previous tile drained it before its closing barrier)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.corpus + row0u * D), (short)0, nrows * D * 2, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.inv_norm + row0u), (short)0, nrows * 4, 0x00020000);
+
+        const int nblk = (nrows + 31) / 32;
+        // DMA of one stage (block b, phase j) into the LDS slot at byte offset
+        // `so`: pieces 0, 1 = rows 4w+2i, 4w+2i+1 (lane l: row 4w + 2i + (l&1),
+        // chunk l >> 1; piece 1 is piece 0 + 2 rows through soffset); in the
+        // block's last phase the wave's 4 norms too.
+        // the pieces of wave w (its 4 rows of the block and their norms)
+        auto dma_stage_w = [&](int so, int b, int j, int w) {
+            if (kNoDma) return;
+            unsigned char* sl = ring + so;
+            const int nb_area = b % 3;  // norms of block b: slot (b % 3)'s norm area
+            if (kL2Src) b &= 3;
+            const uint32_t vo_row = (uint32_t)((4 * w + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * w) * PIECEP), 16, vo_row,
+                                                     b * (32 * D * 2) + j * ROWB, 0, kAux);
+            // (+2 rows through soffset: an instruction offset would move the
+            // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * w + 1) * PIECEP), 16,
+                                                     vo_row, b * (32 * D * 2) + j * ROWB + 2 * D * 2,
+                                                     0, kAux);
+            if (j == NST - 1 && lane < 4)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(ring + nb_area * STAGE + NORM_OFF + 16 * w),
+                                                         4, (uint32_t)((4 * w + opaque(lane)) * 4), b * 128, 0, 0);
+        };
+        auto dma_stage = [&](int so, int b, int j) { dma_stage_w(so, b, j, wave); };
+        // block b lives in slots NST*(b&1) .. +NST-1; block 0 is the prologue,
+        // block b+1's DMA rides in block b
+#pragma unroll
+        for (int j = 0; j < NST; ++j) dma_stage(j * STAGE, 0, j);
+
         half8 qf[NQF];
         // the lane's bound: only objects with ord(d) <= thr can enter the
         // pair's top-KL (the distance part of a key: the bound may come from
@@ -1584,39 +1621,6 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         __syncthreads();
 
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(a.corpus + row0u * D), (short)0, nrows * D * 2, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(a.inv_norm + row0u), (short)0, nrows * 4, 0x00020000);
-
-        const int nblk = (nrows + 31) / 32;
-        // DMA of one stage (block b, phase j) into the LDS slot at byte offset
-        // `so`: pieces 0, 1 = rows 4w+2i, 4w+2i+1 (lane l: row 4w + 2i + (l&1),
-        // chunk l >> 1; piece 1 is piece 0 + 2 rows through soffset); in the
-        // block's last phase the wave's 4 norms too.
-        // the pieces of wave w (its 4 rows of the block and their norms)
-        auto dma_stage_w = [&](int so, int b, int j, int w) {
-            if (kNoDma) return;
-            unsigned char* sl = ring + so;
-            const int nb_area = b % 3;  // norms of block b: slot (b % 3)'s norm area
-            if (kL2Src) b &= 3;
-            const uint32_t vo_row = (uint32_t)((4 * w + (lane & 1)) * (D * 2) + (lane >> 1) * 16);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * w) * PIECEP), 16, vo_row,
-                                                     b * (32 * D * 2) + j * ROWB, 0, kAux);
-            // (+2 rows through soffset: an instruction offset would move the
-            // LDS destination as well, LDS_ADDR = M0 + inst_offset + lane * 16)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_t)(sl + (2 * w + 1) * PIECEP), 16,
-                                                     vo_row, b * (32 * D * 2) + j * ROWB + 2 * D * 2,
-                                                     0, kAux);
-            if (j == NST - 1 && lane < 4)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (lds_t)(ring + nb_area * STAGE + NORM_OFF + 16 * w),
-                                                         4, (uint32_t)((4 * w + opaque(lane)) * 4), b * 128, 0, 0);
-        };
-        auto dma_stage = [&](int so, int b, int j) { dma_stage_w(so, b, j, wave); };
-        // block b lives in slots NST*(b&1) .. +NST-1; block 0 is the prologue,
-        // block b+1's DMA rides in block b
-#pragma unroll
-        for (int j = 0; j < NST; ++j) dma_stage(j * STAGE, 0, j);
         // a lane's A-fragment base inside a slot (row col = lane & 31, half h)
         const uint32_t lane_off = (uint32_t)(((lane >> 1) & 15) * PIECEP + (lane & 1) * 16 + (lane >> 5) * 32);
 
