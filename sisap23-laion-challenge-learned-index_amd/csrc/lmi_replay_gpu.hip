@@ -140,6 +140,7 @@ __device__ void stable_argsort_dev(const double* row, int n, int* idx) {
 }
 
 constexpr int kUCap = 8192;  // relevant positions of a group held in LDS
+constexpr int kBmBits = 196608;  // selection bitmap: U's positions spanning < 192K (24 KiB)
 constexpr int kTG = 1024;    // group kernel: one large workgroup per category
 
 template <int NT>
@@ -229,6 +230,8 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
     __shared__ int32_t Ul[kUCap];
     __shared__ int32_t Sw[kTG / 64][2 * kMaxKr];  // per wave: smallest members of its share
     __shared__ int nsw[kTG / 64 + 1];
+    __shared__ int wsum[kTG / 64];
+    __shared__ uint32_t bm[kBmBits / 32];  // U as a bitmap (positions - umin)
     const int c = blockIdx.x;
     const int tid = threadIdx.x;
     if (a.bucket_size[c] <= 0) return;  // groupby visits non-empty categories only
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
         // latency chain per entry)
         constexpr int kUL = 8;
         int nb_tot = 0;
+        int umin = INT32_MAX, umax = -1;  // range of U's relevant positions
         for (int e0 = tid; e0 < nU; e0 += kUL * kTG) {
             int qv[kUL];
             size_t ov[kUL];
@@ -279,18 +283,66 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
                 const bool rel = pv[u] >= 0 && dv[u] < tv[u];
                 if (e < nU) U[e] = rel ? pv[u] : INT32_MAX;
                 nb_tot += rel ? 1 : 0;
+                if (rel) {
+                    umin = min(umin, pv[u]);
+                    umax = max(umax, pv[u]);
+                }
             }
         }
         nb_tot = block_sum_g(nb_tot, sh);  // (its barriers publish U)
         if (nb_tot == 0) return;  // LearnedIndex.py:157-159
+        umin = block_min_g(umin, sh);
+        umax = -block_min_g(-umax, sh);
 #ifdef LMI_ABLATION
         if (a.abl == 2) return;
 #endif
         const int want = kr + kl_use;
+        const int lane = tid & 63, wv = tid >> 6;
+        if (umax - umin < kBmBits) {
+            // U's positions as a bitmap over [umin, umax] (unique by
+            // construction), then the `want` lowest set bits by one block-wide
+            // prefix count: a few barriers instead of `want` dependent
+            // wave-minimum rounds twice over (the bench's groups: ~28 -> a few us)
+            const int nw = ((umax - umin) >> 5) + 1;
+            for (int i = tid; i < nw; i += kTG) bm[i] = 0u;
+            __syncthreads();
+            for (int e = tid; e < nU; e += kTG) {
+                const int32_t p = U[e];
+                if (p != INT32_MAX) atomicOr(&bm[(p - umin) >> 5], 1u << ((p - umin) & 31));
+            }
+            __syncthreads();
+            const int wpt = (nw + kTG - 1) / kTG;
+            const int w0 = min(nw, tid * wpt), w1 = min(nw, w0 + wpt);
+            int cnt_t = 0;
+            for (int i = w0; i < w1; ++i) cnt_t += __popc(bm[i]);
+            int incl = cnt_t;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            if (lane == 63) wsum[wv] = incl;
+            __syncthreads();
+            int pre = 0, tot = 0;
+#pragma unroll
+            for (int w = 0; w < kTG / 64; ++w) {
+                pre += (w < wv) ? wsum[w] : 0;
+                tot += wsum[w];
+            }
+            int o = pre + incl - cnt_t;  // set bits before this thread's words
+            for (int i = w0; i < w1 && o < want; ++i) {
+                uint32_t m = bm[i];
+                while (m != 0u && o < want) {
+                    const int b = __builtin_ctz(m);
+                    m &= m - 1u;
+                    S[o++] = umin + 32 * i + b;
+                }
+            }
+            if (tid == 0) nsw[kTG / 64] = min(tot, want);
+        } else {
         // the smallest `want` members of U: each wave finds those of its
         // share (every 4th 64-entry run), then wave 0 merges the four lists
         // (a global member among the smallest `want` is among its share's)
-        const int lane = tid & 63, wv = tid >> 6;
         int prev = -1, cnt = 0;
         // the lane's share (<= NR entries) read once into registers, then the
         // `want` rounds run on them; NR by the group's size (the compares of
@@ -370,6 +422,7 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
             else
                 mrg(std::integral_constant<int, 16>{});
         }
+        }  // (register selection)
         __syncthreads();
         const int ns = nsw[kTG / 64];
 #ifdef LMI_ABLATION
@@ -406,32 +459,45 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
                     a.dr_p[(size_t)qv[u] * kr + j] = pv[u];
                 }
             }
-            for (int gi = g0 + tid; gi < g1; gi += kTG) {
-                const int q = G[gi];
-                const int32_t* u = U + (size_t)(gi - g0) * kl_use;
-                int32_t lp[kMaxKr];
-                int n_rel = 0;
+            // the query's relevant positions in NL registers (NL >= kl_use:
+            // 10 at the bench's k, so the membership test of each of the ns
+            // smallest members of U is 10 compares, not kMaxKr)
+            auto fill = [&](auto nl) {
+                constexpr int NL = decltype(nl)::value;
+                for (int gi = g0 + tid; gi < g1; gi += kTG) {
+                    const int q = G[gi];
+                    const int32_t* u = U + (size_t)(gi - g0) * kl_use;
+                    int32_t lp[NL];
+                    int n_rel = 0;
 #pragma unroll
-                for (int j = 0; j < kMaxKr; ++j) {
-                    lp[j] = j < kl_use ? u[j] : INT32_MAX;
-                    n_rel += lp[j] != INT32_MAX ? 1 : 0;
-                }
-                double* od = a.dr_d + (size_t)q * kr;
-                int32_t* op = a.dr_p + (size_t)q * kr;
-                int n = n_rel;
-                for (int v = 0; v < ns && n < kr; ++v) {
-                    const int32_t sv = S[v];
-                    bool mine = false;
-#pragma unroll
-                    for (int j = 0; j < kMaxKr; ++j) mine |= lp[j] == sv;
-                    if (!mine) {
-                        od[n] = kFill;
-                        op[n] = sv;
-                        ++n;
+                    for (int j = 0; j < NL; ++j) {
+                        lp[j] = j < kl_use ? u[j] : INT32_MAX;
+                        n_rel += lp[j] != INT32_MAX ? 1 : 0;
                     }
+                    double* od = a.dr_d + (size_t)q * kr;
+                    int32_t* op = a.dr_p + (size_t)q * kr;
+                    int n = n_rel;
+                    for (int v = 0; v < ns && n < kr; ++v) {
+                        const int32_t sv = S[v];
+                        bool mine = false;
+#pragma unroll
+                        for (int j = 0; j < NL; ++j) mine |= lp[j] == sv;
+                        if (!mine) {
+                            od[n] = kFill;
+                            op[n] = sv;
+                            ++n;
+                        }
+                    }
+                    if (n < kr) atomicOr(a.status, 1);  // cannot happen: |U| >= kr
                 }
-                if (n < kr) atomicOr(a.status, 1);  // cannot happen: |U| >= kr
-            }
+            };
+            static_assert(kMaxKr == 32, "membership widths");
+            if (kl_use <= 10)
+                fill(std::integral_constant<int, 10>{});
+            else if (kl_use <= 16)
+                fill(std::integral_constant<int, 16>{});
+            else
+                fill(std::integral_constant<int, 32>{});
         } else {
             // |U| < kr: the quirk on row 0 (q0 = first query of the group)
             if (tid == 0) {

@@ -122,3 +122,38 @@ def test_device_replay_large_groups(use_threshold, nq, C):
     assert int(st.item()) == 0
     np.testing.assert_array_equal(dd.cpu().numpy(), ref_d)
     np.testing.assert_array_equal(aa.cpu().numpy().view(np.uint32), ref_a)
+
+
+@pytest.mark.parametrize("use_threshold", [True, False])
+def test_device_replay_wide_position_range(use_threshold):
+    """A bucket of 300K rows: a group's relevant positions can span more than
+    the group kernel's selection bitmap (192K positions), so that group
+    selects by wave-minimum rounds; the other buckets take the bitmap."""
+    rng = np.random.default_rng(77)
+    nq, R, kl = 400, 2, 10
+    size = np.array([300_000, 60, 250, 7], np.int64)
+    off = np.concatenate([[0], np.cumsum(size)])
+    classes = np.stack([rng.choice(4, R, replace=False, p=[0.5, 0.2, 0.2, 0.1])
+                        for _ in range(nq)]).astype(np.int32)
+    d = np.full((nq, R, kl), np.inf, np.float32)
+    pos = np.full((nq, R, kl), -1, np.int32)
+    for q in range(nq):
+        for r in range(R):
+            c = classes[q, r]
+            n = min(kl, int(size[c]))
+            pp = np.unique(rng.integers(0, size[c], 4 * n))[:n]
+            pp = rng.permutation(pp)[:n] + off[c]
+            dd = np.round(rng.random(pp.size) * 0.6 + 0.2, 3).astype(np.float32)
+            o = np.lexsort((pp, dd))
+            d[q, r, :pp.size], pos[q, r, :pp.size] = dd[o], pp[o]
+    ids = rng.permutation(int(off[-1])).astype(np.int64) + 1
+    ref_d, ref_a = replay(classes, d, pos, k_round=10, k_final=10, bucket_size=size, pos_to_id=ids,
+                          use_threshold=use_threshold)
+    dev = torch.device("cuda")
+    dd_, aa, st = replay_device(torch.from_numpy(classes).to(dev), torch.from_numpy(d).to(dev),
+                                torch.from_numpy(pos).to(dev), k_round=10, k_final=10,
+                                bucket_size=torch.from_numpy(size).to(dev),
+                                pos_to_id=torch.from_numpy(ids).to(dev), use_threshold=use_threshold)
+    assert int(st.item()) == 0
+    np.testing.assert_array_equal(dd_.cpu().numpy(), ref_d)
+    np.testing.assert_array_equal(aa.cpu().numpy().view(np.uint32), ref_a)
