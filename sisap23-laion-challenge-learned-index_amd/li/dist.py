@@ -119,7 +119,8 @@ def packed_lists(rows: int, k: int, f64: bool, device):
     return buf, d, pos, status
 
 
-def gather_merge_packed(buf: torch.Tensor, rows: int, k: int, f64: bool, group=None):
+def gather_merge_packed(buf: torch.Tensor, rows: int, k: int, f64: bool, group=None,
+                        status_out: Optional[torch.Tensor] = None):
     """All-gather every rank's packed buffer (packed_lists) in one collective,
     then K3 over the gathered buffer in place (lmi_merge_topk_packed): the
     merged lists [rows, k] and the OR of every rank's status word, so all
@@ -133,7 +134,8 @@ def gather_merge_packed(buf: torch.Tensor, rows: int, k: int, f64: bool, group=N
     _all_gather(out, buf, group)
     md = torch.empty((rows, k), dtype=torch.float64 if f64 else torch.float32, device=buf.device)
     mp = torch.empty((rows, k), dtype=torch.int32, device=buf.device)
-    st = torch.empty((1,), dtype=torch.int32, device=buf.device)
+    st = status_out if status_out is not None else torch.empty((1,), dtype=torch.int32,
+                                                               device=buf.device)
     check("lmi_merge_topk_packed", _lib.load().lmi_merge_topk_packed(
         ptr(out), G, W, rows, k, int(bool(f64)), ptr(md), ptr(mp), ptr(st),
         _lib.stream_handle(buf.device)))

@@ -496,10 +496,12 @@ def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k
 
 def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch.Tensor, *,
                   k_round: int, k_final: int, bucket_size: torch.Tensor, pos_to_id: torch.Tensor,
-                  use_threshold: bool, thr_round0: Optional[torch.Tensor] = None, stream=None):
+                  use_threshold: bool, thr_round0: Optional[torch.Tensor] = None, stream=None,
+                  out=None):
     """A5 on the device (lmi_replay_device, or lmi_replay_device_f64 for
     float64 lists): same results as `replay`, device tensors in and out:
-    (dists f64 [nq, w], anns uint32-as-int32 [nq, w], status)."""
+    (dists f64 [nq, w], anns uint32-as-int32 [nq, w], status); `out` = such a
+    triple to write into (the status word zeroed by the caller)."""
     lib = _lib.load()
     dev = lists_d.device
     classes = _as_torch(classes, dev, torch.int32)
@@ -511,9 +513,12 @@ def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch
     lists_pos = _as_torch(lists_pos, dev, torch.int32).reshape(nq, R, -1).contiguous()
     k_list = lists_d.shape[2]
     w = k_round if R == 1 else k_final
-    dists = torch.empty((nq, w), dtype=torch.float64, device=dev)
-    anns = torch.empty((nq, w), dtype=torch.int32, device=dev)  # uint32 bits
-    status = torch.zeros((1,), dtype=torch.int32, device=dev)
+    if out is None:
+        dists = torch.empty((nq, w), dtype=torch.float64, device=dev)
+        anns = torch.empty((nq, w), dtype=torch.int32, device=dev)  # uint32 bits
+        status = torch.zeros((1,), dtype=torch.int32, device=dev)
+    else:
+        dists, anns, status = out
     n_b = int(bucket_size.numel())
     need = lib.lmi_replay_device_workspace_bytes(nq, R, k_list, k_round, k_final, n_b)
     ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
@@ -529,6 +534,27 @@ def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch
         ptr(bucket_size), n_b, ptr(pos_to_id), int(pos_to_id.numel()), int(bool(use_threshold)),
         ptr(thr), ptr(dists), ptr(anns), ptr(status), ptr(ws), ws.numel(), s))
     return dists, anns, status
+
+
+def answer_buffer(nq: int, w: int, device):
+    """The step's answer in ONE device buffer, so it crosses PCIe in one copy:
+    int32 words [dists f64 nq*w (2 words each)][anns uint32 nq*w][scan status,
+    replay status] -> (buf, dists [nq, w], anns [nq, w], status words [2],
+    zeroed)."""
+    n = nq * w
+    buf = torch.empty((3 * n + 2,), dtype=torch.int32, device=device)
+    st = buf[3 * n:]
+    st.zero_()
+    return buf, buf[:2 * n].view(torch.float64).view(nq, w), buf[2 * n:3 * n].view(nq, w), st
+
+
+def answer_views(h: torch.Tensor, nq: int, w: int):
+    """numpy views of an answer buffer copied to the host:
+    (dists f64 [nq, w], anns uint32 [nq, w], scan status, replay status)."""
+    a = h.numpy()
+    n = nq * w
+    return (a[:2 * n].view(np.float64).reshape(nq, w), a[2 * n:3 * n].view(np.uint32).reshape(nq, w),
+            int(a[3 * n]), int(a[3 * n + 1]))
 
 
 class Searcher:
@@ -567,11 +593,19 @@ class Searcher:
         self._qcheck = (key, mode)
         return mode
 
-    def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool, lap=None):
+    def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool, lap=None,
+              status_out=None):
         """K2 on this shard (+ all-gather and K3 for G > 1 ranks, the status
         words riding along so every rank sees every rank's bits).  `lap`
-        (measurement only) is called after the scan and after the exchange."""
+        (measurement only) is called after the scan and after the exchange.
+        `status_out` (a zeroed device int32 word): the status lands there."""
         out = None
+        if self.index.world == 1 and status_out is not None:
+            nq, R = classes.shape
+            dev = self.index.device
+            out = (torch.empty((nq, R, k_list), dtype=torch.float64 if f64 else torch.float32,
+                               device=dev),
+                   torch.empty((nq, R, k_list), dtype=torch.int32, device=dev), status_out)
         if self.index.world > 1:
             # the lists and the status word land in this rank's slice of the
             # all-gather's packed send buffer (li.dist.packed_lists)
@@ -588,7 +622,8 @@ class Searcher:
             lap("scan")
         if self.index.world > 1:
             from .dist import gather_merge_packed
-            d, pos, status = gather_merge_packed(buf, nq * R, k_list, f64, self.group)
+            d, pos, status = gather_merge_packed(buf, nq * R, k_list, f64, self.group,
+                                                 status_out=status_out)
             d, pos = d.view(nq, R, k_list), pos.view(nq, R, k_list)
             if lap:
                 lap("allgather")
@@ -689,9 +724,15 @@ class Searcher:
         def lap_at(name):
             tl[0] = lap(name, tl[0])
 
-        d, pos, status = self._scan(q_search, classes, k_list, qmode, f64, lap_at if sync else None)
-        t0 = tl[0]
         nq = classes.shape[0]
+        ans = None
+        if semantics == "reference" and replay_on == "device":
+            # the answer and both status words in one buffer: one D2H copy
+            w_ans = k_round if classes.shape[1] == 1 else k
+            ans = answer_buffer(nq, w_ans, dev)
+        d, pos, status = self._scan(q_search, classes, k_list, qmode, f64, lap_at if sync else None,
+                                    status_out=None if ans is None else ans[3][0:1])
+        t0 = tl[0]
         h_st = self._host("st", (2,), torch.int32)
 
         def check_status(st, rst=0):
@@ -735,32 +776,31 @@ class Searcher:
         if replay_on == "device":
             bsz, p2id = self._device_tables()
 
-            def run_replay(d, pos):
-                return replay_device(classes, d, pos, k_round=k_round, k_final=k, bucket_size=bsz,
-                                     pos_to_id=p2id, use_threshold=use_threshold)
+            def run_replay(d, pos, ans):
+                replay_device(classes, d, pos, k_round=k_round, k_final=k, bucket_size=bsz,
+                              pos_to_id=p2id, use_threshold=use_threshold,
+                              out=(ans[1], ans[2], ans[3][1:2]))
+                # a fresh pinned buffer from torch's caching host allocator,
+                # handed to the caller as numpy views (no host copy; it returns
+                # to the cache when the caller drops the arrays)
+                h = torch.empty(tuple(ans[0].shape), dtype=torch.int32, pin_memory=True)
+                h.copy_(ans[0], non_blocking=True)
+                return h
 
-            rd, ra, rst = run_replay(d, pos)
+            h = run_replay(d, pos, ans)
             t0 = lap("replay", t0)
-            # fresh pinned outputs from torch's caching host allocator: handed
-            # to the caller as they are (no host copy; a buffer returns to the
-            # cache when the caller drops the arrays)
-            h_d = torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True)
-            h_a = torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True)
-            h_d.copy_(rd, non_blocking=True)
-            h_a.copy_(ra, non_blocking=True)
-            h_st[0:1].copy_(status, non_blocking=True)
-            h_st[1:2].copy_(rst, non_blocking=True)
             torch.cuda.current_stream(dev).synchronize()
             t0 = lap("d2h", t0)
-            if check_status(int(h_st[0]), int(h_st[1])):
-                d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64)
-                rd, ra, rst = run_replay(d, pos)
-                h_d.copy_(rd)
-                h_a.copy_(ra)
-                h_st[0:1].copy_(status)
-                h_st[1:2].copy_(rst)
-                check_status(int(h_st[0]) & ~_lib.LMI_STATUS_QUERY_NOT_F16, int(h_st[1]))
-            return h_d.numpy(), h_a.numpy().view(np.uint32)
+            hd, ha, st0, st1 = answer_views(h, nq, w_ans)
+            if check_status(st0, st1):
+                ans = answer_buffer(nq, w_ans, dev)
+                d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64,
+                                            status_out=ans[3][0:1])
+                h = run_replay(d, pos, ans)
+                torch.cuda.current_stream(dev).synchronize()
+                hd, ha, st0, st1 = answer_views(h, nq, w_ans)
+                check_status(st0 & ~_lib.LMI_STATUS_QUERY_NOT_F16, st1)
+            return hd, ha
         h_cls = self._host("cls", (nq, R), torch.int32)
         h_d = self._host("d", tuple(d.shape), d.dtype)
         h_pos = self._host("pos", tuple(pos.shape), torch.int32)
@@ -813,13 +853,20 @@ class GraphedSearch:
         f64 = dist == "f64"
         bsz, p2id = s._device_tables()
 
+        nq = self.q_search.shape[0]
+        self.w = k_round if R == 1 else k
+
         def step():
+            # the answer and both status words land in one buffer, copied to
+            # the host in one D2H (answer_buffer)
+            ans = answer_buffer(nq, self.w, dev)
             classes = s.route(self.q_nav, R)
-            d, pos, status = s._scan(self.q_search, classes, k_round, self.qmode, f64)
-            rd, ra, rst = replay_device(classes, d, pos, k_round=k_round, k_final=k,
-                                        bucket_size=bsz, pos_to_id=p2id,
-                                        use_threshold=use_threshold)
-            return rd, ra, status, rst
+            d, pos, _ = s._scan(self.q_search, classes, k_round, self.qmode, f64,
+                                status_out=ans[3][0:1])
+            replay_device(classes, d, pos, k_round=k_round, k_final=k, bucket_size=bsz,
+                          pos_to_id=p2id, use_threshold=use_threshold,
+                          out=(ans[1], ans[2], ans[3][1:2]))
+            return ans[0]
 
         # warm up on a side stream (allocations, kernel attributes, RCCL
         # communicators), then capture
@@ -827,20 +874,15 @@ class GraphedSearch:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(2):
-                rd, ra, st, rst = step()
+                buf = step()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        self.h_d = torch.empty(tuple(rd.shape), dtype=torch.float64, pin_memory=True)
-        self.h_a = torch.empty(tuple(ra.shape), dtype=torch.int32, pin_memory=True)
-        self.h_st = torch.zeros((2,), dtype=torch.int32, pin_memory=True)
+        self.h = torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
-            rd, ra, st, rst = step()
-            self.h_d.copy_(rd, non_blocking=True)
-            self.h_a.copy_(ra, non_blocking=True)
-            self.h_st[0:1].copy_(st, non_blocking=True)
-            self.h_st[1:2].copy_(rst, non_blocking=True)
-        self._keep = (rd, ra, st, rst)
+            buf = step()
+            self.h.copy_(buf, non_blocking=True)
+        self._keep = buf
         torch.cuda.synchronize(dev)
 
     def run(self):
@@ -848,7 +890,7 @@ class GraphedSearch:
         dev = self.searcher.index.device
         self.graph.replay()
         torch.cuda.current_stream(dev).synchronize()
-        st, rst = int(self.h_st[0]), int(self.h_st[1])
+        hd, ha, st, rst = answer_views(self.h, self.q_search.shape[0], self.w)
         if st & _lib.LMI_STATUS_INTERNAL or rst:
             raise RuntimeError(f"search: internal status {st}/{rst}")
         if st & _lib.LMI_STATUS_QUERY_NOT_F16:
@@ -857,4 +899,4 @@ class GraphedSearch:
             return self.searcher.search(self.q_nav, self.q_search, self.R, k=self.k,
                                         k_round=self.k_round, use_threshold=self.use_threshold,
                                         dist=self.dist)
-        return self.h_d.numpy(), self.h_a.numpy().view(np.uint32)
+        return hd, ha
