@@ -4,10 +4,11 @@
     python bench.py [--gpus N --steps K --warmup W] [--scale 10M|300K|...]
 
 One step = one search of the whole 10k-query batch exactly as the reference
-times it (search.py:116-141): router (K1) + per-(query, probe) bucket scan
-(K2) [+ RCCL all-gather + K3 merge for N > 1] + D2H of the lists + the replay
-of the reference's merge (host C++).  Inputs (corpus index, queries) are
-resident in HBM before the timed region.  N > 1: one process per GPU,
+times it (search.py:116-141): H2D of the query batch from pinned host memory
+(the reference's queries are host arrays, search.py:49, :85-87) + router (K1)
++ per-(query, probe) bucket scan (K2) [+ RCCL all-gather + K3 merge for N > 1]
++ the replay of the reference's merge (K4) + D2H of the answer.  The corpus
+index is resident in HBM before the timed region.  N > 1: one process per GPU,
 started by torchrun or, without one, by this script itself (launch_ranks);
 the corpus striped over the ranks; all ranks search the same batch (strong
 scaling: value = nq / max-over-ranks step time, the RCCL all-gather inside).
@@ -18,6 +19,10 @@ Besides the JSON fields of the driver contract the line carries:
   cpu_baseline  the oracle restatement (oracle/lmi_oracle.py, "port") timed on
                 a bounded sample of the same workload on this host's cores
   recall        recall@k of the returned ids against exact k-NN on a sample
+  parity        the graph's first answer vs an eager step (bitwise), and the
+                per-(query, probe) lists of sampled queries (rank 0's merged
+                lists at N > 1) vs a float64 brute force (list_parity)
+  h2d           the step's query upload alone (HIP events)
 """
 from __future__ import annotations
 
@@ -196,6 +201,90 @@ def cpu_baseline(index, q, classes, lists_d, args, budget_s=15.0):
     return out
 
 
+@torch.no_grad()
+def list_parity(index, x, q, classes, lists_d, lists_pos, n_sample, f64, seed=5):
+    """Parity of the per-(query, probe) lists the timed step is built on, on
+    `n_sample` sampled queries: every list against an independent brute force
+    over the same bucket rows -- torch float64 on the GPU, sklearn's arithmetic
+    (rows and query normalised, then the dot, utils.py:11), full rows sorted
+    by (distance, global position), first k (LearnedIndex.py:170-172).  At
+    G > 1 these are rank 0's lists after the all-gather + K3 merge, and the
+    rows come from the full corpus (every rank generated it), so the check
+    covers the striped scan and the exchange.  Distances must agree within
+    1e-5 (float32 lists; north_star) or 1e-12 (float64 lists); ids must be
+    equal, except inside runs of distances tied within 1e-6 / 1e-12 (the
+    reference's unstable argsort order there is unspecified):
+    `tie_window_rows` counts the lists that needed that window."""
+    nq, R, k = lists_d.shape
+    atol, tie = (1e-12, 1e-12) if f64 else (1e-5, 1e-6)
+    sample = np.sort(np.random.default_rng(seed).choice(nq, min(n_sample, nq), replace=False))
+    ld = lists_d.double().cpu().numpy()[sample]
+    lp = lists_pos.cpu().numpy()[sample]
+    cls = np.asarray(classes)[sample]
+    off = index.layout.bucket_off
+    dev = index.device
+    qs = q[torch.from_numpy(sample).to(q.device)].double().to(dev)
+    qs = qs / torch.where(qs.norm(dim=1, keepdim=True) < 10 * 1.1920929e-07, 1.0,
+                          qs.norm(dim=1, keepdim=True))
+    full = index.world == 1
+    if not full and not isinstance(x, torch.Tensor):
+        return {"checked_lists": 0, "note": "corpus not materialised on rank 0 (RowSource)"}
+    order = torch.from_numpy(index.layout.order)
+    checked = bad = tie_rows = 0
+    for c in np.unique(cls):
+        a, b = int(off[c]), int(off[c + 1])
+        if full:
+            y = index.corpus[a:b, :index.d]
+        else:
+            y = x[order[a:b].to(x.device)].to(dev)
+        y = y.double()
+        yn = y.norm(dim=1, keepdim=True)
+        y = y / torch.where(yn < 10 * 1.1920929e-07, 1.0, yn)
+        sel_q, sel_r = np.nonzero(cls == c)
+        D = 1.0 - qs[torch.from_numpy(sel_q).to(dev)] @ y.T          # [pairs, N_c]
+        o = torch.sort(D, dim=1, stable=True).indices[:, :k]       # (d, position) order
+        rd = torch.gather(D, 1, o).cpu().numpy()
+        rp = (o + a).cpu().numpy()
+        Dh = D.cpu().numpy()
+        for j, (i, r) in enumerate(zip(sel_q, sel_r)):
+            kk = min(k, b - a)
+            gd, gp = ld[i, r, :kk], lp[i, r, :kk]
+            checked += 1
+            ok = np.allclose(gd, rd[j, :kk], rtol=0, atol=atol) and bool(np.all(gp >= a)) and \
+                bool(np.all(gp < b))
+            used_tie = False
+            if ok and not np.array_equal(gp, rp[j, :kk]):
+                # ids differ: each must sit at its rank's distance within the tie window
+                dd = Dh[j, gp - a]
+                ok = bool(np.all(np.abs(dd - rd[j, :kk]) <= tie)) and len(set(gp)) == kk
+                used_tie = ok
+            if kk < k:
+                ok = ok and bool(np.all(lp[i, r, kk:] < 0))
+            bad += 0 if ok else 1
+            tie_rows += 1 if used_tie else 0
+    return {"checked_lists": int(checked), "queries": int(sample.size), "mismatches": int(bad),
+            "tie_window_rows": int(tie_rows), "atol": atol, "tie": tie,
+            "checker": "torch float64 brute force over the same bucket rows (bench.list_parity)"}
+
+
+@torch.no_grad()
+def h2d_ms(gs, reps=10):
+    """The step's host -> device upload alone (this rank's staged block), HIP
+    events on the current stream: ms per copy and GB/s."""
+    dev = gs.searcher.index.device
+    g = gs.searcher.index.rank
+    dst = torch.empty_like(gs.d_blk)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dst.copy_(gs.h_blk[g], non_blocking=True)
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(gs.h_blk[g], non_blocking=True)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    return ms, gs.upload_bytes() / (ms * 1e-3) / 1e9
+
+
 def pmc_traffic(kernel_ms):
     """HBM-side bytes per scan launch from the committed rocprofv3 PMC passes
     (tools/gpu_profile.sh -> profiles/*pmc_traffic.json): FETCH_SIZE x 2 (gfx950
@@ -288,6 +377,8 @@ def main():
                     help="scan chunk (rows); default by GPU count: 8192 on 1, 4096 on 2-4, 2048 on "
                          "more (a shard's tiles must still fill 256 CUs; tools/gpu_shards.sh)")
     ap.add_argument("--recall-sample", type=int, default=200)
+    ap.add_argument("--parity-sample", type=int, default=64,
+                    help="queries whose lists are checked against a float64 brute force")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager step (every launch from the host) instead of the "
@@ -315,33 +406,70 @@ def main():
 
     use_graph = not args.no_graph and (world == 1 or torch.distributed.get_backend() == "nccl")
     graph_failed = []
+    # the batch starts in HOST memory, as the reference's (search.py:49,
+    # :85-87): pinned buffers filled once before the timer (like its h5 loads);
+    # every timed step uploads it (H2D), searches and copies the answer back
+    qn_h = qn.cpu().numpy()
+    q_h = q.cpu().numpy()
+    q16_exact = index.storage == "f16" and bool(np.array_equal(q_h.astype(np.float16).astype(np.float32), q_h))
+    qn_pin = torch.from_numpy(qn_h).pin_memory()
+    q_pin = torch.from_numpy(q_h.astype(np.float16) if q16_exact else q_h).pin_memory()
+    checks = {}
+
+    def eager_step(dist):
+        qn_d = qn_pin.to(device, non_blocking=True)
+        q_d = q_pin.to(device, non_blocking=True).float()
+        return searcher.search(qn_d, q_d, args.R, k=args.k, use_threshold=True, dist=dist)
+
+    def agree(flag):
+        if world == 1:
+            return bool(flag)
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=device)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+        return bool(t.item())
+
+    def kernel_ms(dist):
+        """The scan kernel's mean duration: HIP events the library records on
+        the launch stream around every timed launch, over K eager steps
+        (events recorded into a graph cannot be timed on ROCm; a kernel runs
+        the same whichever way it is launched)."""
+        lib.lmi_timing_read(None, 0)
+        lib.lmi_timing_enable(1)
+        for _ in range(args.steps):
+            eager_step(dist)
+        torch.cuda.synchronize()
+        lib.lmi_timing_enable(0)
+        ms = (_lib.C.c_float * max(args.steps, 1))()
+        n_ev = lib.lmi_timing_read(ms, args.steps)
+        return float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
 
     def timed_graph(dist):
         """The step captured once as a HIP graph (Searcher.graph) and replayed:
         W untimed replays, then K replays bracketed by barrier + synchronize.
-        Events recorded into a graph cannot be timed on ROCm, so the scan
-        kernel's duration comes from HIP events around the same launches in K
-        eager steps right after (outside the timed region; a kernel runs the
-        same whichever way it is launched)."""
-        # a capture that fails on any rank (e.g. a collective the runtime
-        # cannot capture) sends every rank to the eager step: collectives
-        # are only recorded during capture, so no rank waits on a failed one
+        Before timing, the first replay's answer must equal an eager step's bit
+        for bit on every rank, else the eager step is timed instead."""
         try:
-            gs = searcher.graph(qn, q, args.R, k=args.k, dist=dist)
+            gs = searcher.graph(qn_h, q_h, args.R, k=args.k, dist=dist)
             ok = 1
         except Exception as e:  # noqa: BLE001 (reported in the JSON line)
             log(f"[bench] graph capture failed ({e!r}); timing eager launches")
             graph_failed.append(repr(e)[:200])
             gs, ok = None, 0
-        if world > 1:
-            t = torch.tensor([ok], dtype=torch.int32, device=device)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
-            ok = int(t.item())
-        if not ok:
+        if not agree(ok):
             if not graph_failed:
                 graph_failed.append("capture failed on another rank")
             del gs
             return timed_eager(dist)
+        g_d, g_a = (a.copy() for a in gs.run())
+        e_d, e_a = eager_step(dist)
+        same = agree(np.array_equal(g_d, e_d) and np.array_equal(g_a, e_a))
+        checks[f"graph_vs_eager_{dist}"] = "bitwise equal" if same else "DIFFER"
+        if not same:
+            log(f"[bench] graph replay differs from the eager step ({dist}); timing eager launches")
+            graph_failed.append("first replay differs from the eager step")
+            del gs
+            return timed_eager(dist)
+        h2d = h2d_ms(gs)
         out = None
         for _ in range(args.warmup):
             out = gs.run()
@@ -361,21 +489,12 @@ def main():
             t = torch.tensor([el], dtype=torch.float64, device=device)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
-        lib.lmi_timing_read(None, 0)
-        lib.lmi_timing_enable(1)
-        for _ in range(args.steps):
-            searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
-        torch.cuda.synchronize()
-        lib.lmi_timing_enable(0)
-        ms = (_lib.C.c_float * max(args.steps, 1))()
-        n_ev = lib.lmi_timing_read(ms, args.steps)
-        kms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
-        return el, kms, out
+        return el, kernel_ms(dist), out, h2d
 
     def timed(dist):
         """W untimed warmup steps, then K steps bracketed by barrier +
         synchronize; returns (max-over-ranks seconds, mean scan-kernel ms,
-        the last step's output)."""
+        the last step's output, (H2D ms, GB/s) or None)."""
         if use_graph:
             return timed_graph(dist)
         return timed_eager(dist)
@@ -383,7 +502,7 @@ def main():
     def timed_eager(dist):
         out = None
         for _ in range(args.warmup):
-            out = searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
+            out = eager_step(dist)
         lib.lmi_timing_read(None, 0)  # drop warmup records
         lib.lmi_timing_enable(1)
         if world > 1:
@@ -391,7 +510,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            out = searcher.search(qn, q, args.R, k=args.k, use_threshold=True, dist=dist)
+            out = eager_step(dist)
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()
@@ -405,15 +524,15 @@ def main():
                              device=device if torch.distributed.get_backend() == "nccl" else "cpu")
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
-        return el, kms, out
+        return el, kms, out, None
 
-    el, scan_ms, (dists, anns) = timed(args.dist)
+    el, scan_ms, (dists, anns), h2d = timed(args.dist)
     ms_step = el / args.steps * 1e3
     value = args.nq / (el / args.steps)
     # the other arithmetic, timed the same way (float64: the reference's on
     # float16 data, e.g. the real clip768 'emb'; float32: on float32 data)
     other = "f64" if args.dist == "f32" else "f32"
-    el_o, scan_ms_o, (dists_o, anns_o) = timed(other)
+    el_o, scan_ms_o, (dists_o, anns_o), _ = timed(other)
 
     # per-stage breakdown (separate, synchronised passes; not the timed loop)
     tm = {}
@@ -421,12 +540,20 @@ def main():
     for _ in range(3):
         searcher.search(qn, q, args.R, k=args.k, use_threshold=True, timings=tm, dist=args.dist)
     breakdown = {kk: round(v / 3, 3) for kk, v in tm.items()}
+    if h2d is not None:
+        breakdown = {"h2d": round(h2d[0], 3), **breakdown}
     # the optional exact-top-k semantics over the same probed buckets (untimed;
     # every rank takes part: with G > 1 the search has collectives)
     _, anns_x = searcher.search(qn, q, args.R, k=args.k, semantics="exact")
     classes, _ = router.topr(qn, args.R)
     classes = classes.cpu().numpy()
     byts, flops, rows = algorithmic_bytes(index, classes, args.nq)
+    # parity of the lists the step is built on (all ranks take part in the
+    # exchange; rank 0 checks), both arithmetics
+    lists = {}
+    for dd in (args.dist, other):
+        _, l_d, l_p, l_st = searcher.lists(qn, q, args.R, args.k, dist=dd)
+        lists[dd] = (l_d, l_p, int(l_st.item()))
     if rank != 0:
         if world > 1:
             torch.distributed.barrier()
@@ -458,10 +585,14 @@ def main():
                             for i in range(sample)]))
     recall_x = float(np.mean([len(set(anns_x[i][: args.k]) & set(truth[i])) / args.k
                               for i in range(sample)]))
+    parity = dict(checks)
+    for dd, (l_d, l_p, l_st) in lists.items():
+        parity[f"lists_{dd}"] = list_parity(index, x, q, classes, l_d, l_p, args.parity_sample,
+                                            dd == "f64")
+        parity[f"lists_{dd}"]["status"] = l_st
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        _, lists_d, _, _ = searcher.lists(qn, q, args.R, args.k, dist=args.dist)
-        cpu = cpu_baseline(index, q, classes, lists_d, args)
+        cpu = cpu_baseline(index, q, classes, lists[args.dist][0], args)
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "queries/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
@@ -476,10 +607,16 @@ def main():
                    "chunk_rows": args.chunk_rows},
         "roofline": roof, "cpu_baseline": cpu,
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
-        "recall_sample": sample, "breakdown_ms": breakdown,
+        "recall_sample": sample, "breakdown_ms": breakdown, "parity": parity,
+        "h2d": None if h2d is None else {"ms": round(h2d[0], 4), "gb_s": round(h2d[1], 1),
+                                         "bytes_per_rank": int(4 * (-(-args.nq // world)) * (96 + (384 if q16_exact else 768))),
+                                         "queries_staged_as": "f16" if q16_exact else "f32",
+                                         "in_step": True},
         "dist": args.dist,
-        "step": ("hip-graph replay" if use_graph and not graph_failed else
-                 "eager launches" + (f" (graph capture failed: {graph_failed[0]})" if graph_failed else "")),
+        "step": ("hip-graph replay (H2D of the host batch + search + D2H of the answer)"
+                 if use_graph and not graph_failed else
+                 "eager launches (H2D of the host batch + search + D2H)" +
+                 (f" (graph not used: {graph_failed[0]})" if graph_failed else "")),
         "other_dist": {"dist": other, "value": round(args.nq / (el_o / args.steps), 1),
                        "ms_per_step": round(el_o / args.steps * 1e3, 3),
                        "scan_kernel_ms": round(scan_ms_o, 4),

@@ -334,7 +334,7 @@ def search_via_lists(labels, ids, data_search, queries_search, classes, n_bucket
 # ---------------------------------------------------------------------------
 # comparator
 # ---------------------------------------------------------------------------
-def compare_lists(d_a, p_a, d_b, p_b, *, atol=1e-5, tie=1e-6):
+def compare_lists(d_a, p_a, d_b, p_b, *, atol=1e-5, tie=1e-6, stats=None):
     """Tie-aware comparison of per-row sorted lists.
 
     A row matches when (a) the finite masks agree and |d_a - d_b| <= atol
@@ -342,28 +342,42 @@ def compare_lists(d_a, p_a, d_b, p_b, *, atol=1e-5, tie=1e-6):
     tie: list b's id sits elsewhere in list a at a distance within `tie` of
     this position, or — if a does not hold it at all — its distance is within
     `tie` of a's last entry (the k-th place was cut inside a run of ties).
-    Returns the number of rows that do not match."""
+    Returns the number of rows that do not match.  `stats` (a dict) receives
+    the counts: rows, mismatched rows, and `tie_rows` = matching rows whose
+    ids differ somewhere, i.e. rows that matched only through the tie window
+    (`exact_tie_rows`: of those, rows where every differing id sits at
+    exactly the same distance in both lists)."""
     d_a = np.asarray(d_a, np.float64)
     k = d_a.shape[-1]
     d_a = d_a.reshape(-1, k)
     d_b = np.asarray(d_b, np.float64).reshape(-1, k)
     p_a = np.asarray(p_a).reshape(-1, k)
     p_b = np.asarray(p_b).reshape(-1, k)
-    bad = 0
+    bad = tie_rows = exact_tie_rows = 0
     for i in range(d_a.shape[0]):
         fa, fb = np.isfinite(d_a[i]), np.isfinite(d_b[i])
         if not np.array_equal(fa, fb) or np.any(np.abs(d_a[i][fa] - d_b[i][fb]) > atol):
             bad += 1
             continue
-        for j in np.nonzero(p_a[i] != p_b[i])[0]:
+        diff = np.nonzero(p_a[i] != p_b[i])[0]
+        exact = True
+        for j in diff:
             where = np.nonzero(p_a[i] == p_b[i][j])[0]
             if where.size:
-                ok = abs(d_a[i][where[0]] - d_a[i][j]) <= tie
+                gap = abs(d_a[i][where[0]] - d_a[i][j])
             else:
-                ok = abs(d_b[i][j] - d_a[i][fa][-1]) <= tie if fa.any() else False
-            if not ok:
+                gap = abs(d_b[i][j] - d_a[i][fa][-1]) if fa.any() else np.inf
+            exact = exact and gap == 0
+            if not gap <= tie:
                 bad += 1
                 break
+        else:
+            if diff.size:
+                tie_rows += 1
+                exact_tie_rows += 1 if exact else 0
+    if stats is not None:
+        stats.update(rows=int(d_a.shape[0]), mismatched=int(bad), tie_rows=int(tie_rows),
+                     exact_tie_rows=int(exact_tie_rows), tie=tie, atol=atol)
     return bad
 
 

@@ -42,7 +42,12 @@ def init_from_env(backend: Optional[str] = None):
     if backend == "nccl":
         torch.cuda.set_device(local)
     if not dist.is_initialized():
-        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+        # a rank that dies or raises inside a collective must not leave the
+        # others waiting forever: past this timeout the process group's
+        # watchdog aborts the waiting ranks (non-zero exit, no hang)
+        import datetime
+        timeout = datetime.timedelta(seconds=float(os.environ.get("LMI_DIST_TIMEOUT_S", "300")))
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout)
     return rank, world, local
 
 
@@ -119,19 +124,43 @@ def packed_lists(rows: int, k: int, f64: bool, device):
     return buf, d, pos, status
 
 
+def unpack_gathered(out: torch.Tensor, G: int, rows: int, k: int, f64: bool):
+    """Views of a gathered packed buffer [G * W] int32: (d [G, rows, k]
+    f32/f64, pos [G, rows, k] int32, status [G] int32) -- the layout
+    lmi_merge_topk_packed reads in place."""
+    W = out.numel() // G
+    o = out.view(G, W)
+    n = rows * k
+    nd = n * (2 if f64 else 1)
+    d = o[:, :nd].contiguous().view(torch.float64 if f64 else torch.float32).view(G, rows, k)
+    return d, o[:, nd:nd + n].reshape(G, rows, k), o[:, nd + n]
+
+
 def gather_merge_packed(buf: torch.Tensor, rows: int, k: int, f64: bool, group=None,
-                        status_out: Optional[torch.Tensor] = None):
+                        status_out: Optional[torch.Tensor] = None, merge: Optional[Callable] = None):
     """All-gather every rank's packed buffer (packed_lists) in one collective,
     then K3 over the gathered buffer in place (lmi_merge_topk_packed): the
     merged lists [rows, k] and the OR of every rank's status word, so all
     ranks fail together.  Two launches at any G (gather_merge's unpacking
-    copies and per-rank status ORs are ~10 small kernels at G = 8)."""
+    copies and per-rank status ORs are ~10 small kernels at G = 8).
+    `merge(gd, gp, k) -> (d, pos)` replaces K3 in the CPU gloo tests (the
+    gathered buffer is then unpacked with unpack_gathered)."""
     from . import _lib
     from .index import check, ptr
     G = dist.get_world_size(group)
     W = buf.numel()
     out = torch.empty((G * W,), dtype=torch.int32, device=buf.device)
     _all_gather(out, buf, group)
+    if merge is not None:
+        gd, gp, gs = unpack_gathered(out, G, rows, k, f64)
+        md, mp = merge(gd, gp, k)
+        st = gs[0:1].clone()
+        for g in range(1, G):
+            st = torch.bitwise_or(st, gs[g:g + 1])
+        if status_out is not None:
+            status_out.copy_(st)
+            st = status_out
+        return md.reshape(rows, k), mp.reshape(rows, k), st
     md = torch.empty((rows, k), dtype=torch.float64 if f64 else torch.float32, device=buf.device)
     mp = torch.empty((rows, k), dtype=torch.int32, device=buf.device)
     st = status_out if status_out is not None else torch.empty((1,), dtype=torch.int32,

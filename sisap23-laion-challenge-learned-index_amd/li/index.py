@@ -46,6 +46,17 @@ def _as_torch(x, device=None, dtype=None) -> torch.Tensor:
     return t.contiguous()
 
 
+def _rows_f32(x, device) -> torch.Tensor:
+    """x as float32 rows on `device` for a kernel that takes a row stride
+    (ldq / ldx): a device float32 tensor whose rows are contiguous is passed
+    as it is (e.g. a column slice of a staged query batch), anything else is
+    converted to a contiguous tensor."""
+    if isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.dim() == 2 and \
+            x.device == torch.device(device) and (x.stride(1) == 1 or x.shape[1] == 1):
+        return x
+    return _as_torch(x, device, torch.float32)
+
+
 def fp16_exact(x: torch.Tensor) -> bool:
     """True when every value of the float tensor round-trips through fp16."""
     x = x.float()
@@ -360,10 +371,18 @@ class DeviceRouter:
                 raise ValueError("expected ReLU after every hidden Linear")
         return cls(layers, device)
 
-    def topr(self, x: torch.Tensor, R: int, with_probs: bool = False, stream=None):
-        x = _as_torch(x, self.device, torch.float32)
+    def topr(self, x: torch.Tensor, R: int, with_probs: bool = False, stream=None, out=None):
+        """K1 TOPR: classes [nq, R] int32 (into `out` when given, a contiguous
+        int32 tensor of nq*R elements) and, with `with_probs`, their softmax
+        probabilities."""
+        x = _rows_f32(x, self.device)
         nq = x.shape[0]
-        classes = torch.empty((nq, R), dtype=torch.int32, device=self.device)
+        if out is not None:
+            if out.dtype != torch.int32 or out.numel() != nq * R or not out.is_contiguous():
+                raise ValueError("out must be a contiguous int32 tensor of nq*R elements")
+            classes = out.view(nq, R)
+        else:
+            classes = torch.empty((nq, R), dtype=torch.int32, device=self.device)
         probs = torch.empty((nq, R), dtype=torch.float32, device=self.device) if with_probs else None
         s = stream if stream is not None else _lib.stream_handle(self.device)
         check("lmi_router", _lib.load().lmi_router(ptr(x), nq, x.stride(0), C.byref(self._desc), R,
@@ -371,7 +390,7 @@ class DeviceRouter:
         return classes, probs
 
     def argmax(self, x: torch.Tensor, stream=None) -> torch.Tensor:
-        x = _as_torch(x, self.device, torch.float32)
+        x = _rows_f32(x, self.device)
         nq = x.shape[0]
         out = torch.empty((nq,), dtype=torch.int32, device=self.device)
         s = stream if stream is not None else _lib.stream_handle(self.device)
@@ -383,12 +402,21 @@ class DeviceRouter:
 # ---------------------------------------------------------------------------
 # scan / merge / replay
 # ---------------------------------------------------------------------------
+def _workspace(ws, need: int, what: str) -> torch.Tensor:
+    if ws.dtype != torch.uint8 or ws.numel() < need:
+        raise ValueError(f"{what} workspace too small ({ws.numel()} < {need} bytes)")
+    return ws
+
+
 def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
-                qmode: Optional[int] = None, stream=None, out=None):
+                qmode: Optional[int] = None, stream=None, out=None, ws=None):
     """K2 on one shard.  Returns (d [nq,R,k] f32, pos [nq,R,k] int32, status int32 tensor);
-    `out` = such a triple to write into (the status word zeroed by the caller)."""
+    `out` = such a triple to write into (the status word zeroed by the caller);
+    `ws` = a caller-owned uint8 workspace (default: the index's cached one,
+    which a later call with a larger batch may replace — a captured graph
+    passes its own)."""
     lib = _lib.load()
-    q = _as_torch(q, index.device, torch.float32)
+    q = _rows_f32(q, index.device)
     classes = _as_torch(classes, index.device, torch.int32)
     nq, R = classes.shape
     if q.shape[0] != nq or q.shape[1] != index.d:
@@ -401,7 +429,10 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
         status = torch.zeros((1,), dtype=torch.int32, device=index.device)
     else:
         out_d, out_pos, status = out
-    ws = index.workspace(nq, R, k, qmode)
+    if ws is None:
+        ws = index.workspace(nq, R, k, qmode)
+    else:
+        _workspace(ws, lib.lmi_scan_workspace_bytes(C.byref(index.desc), nq, R, k, qmode), "scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
     check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(index.desc), ptr(q), nq, q.stride(0),
                                                  ptr(classes), R, k, qmode, ptr(out_d),
@@ -411,12 +442,13 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
 
 def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
                     qmode: Optional[int] = None, eps: float = _lib.LMI_REFINE_EPS, stream=None,
-                    fallback_count: bool = False, out=None):
+                    fallback_count: bool = False, out=None, ws=None):
     """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
     arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
-    (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback])."""
+    (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback]);
+    `out` and `ws` as bucket_topk."""
     lib = _lib.load()
-    q = _as_torch(q, index.device, torch.float32)
+    q = _rows_f32(q, index.device)
     classes = _as_torch(classes, index.device, torch.int32)
     nq, R = classes.shape
     if q.shape[0] != nq or q.shape[1] != index.d:
@@ -430,10 +462,13 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     else:
         out_d, out_pos, status = out
     need = lib.lmi_scan_f64_workspace_bytes(C.byref(index.desc), nq, R, k, qmode)
-    ws = index._ws.get("f64")
-    if ws is None or ws.numel() < need:
-        ws = torch.empty(max(need, 256), dtype=torch.uint8, device=index.device)
-        index._ws["f64"] = ws
+    if ws is None:
+        ws = index._ws.get("f64")
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(max(need, 256), dtype=torch.uint8, device=index.device)
+            index._ws["f64"] = ws
+    else:
+        _workspace(ws, need, "float64 scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
     check("lmi_bucket_topk_f64", lib.lmi_bucket_topk_f64(
         C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(classes), R, k, qmode, float(eps),
@@ -594,11 +629,12 @@ class Searcher:
         return mode
 
     def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool, lap=None,
-              status_out=None):
+              status_out=None, ws=None):
         """K2 on this shard (+ all-gather and K3 for G > 1 ranks, the status
         words riding along so every rank sees every rank's bits).  `lap`
         (measurement only) is called after the scan and after the exchange.
-        `status_out` (a zeroed device int32 word): the status lands there."""
+        `status_out` (a zeroed device int32 word): the status lands there.
+        `ws`: a caller-owned scan workspace (GraphedSearch's)."""
         out = None
         if self.index.world == 1 and status_out is not None:
             nq, R = classes.shape
@@ -615,9 +651,10 @@ class Searcher:
             out = (dv.view(nq, R, k_list), pv.view(nq, R, k_list), sv)
         if f64:
             d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode,
-                                             out=out)
+                                             out=out, ws=ws)
         else:
-            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode, out=out)
+            d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode, out=out,
+                                         ws=ws)
         if lap:
             lap("scan")
         if self.index.world > 1:
@@ -634,7 +671,7 @@ class Searcher:
         """Device part: router + scan (+ RCCL merge).  Returns device tensors."""
         if classes is None:
             classes = self.route(q_nav, R)
-        q_search = _as_torch(q_search, self.index.device, torch.float32)
+        q_search = _rows_f32(q_search, self.index.device)
         d, pos, status = self._scan(q_search, classes, k_list, self.qmode(q_search), dist == "f64")
         return classes, d, pos, status
 
@@ -643,8 +680,7 @@ class Searcher:
         the classes are all-gathered (li.dist.route_sharded)."""
         if self.index.world > 1:
             from .dist import route_sharded
-            return route_sharded(self.router, _as_torch(q_nav, self.index.device, torch.float32), R,
-                                 self.group)
+            return route_sharded(self.router, _rows_f32(q_nav, self.index.device), R, self.group)
         return self.router.topr(q_nav, R)[0]
 
     def _device_tables(self):
@@ -658,7 +694,8 @@ class Searcher:
         return t
 
     def graph(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "GraphedSearch":
-        """The step captured as a HIP graph (GraphedSearch): same results as
+        """The step captured as a HIP graph (GraphedSearch), from the batch in
+        host memory to the answer in host memory: same results as
         search(..., semantics="reference", replay_on="device")."""
         return GraphedSearch(self, q_nav, q_search, R, k, **kw)
 
@@ -714,7 +751,7 @@ class Searcher:
             return t0
 
         t0 = time.perf_counter()
-        q_search = _as_torch(q_search, dev, torch.float32)
+        q_search = _rows_f32(q_search, dev)
         qmode = self.qmode(q_search)
         if classes is None:
             classes = self.route(q_nav, R)
@@ -823,60 +860,151 @@ class Searcher:
         return out
 
 
+def _host_array(x) -> np.ndarray:
+    """A query batch (numpy, or a torch tensor on any device) as a host array."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
 class GraphedSearch:
-    """One search step (router + scan [+ all-gather + K3] + device replay +
-    the D2H of the answer and of the status words) captured once as a HIP
-    graph and replayed per batch: the ~25 launches of the step go to the GPU
-    as one graph launch, with no host work between them (the host gap between
-    steps in the kernel trace).
+    """One search step captured once as a HIP graph and replayed per batch,
+    from queries in HOST memory to the answer in host memory, as the
+    reference's timer sees it (search.py:116-141; its queries are host arrays,
+    search.py:49, :85-87):
 
-    The graph reads the query tensors it was captured with: to search another
-    batch of the same shape, copy it into `q_nav` / `q_search` first.  The
-    query precision class (fp16-exact or not, Searcher.qmode) is fixed at
-    capture; a batch that is not fp16-exact under an fp16 capture is detected
-    by the scan's status word and answered by the eager path instead.
-    `run()` returns numpy views of the graph's pinned output buffers, valid
-    until the next run (copy them to keep them)."""
+        H2D of the staged batch (pinned host rows)
+        -> router (K1) -> scan (K2) [-> all-gather + K3] -> replay (K4)
+        -> D2H of the answer and of both status words
 
-    def __init__(self, searcher: "Searcher", q_nav: torch.Tensor, q_search: torch.Tensor, R: int,
+    The ~25 launches and the copies go to the GPU as one graph launch, with no
+    host work between them.
+
+    Staging (`stage`, outside the step, like the reference's h5 loads before
+    its timer): the batch is written into a pinned host buffer laid out per
+    rank block as [pca96 f32 (per x 96) | clip768 (per x d) | classes (per x
+    R, G > 1 only)].  The clip768 rows are staged as fp16 when the index is
+    fp16 and every query value is fp16-representable (checked on the host at
+    staging; float16 input is exact by construction): half the bytes over
+    PCIe, widened to float32 on the device.  A batch that is not fp16-exact
+    under an fp16 capture is answered by the eager path instead.
+
+    G > 1 ranks: rank g uploads only its block (1/G of the batch), routes its
+    queries into the block's classes, and ONE all-gather over xGMI hands every
+    rank the whole batch and all classes; then the striped scan and the list
+    exchange as in Searcher.search.
+
+    The graph owns its scan workspace (index._ws may be replaced by a later
+    eager call with a bigger batch).  `run()` returns numpy views
+    of the graph's pinned output buffer, valid until the next run."""
+
+    def __init__(self, searcher: "Searcher", q_nav, q_search, R: int,
                  k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32"):
         s = searcher
-        dev = s.index.device
+        ix = s.index
+        dev = ix.device
+        lib = _lib.load()
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
         self.use_threshold, self.dist = use_threshold, dist
-        self.q_nav = _as_torch(q_nav, dev, torch.float32)
-        self.q_search = _as_torch(q_search, dev, torch.float32)
-        if k_round > _lib.LMI_MAX_K or (s.index.world > 1 and
-                                       torch.distributed.get_backend(s.group) != "nccl"):
+        G = ix.world
+        if k_round > _lib.LMI_MAX_K or (G > 1 and torch.distributed.get_backend(s.group) != "nccl"):
             raise ValueError("graph capture needs k_round <= 16 and RCCL collectives")
-        self.qmode = s.qmode(self.q_search)
+        nav = _host_array(q_nav)
+        qs = _host_array(q_search)
+        nq, d, dn = int(qs.shape[0]), ix.d, int(nav.shape[1])
+        if qs.shape != (nq, d) or nav.shape[0] != nq:
+            raise ValueError("query shapes do not match the index")
+        self.nq, self.d, self.dn = nq, d, dn
+        # the batch's precision class is decided on the host, once per capture
+        self.f16_up = ix.storage == "f16" and d % 2 == 0 and (
+            qs.dtype == np.float16 or _np_fp16_exact(qs))
+        self.qmode = _lib.LMI_Q_F16 if self.f16_up else _lib.LMI_Q_F32
         f64 = dist == "f64"
+        self.per = per = -(-nq // G)
+        self.wq = wq = d // 2 if self.f16_up else d          # int32 words per staged row
+        self.bw = bw = per * dn + per * wq + (per * R if G > 1 else 0)
+        pin = torch.cuda.is_available()
+        self.h_blk = torch.zeros((G, bw), dtype=torch.int32, pin_memory=pin)
+        if not self.stage(nav, qs):
+            raise ValueError("staging failed")
+        need = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
+            C.byref(ix.desc), nq, R, k_round, self.qmode)
+        self.ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
+        self.d_blk = torch.empty((bw,), dtype=torch.int32, device=dev)
+        self.d_all = torch.empty((G, bw), dtype=torch.int32, device=dev) if G > 1 else None
+        self.q32 = torch.empty((G * per, d), dtype=torch.float32, device=dev) \
+            if (self.f16_up or G > 1) else None
+        self.cls = torch.empty((G * per, R), dtype=torch.int32, device=dev) if G > 1 else None
         bsz, p2id = s._device_tables()
-
-        nq = self.q_search.shape[0]
         self.w = k_round if R == 1 else k
+        g = ix.rank
+        copy_stream = torch.cuda.Stream(dev)
 
         def step():
-            # the answer and both status words land in one buffer, copied to
-            # the host in one D2H (answer_buffer)
             ans = answer_buffer(nq, self.w, dev)
-            classes = s.route(self.q_nav, R)
-            d, pos, _ = s._scan(self.q_search, classes, k_round, self.qmode, f64,
-                                status_out=ans[3][0:1])
-            replay_device(classes, d, pos, k_round=k_round, k_final=k, bucket_size=bsz,
+            main = torch.cuda.current_stream(dev)
+            if G == 1:
+                # pca96 rows first; the clip768 rows come in on a second stream
+                # while the router runs
+                self.d_blk[:per * dn].copy_(self.h_blk[0, :per * dn], non_blocking=True)
+                copy_stream.wait_stream(main)
+                with torch.cuda.stream(copy_stream):
+                    self.d_blk[per * dn:].copy_(self.h_blk[0, per * dn:], non_blocking=True)
+                classes = s.router.topr(self.d_blk[:per * dn].view(torch.float32).view(per, dn), R)[0]
+                main.wait_stream(copy_stream)
+                sv = self.d_blk[per * dn:per * dn + per * wq]
+                if self.f16_up:
+                    q = self.q32
+                    q.copy_(sv.view(torch.float16).view(per, d))
+                else:
+                    q = sv.view(torch.float32).view(per, d)
+            else:
+                # this rank's block: upload, route its queries into the block,
+                # one all-gather of every block (queries + classes)
+                from .dist import _all_gather
+                self.d_blk.copy_(self.h_blk[g], non_blocking=True)
+                s.router.topr(self.d_blk[:per * dn].view(torch.float32).view(per, dn), R,
+                              out=self.d_blk[per * (dn + wq):])
+                _all_gather(self.d_all.view(-1), self.d_blk, s.group)
+                sv = self.d_all[:, per * dn:per * (dn + wq)]
+                if self.f16_up:
+                    self.q32.view(G, per, d).copy_(sv.view(torch.float16).view(G, per, d))
+                else:
+                    self.q32.view(G, per, d).copy_(sv.view(torch.float32).view(G, per, d))
+                self.cls.view(G, per, R).copy_(self.d_all[:, per * (dn + wq):].view(G, per, R))
+                q = self.q32[:nq]
+                classes = self.cls[:nq]
+            d_, pos, _ = s._scan(q, classes, k_round, self.qmode, f64, status_out=ans[3][0:1],
+                                 ws=self.ws)
+            replay_device(classes, d_, pos, k_round=k_round, k_final=k, bucket_size=bsz,
                           pos_to_id=p2id, use_threshold=use_threshold,
                           out=(ans[1], ans[2], ans[3][1:2]))
             return ans[0]
 
         # warm up on a side stream (allocations, kernel attributes, RCCL
-        # communicators), then capture
+        # communicators), then capture.  G > 1: the ranks agree that every
+        # rank's warm-up succeeded before any rank captures (a rank that
+        # raised before entering a collective would otherwise leave the others
+        # waiting in the next one; a rank that fails inside a collective is
+        # ended by the process group's timeout, li.dist.init_from_env)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                buf = step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        torch.cuda.synchronize(dev)
+        err = None
+        try:
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    buf = step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+        except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
+            err = e
+        if G > 1:
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
+            if int(ok.item()) == 0:
+                raise RuntimeError(f"graph warm-up failed on some rank: {err!r}")
+        elif err is not None:
+            raise err
         self.h = torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
@@ -885,18 +1013,76 @@ class GraphedSearch:
         self._keep = buf
         torch.cuda.synchronize(dev)
 
-    def run(self):
-        """Replay the step -> (dists f64 [nq, w], anns uint32 [nq, w])."""
-        dev = self.searcher.index.device
+    def stage(self, q_nav, q_search) -> bool:
+        """Write a batch (host or device arrays of the captured shape) into the
+        pinned staging buffer.  False if it cannot be staged in the captured
+        precision (clip768 values not fp16-representable under an fp16
+        capture): run() then answers it on the eager path."""
+        nav = _host_array(q_nav).astype(np.float32, copy=False)
+        qs = _host_array(q_search)
+        nq, d, dn, per, wq = self.nq, self.d, self.dn, self.per, self.wq
+        if nav.shape != (nq, dn) or qs.shape != (nq, d):
+            raise ValueError("a staged batch must have the captured shape")
+        if self.f16_up:
+            if qs.dtype == np.float16:
+                q16 = qs
+            else:
+                q32 = qs.astype(np.float32, copy=False)
+                q16 = q32.astype(np.float16)
+                if not np.array_equal(q16.astype(np.float32), q32):
+                    return False
+            src, sdt = q16, np.float16
+        else:
+            src, sdt = qs.astype(np.float32, copy=False), np.float32
+        blk = self.h_blk.numpy()
+        for g in range(blk.shape[0]):
+            lo, hi = min(nq, g * per), min(nq, (g + 1) * per)
+            nv = blk[g, :per * dn].view(np.float32).reshape(per, dn)
+            nv[:hi - lo] = nav[lo:hi]
+            nv[hi - lo:] = 0
+            sv = blk[g, per * dn:per * (dn + wq)].view(sdt).reshape(per, d)
+            sv[:hi - lo] = src[lo:hi]
+            sv[hi - lo:] = 0
+        self._staged = (nav, qs)
+        return True
+
+    def upload_bytes(self) -> int:
+        """Bytes this rank moves host -> device per step."""
+        per, dn, wq = self.per, self.dn, self.wq
+        return 4 * per * (dn + wq)
+
+    def run(self, q_nav=None, q_search=None):
+        """Replay the step (after staging a new batch, if given) -> (dists f64
+        [nq, w], anns uint32 [nq, w])."""
+        s = self.searcher
+        dev = s.index.device
+        if q_nav is not None or q_search is not None:
+            if q_nav is None or q_search is None:
+                raise ValueError("stage both q_nav and q_search")
+            if not self.stage(q_nav, q_search):
+                return self._eager(q_nav, q_search)
         self.graph.replay()
         torch.cuda.current_stream(dev).synchronize()
-        hd, ha, st, rst = answer_views(self.h, self.q_search.shape[0], self.w)
+        hd, ha, st, rst = answer_views(self.h, self.nq, self.w)
         if st & _lib.LMI_STATUS_INTERNAL or rst:
             raise RuntimeError(f"search: internal status {st}/{rst}")
-        if st & _lib.LMI_STATUS_QUERY_NOT_F16:
-            # captured for fp16-exact queries; this batch is not: the eager path
-            self.searcher._qcheck = None
-            return self.searcher.search(self.q_nav, self.q_search, self.R, k=self.k,
-                                        k_round=self.k_round, use_threshold=self.use_threshold,
-                                        dist=self.dist)
         return hd, ha
+
+    def _eager(self, q_nav, q_search):
+        dev = self.searcher.index.device
+        self.searcher._qcheck = None
+        return self.searcher.search(_as_torch(_host_array(q_nav), dev, torch.float32),
+                                    _as_torch(_host_array(q_search), dev, torch.float32),
+                                    self.R, k=self.k, k_round=self.k_round,
+                                    use_threshold=self.use_threshold, dist=self.dist)
+
+
+def _np_fp16_exact(x: np.ndarray) -> bool:
+    """True when every value of a host array round-trips through fp16."""
+    x = np.asarray(x)
+    if x.dtype == np.float16:
+        return True
+    x32 = x.astype(np.float32, copy=False)
+    if x.dtype != np.float32 and not np.array_equal(x32.astype(x.dtype), x):
+        return False
+    return bool(np.array_equal(x32.astype(np.float16).astype(np.float32), x32))

@@ -1,0 +1,48 @@
+"""One rank of tests/test_gpu_dist.py: the PRODUCT multi-GPU path
+(Searcher.search: route_sharded, K2 into the packed send buffer,
+gather_merge_packed -> lmi_merge_topk_packed, device replay) with
+torch.distributed over gloo, two ranks sharing the box's one GPU (RCCL refuses
+two ranks on one device; gloo stages the collectives through host memory).
+Rank 0 writes the answers to the .npz named on the command line."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"), HERE]
+
+
+def main(out_path):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import workloads
+    from li.dist import init_from_env
+    from li.index import DeviceIndex, DeviceRouter, Searcher
+    rank, world, _ = init_from_env(backend="gloo")
+    torch.cuda.set_device(0)
+    w = workloads.clustered(n=8000, nq=240, C=16, seed=61, label_mode="skewed")
+    ix = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=512, device="cuda:0", rank=rank,
+                     world=world)
+    s = Searcher(ix, DeviceRouter(w["layers"], device="cuda:0"))
+    qn = torch.from_numpy(w["qn"]).cuda()
+    q = torch.from_numpy(w["q"]).cuda()
+    res = {}
+    for dist_ in ("f32", "f64"):
+        for R in (1, 4):
+            d, a = s.search(qn, q, R, k=10, dist=dist_)
+            res[f"{dist_}_R{R}_d"], res[f"{dist_}_R{R}_a"] = d, a
+        _, ld, lp, st = s.lists(qn, q, 4, 10, dist=dist_)
+        res[f"{dist_}_lists_d"], res[f"{dist_}_lists_p"] = ld.cpu().numpy(), lp.cpu().numpy()
+        res[f"{dist_}_lists_st"] = np.array([int(st.item())])
+    d, a = s.search(qn, q, 4, k=10, semantics="exact")
+    res["exact_d"], res["exact_a"] = d, a
+    if rank == 0:
+        np.savez(out_path, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

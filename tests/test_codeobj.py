@@ -22,9 +22,9 @@ LIB = os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd", "li", "lib
 OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
 
 
-def _disassembly(tmp_path):
+def _disassembly(tmp_path, lib=LIB):
     so = tmp_path / "lib.so"
-    shutil.copy(LIB, so)
+    shutil.copy(lib, so)
     subprocess.run([OBJDUMP, "--offloading", str(so)], cwd=tmp_path, check=True,
                    capture_output=True)
     text = []
@@ -52,7 +52,24 @@ def _functions(dis):
 @pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)),
                     reason="needs the built library and llvm-objdump")
 def test_no_spill_inside_scan3_mfma_stream(tmp_path):
-    funcs = _functions(_disassembly(tmp_path))
+    _check_scan3(tmp_path, LIB)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="needs llvm-objdump")
+def test_mapped_library_scan3_mfma_stream(tmp_path):
+    """The same guard on the library this GPU process actually maps (VERDICT
+    r2: the CPU test checks only the container-built file)."""
+    from li import _lib
+    _lib.load()
+    with open("/proc/self/maps") as f:
+        mapped = {line.split()[-1] for line in f if line.rstrip().endswith("/" + _lib.LIB_NAME)}
+    assert len(mapped) == 1, mapped
+    _check_scan3(tmp_path, mapped.pop())
+
+
+def _check_scan3(tmp_path, lib):
+    funcs = _functions(_disassembly(tmp_path, lib))
     scan3 = {k: v for k, v in funcs.items() if "scan3_kernel" in k}
     assert scan3, "no scan3_kernel in the code object"
     for name, ins in scan3.items():

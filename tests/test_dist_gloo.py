@@ -1,6 +1,8 @@
 """Multi-process (gloo, CPU) test of the multi-GPU protocol of li/dist.py:
 corpus striped over the ranks (BucketLayout.shard), per-shard lists keyed by
-global position, all_gather_into_tensor, merge by (distance, position).  The
+global position, all_gather_into_tensor, merge by (distance, position) -- both
+through gather_merge and through the product's packed exchange
+(packed_lists + gather_merge_packed, the layout lmi_merge_topk_packed reads).  The
 per-shard lists and the merge are computed by the oracle here (no HIP device);
 on the GPU they are lmi_bucket_topk and lmi_merge_topk (tests/test_gpu_parity.py
 checks that the GPU merge equals the single-shard result bitwise)."""
@@ -66,15 +68,34 @@ def _worker(rank, world, port, result_path):
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import lmi_oracle as O
     import workloads
-    from li.dist import gather_merge, init_from_env, route_sharded
+    from li.dist import (gather_merge, gather_merge_packed, init_from_env, packed_lists,
+                         route_sharded)
     from li.index import BucketLayout
     init_from_env(backend="gloo")
     w = workloads.clustered(n=2500, nq=80, C=16, seed=31, label_mode="skewed")
     R, k, C = 3, 10, 16
+    nq = w["q"].shape[0]
     classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
     gpos, _ = BucketLayout.from_labels(w["labels"], C).shard(rank, world)
     d, p = _shard_lists(w, classes, R, k, C, gpos)
     md, mp_ = gather_merge(torch.from_numpy(d), torch.from_numpy(p), k, merge=_oracle_merge)
+    # the product's packed exchange (Searcher._scan at G > 1): the lists and the
+    # status word written into this rank's send buffer (packed_lists), one
+    # all-gather, the gathered buffer unpacked in lmi_merge_topk_packed's layout
+    packed_ok = True
+    for f64 in (False, True):
+        buf, dv, pv, sv = packed_lists(nq * R, k, f64, "cpu")
+        dv.copy_(torch.from_numpy(d.astype(np.float64 if f64 else np.float32)).view(-1))
+        pv.copy_(torch.from_numpy(p).view(-1))
+        sv.fill_(1 << rank)
+        st_out = torch.zeros(1, dtype=torch.int32)
+        pd_, pp_, pst = gather_merge_packed(buf, nq * R, k, f64, status_out=st_out,
+                                            merge=lambda gd, gp, kk: _oracle_merge(
+                                                gd.view(-1, nq, R, kk), gp.view(-1, nq, R, kk), kk))
+        packed_ok = packed_ok and np.array_equal(pd_.numpy().astype(np.float32).reshape(nq, R, k),
+                                                 md.numpy()) and \
+            np.array_equal(pp_.numpy().reshape(nq, R, k), mp_.numpy()) and \
+            int(st_out[0]) == (1 << world) - 1 and pst is st_out
     # float64 lists (lmi_bucket_topk_f64) through the same collective, with
     # every rank's status word OR-ed into the result on every rank
     md64, mp64, st = gather_merge(torch.from_numpy(d.astype(np.float64)), torch.from_numpy(p), k,
@@ -97,7 +118,7 @@ def _worker(rank, world, port, result_path):
         # shape-independent and is checked bitwise in test_gpu_parity.py)
         ok = O.compare_lists(fd, fp, md.numpy(), mp_.numpy()) == 0 and \
             np.array_equal(np.isfinite(md.numpy()), np.isfinite(fd)) and \
-            np.array_equal(routed, classes) and f64_ok
+            np.array_equal(routed, classes) and f64_ok and packed_ok
         with open(result_path, "w") as f:
             f.write("ok" if ok else "mismatch")
     dist.barrier()

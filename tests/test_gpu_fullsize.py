@@ -116,3 +116,63 @@ def test_configs2_10m_lists_match_oracle(w10m, dist):
         ref_p[sel[:, None].repeat(R, 1)[hit], np.nonzero(hit)[1]] = sp[hit] + a
     tie, atol = (TIE32, 1e-5) if dist == "f32" else (TIE64, 1e-12)
     assert O.compare_lists(ref_d, ref_p, d[qs], pos[qs], atol=atol, tie=tie) == 0
+
+
+def _packed_shards(x, labels, q, classes, k, f64, G, chunk_rows, C=122):
+    """The G > 1 product path run one shard at a time on this GPU: rank g's
+    DeviceIndex (slice g of every bucket), K2 into its packed send buffer
+    (li.dist.packed_lists), the buffers concatenated as all_gather_into_tensor
+    leaves them, K3 in place (lmi_merge_topk_packed) -> merged lists + status."""
+    from li import _lib
+    from li.dist import packed_lists
+    from li.index import check, ptr
+    nq, R = classes.shape
+    rows = nq * R
+    scan = bucket_topk_f64 if f64 else bucket_topk
+    bufs = []
+    for g in range(G):
+        ix = DeviceIndex(x, labels, C, chunk_rows=chunk_rows, rank=g, world=G)
+        buf, dv, pv, sv = packed_lists(rows, k, f64, q.device)
+        scan(ix, q, classes, k, out=(dv.view(nq, R, k), pv.view(nq, R, k), sv))
+        torch.cuda.synchronize()
+        bufs.append(buf)
+        del ix
+        torch.cuda.empty_cache()
+    gathered = torch.cat(bufs)
+    del bufs
+    md = torch.empty((rows, k), dtype=torch.float64 if f64 else torch.float32, device=q.device)
+    mp = torch.empty((rows, k), dtype=torch.int32, device=q.device)
+    st = torch.full((1,), -1, dtype=torch.int32, device=q.device)
+    check("lmi_merge_topk_packed", _lib.load().lmi_merge_topk_packed(
+        ptr(gathered), G, gathered.numel() // G, rows, k, int(f64), ptr(md), ptr(mp), ptr(st),
+        _lib.stream_handle(q.device)))
+    return md.view(nq, R, k), mp.view(nq, R, k), int(st.item())
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dist", ["f32", "f64"])
+def test_configs3_eight_shards_equal_one_gpu(w10m, dist):
+    """BASELINE configs[3] (10M, 8 GPUs) exercised on one GPU: the eight
+    stripes built one at a time with the 8-GPU chunk size (2048 rows), each
+    scanned into its packed all-gather buffer, merged by K3 -> bitwise the
+    single-GPU lists; the device replay over them -> bitwise the single-GPU
+    answer."""
+    from li.index import replay_device
+    w = w10m
+    ix, s = w["ix"], w["s"]
+    R, k = 4, 10
+    classes = w["router"].topr(w["qn"], R)[0]
+    f64 = dist == "f64"
+    scan = bucket_topk_f64 if f64 else bucket_topk
+    d1, p1, st1 = scan(ix, w["q"], classes, k)
+    assert int(st1.item()) == 0
+    md, mp, st = _packed_shards(w["x"], w["labels"], w["q"], classes, k, f64, 8, 2048)
+    assert st == 0
+    assert torch.equal(md, d1) and torch.equal(mp, p1)
+    bsz, p2id = s._device_tables()
+    a1 = replay_device(classes, d1, p1, k_round=10, k_final=k, bucket_size=bsz, pos_to_id=p2id,
+                       use_threshold=True)
+    a8 = replay_device(classes, md, mp, k_round=10, k_final=k, bucket_size=bsz, pos_to_id=p2id,
+                       use_threshold=True)
+    assert int(a1[2].item()) == 0 and int(a8[2].item()) == 0
+    assert torch.equal(a1[0], a8[0]) and torch.equal(a1[1], a8[1])

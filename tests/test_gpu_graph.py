@@ -1,7 +1,9 @@
-"""The step captured as a HIP graph (Searcher.graph / GraphedSearch) answers
-exactly as the eager Searcher.search, replay after replay, for new batches
-copied into its query buffers, and falls back to the eager path for a batch
-that is not fp16-exact under an fp16 capture."""
+"""The step captured as a HIP graph (Searcher.graph / GraphedSearch), from the
+batch in host memory (staged in pinned buffers, uploaded inside the step) to
+the answer in host memory, answers exactly as the eager Searcher.search,
+replay after replay, for new batches staged between replays; a batch that is
+not fp16-exact under an fp16 capture is answered by the eager path; and the
+graph keeps working after eager calls that grow the index's own workspace."""
 import numpy as np
 import pytest
 import torch
@@ -26,7 +28,8 @@ def test_graph_equals_eager(setup, dist, R):
     qn = torch.from_numpy(w["qn"]).cuda()
     q = torch.from_numpy(w["q"]).cuda()
     d0, a0 = s.search(qn, q, R, k=10, dist=dist)
-    g = s.graph(qn, q, R, k=10, dist=dist)
+    g = s.graph(w["qn"], w["q"], R, k=10, dist=dist)   # host batch, staged
+    assert g.f16_up
     for _ in range(3):
         d1, a1 = g.run()
         np.testing.assert_array_equal(d1, d0)
@@ -35,19 +38,57 @@ def test_graph_equals_eager(setup, dist, R):
 
 def test_graph_new_batch_and_inexact_queries(setup):
     w, s = setup
-    qn = torch.from_numpy(w["qn"]).cuda()
-    q = torch.from_numpy(w["q"]).cuda()
-    g = s.graph(qn.clone(), q.clone(), 4, k=10)
-    perm = torch.randperm(q.shape[0], generator=torch.Generator().manual_seed(0))
-    g.q_nav.copy_(qn[perm.cuda()])
-    g.q_search.copy_(q[perm.cuda()])
-    d1, a1 = g.run()
-    d0, a0 = s.search(qn[perm.cuda()], q[perm.cuda()], 4, k=10)
+    g = s.graph(w["qn"], w["q"], 4, k=10)
+    perm = np.random.default_rng(0).permutation(w["q"].shape[0])
+    qn2, q2 = w["qn"][perm], w["q"][perm]
+    d1, a1 = g.run(qn2, q2)
+    d0, a0 = s.search(torch.from_numpy(qn2).cuda(), torch.from_numpy(q2).cuda(), 4, k=10)
     np.testing.assert_array_equal(d1, d0)
     np.testing.assert_array_equal(a1, a0)
-    # not fp16-exact: the capture's fp16 path flags it, the eager fp32 path answers
-    g.q_search.add_(1e-5)
-    d2, a2 = g.run()
-    d3, a3 = s.search(g.q_nav, g.q_search, 4, k=10)
+    # float16 input stages as it is
+    d1, a1 = g.run(qn2, q2.astype(np.float16))
+    np.testing.assert_array_equal(d1, d0)
+    np.testing.assert_array_equal(a1, a0)
+    # not fp16-exact: the fp16 capture cannot stage it, the eager fp32 path answers
+    q3 = q2 + np.float32(1e-5)
+    d2, a2 = g.run(qn2, q3)
+    d3, a3 = s.search(torch.from_numpy(qn2).cuda(), torch.from_numpy(q3).cuda(), 4, k=10)
     np.testing.assert_array_equal(d2, d3)
     np.testing.assert_array_equal(a2, a3)
+    # and the graph still answers fp16-exact batches afterwards
+    d4, a4 = g.run(w["qn"], w["q"])
+    d5, a5 = s.search(torch.from_numpy(w["qn"]).cuda(), torch.from_numpy(w["q"]).cuda(), 4, k=10)
+    np.testing.assert_array_equal(d4, d5)
+    np.testing.assert_array_equal(a4, a5)
+
+
+def test_graph_f32_staging(setup):
+    """A batch that is not fp16-exact at capture stages as float32 rows."""
+    w, s = setup
+    q = w["q"] + np.float32(1e-5)
+    g = s.graph(w["qn"], q, 4, k=10)
+    assert not g.f16_up
+    d0, a0 = s.search(torch.from_numpy(w["qn"]).cuda(), torch.from_numpy(q).cuda(), 4, k=10)
+    d1, a1 = g.run()
+    np.testing.assert_array_equal(d1, d0)
+    np.testing.assert_array_equal(a1, a0)
+
+
+@pytest.mark.parametrize("dist", ["f32", "f64"])
+def test_graph_survives_workspace_growth(setup, dist):
+    """an eager call with a bigger batch replaces the index's cached
+    scan workspace; the graph owns its own, so its replays stay correct."""
+    w, s = setup
+    g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist)
+    d0, a0 = g.run()
+    d0, a0 = d0.copy(), a0.copy()
+    big = 4
+    qn_big = torch.from_numpy(np.tile(w["qn"], (big, 1))).cuda()
+    q_big = torch.from_numpy(np.tile(w["q"], (big, 1))).cuda()
+    s.search(qn_big, q_big, 7, k=10, dist=dist)      # more pairs: a bigger workspace
+    torch.cuda.empty_cache()
+    junk = torch.full((64 << 20,), 7, dtype=torch.int32, device="cuda")  # reuse freed memory
+    d1, a1 = g.run()
+    del junk
+    np.testing.assert_array_equal(d1, d0)
+    np.testing.assert_array_equal(a1, a0)

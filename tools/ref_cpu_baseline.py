@@ -44,19 +44,23 @@ def child(size: str, R: int, threads: int, dtype: str, nq: int):
     from li import synth  # this repo's generator (before `li` is re-bound to the reference)
     t0 = time.time()
     x, q, qn, xn, layers = synth.build_lmi_workload(SIZES[size], nq, 122, "MLP-5", "cpu")
+    labels = np.empty(xn.shape[0], np.int64)
     with torch.no_grad():
-        h = xn
-        for i, (w, b) in enumerate(layers):
-            h = h @ w.T + b
-            if i + 1 < len(layers):
-                h = torch.relu(h)
-        labels = h.argmax(dim=1).numpy().astype(np.int64)
+        for a in range(0, xn.shape[0], 1 << 20):   # chunked: 10M x 256 f32 is 10 GB
+            h = xn[a:a + (1 << 20)]
+            for i, (w, b) in enumerate(layers):
+                h = h @ w.T + b
+                if i + 1 < len(layers):
+                    h = torch.relu(h)
+            labels[a:a + h.shape[0]] = h.argmax(dim=1).numpy()
     x = x.numpy()
     q = q.numpy()
+    # copy=False: at 10M the fp16 corpus is 15.4 GB, a second copy would not
+    # leave room for the reference's per-bucket float64 temporaries in 64 GB
     if dtype == "f32":
-        x, q = x.astype(np.float32), q.astype(np.float32)
+        x, q = x.astype(np.float32, copy=False), q.astype(np.float32, copy=False)
     else:
-        x, q = x.astype(np.float16), q.astype(np.float16)
+        x, q = x.astype(np.float16, copy=False), q.astype(np.float16, copy=False)
     xn, qn = xn.numpy(), qn.numpy()
     layers = [(w.numpy(), b.numpy()) for w, b in layers]
     t_build = time.time() - t0
