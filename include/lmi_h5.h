@@ -38,6 +38,14 @@ int lmi_h5_dataset_info(const char* path, const char* name, int64_t* dims_out,
 int lmi_h5_read_f32(const char* path, const char* name, int64_t row0, int64_t nrows,
                     float* out);
 
+/* The same rows in the STORED floating type, as np.array(h5py.File(path)[name])
+ * returns them (search.py:48-49, :79-87: clip768v2 'emb' stays float16, which
+ * decides the reference's float64 arithmetic, utils.py:11): elem_bytes must be
+ * the stored element size (2, 4 or 8, from lmi_h5_dataset_info); the bytes
+ * are copied unconverted (little-endian IEEE). */
+int lmi_h5_read_stored(const char* path, const char* name, int64_t row0, int64_t nrows,
+                       int32_t elem_bytes, void* out);
+
 /* store_results (utils.py:85-97): creates/truncates `path` (the parent
  * directory must exist). */
 int lmi_h5_write_results(const char* path, const uint32_t* knns, const double* dists,

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 5
+#define LMI_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -114,6 +114,13 @@ typedef struct lmi_index_desc {
      * first, so its pruning bound starts near the final k-th distance.
      * Results do not depend on it. */
     const float* chunk_centroid;
+    /* ABI 6: optional (NULL = none) device [n_rows][d_pad] float64: the rows
+     * as the caller gave them when they are float64 (a float64 data_search
+     * DataFrame).  The scan still reads `corpus` (the rows rounded to
+     * float32); the float64 mode (lmi_bucket_topk_f64*) recomputes its band
+     * and fallback distances from these rows, i.e. on the values sklearn sees
+     * (utils.py:11, :19).  Results of the float32 mode do not depend on it. */
+    const double* corpus64;
 } lmi_index_desc;
 
 /* Host helper: fills chunk_first_out[C+1] from host bucket offsets and returns
@@ -159,9 +166,11 @@ int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t 
  *   - the fp32 scan keeps the top-KL (KL >= k + 5: 15 for k <= 10) per (query, probe);
  *   - every list entry within 2*eps of the fp32 k-th distance is recomputed
  *     in float64 from the stored row (sklearn normalize + dot; exact fp16
- *     inputs), sorted by (d64, position); with fewer than KL entries in that
- *     band the result is the exact float64 top-k whenever eps bounds the fp32
- *     error |d32 - d64| (LMI_REFINE_EPS is 40x the largest error measured);
+ *     inputs; idx->corpus64 when set), sorted by (d64, position); with fewer
+ *     than KL entries in that band the result is the exact float64 top-k
+ *     whenever eps bounds the fp32 error |d32 - d64| for every row: the host
+ *     passes a bound derived from d_pad and the MFMA accumulation depth
+ *     (li.index.refine_eps; 2^-16 for the fp16 path at d 768);
  *   - pairs whose band fills the list are recomputed in float64 over their
  *     whole bucket shard (exact, rare: ties or near-ties of > KL-k objects).
  * Same arguments and layout as lmi_bucket_topk; out_d is float64 [nq][R][k]
@@ -175,6 +184,16 @@ int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, int32_t nq, i
                         const int32_t* classes, int32_t R, int32_t k, int32_t qmode, double eps,
                         double* out_d, int32_t* out_pos, int32_t* status, void* workspace,
                         size_t ws_bytes, void* stream);
+/* ABI 6: as lmi_bucket_topk_f64, with float64 query rows q64 (device,
+ * [nq][ldq64], nullable) for the float64 recomputation: the reference's
+ * arithmetic on float64 queries (utils.py:11, :19).  q (float32) is what the
+ * scan reads -- q64 rounded to float32.  Together with idx->corpus64 this is
+ * the float64-input path; eps must then also cover the float32 rounding of
+ * the inputs (8u more; li.index.refine_eps). */
+int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                         const double* q64, int32_t ldq64, const int32_t* classes, int32_t R,
+                         int32_t k, int32_t qmode, double eps, double* out_d, int32_t* out_pos,
+                         int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 /* Diagnostic (synchronises `stream`): how many (query, probe) pairs of the
  * last lmi_bucket_topk_f64 call on this workspace took the whole-bucket path. */
 int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx, int32_t nq,
@@ -288,6 +307,15 @@ int lmi_kmeans_update(const float* x, int64_t n, int32_t d, const int32_t* label
  * under graph capture (events recorded into a hipGraph cannot be timed). */
 int lmi_timing_enable(int32_t on);
 int32_t lmi_timing_read(float* ms_out, int32_t max_n);
+
+/* ---- host utilities (ABI 6) ---------------------------------------------- */
+/* 64-bit content hash of n_bytes of HOST memory on `threads` OpenMP threads
+ * (<= 0: all), independent of the thread count; not cryptographic.  Keys the
+ * drop-in's HBM index cache (li.LearnedIndex): a cached bucket-sorted corpus
+ * is served only for byte-identical data_search / labels / ids, where the
+ * reference re-gathers every bucket from the DataFrame on every call
+ * (LearnedIndex.py:152-153, :168). */
+uint64_t lmi_host_hash64(const void* data, uint64_t n_bytes, int32_t threads);
 
 /* ---- misc --------------------------------------------------------------- */
 const char* lmi_last_error(void);

@@ -105,6 +105,51 @@ int lmi_h5_read_f32(const char* path, const char* name, int64_t row0, int64_t nr
     return rc;
 }
 
+int lmi_h5_read_stored(const char* path, const char* name, int64_t row0, int64_t nrows,
+                       int32_t elem_bytes, void* out) {
+    if (!path || !name || (!out && nrows > 0) || row0 < 0 || nrows < 0)
+        return fail(LMI_E_INVALID, "bad argument");
+    quiet();
+    hid_t f = H5Fopen(path, H5F_ACC_RDONLY, H5P_DEFAULT);
+    if (f < 0) return fail(LMI_E_IO, "cannot open %s", path);
+    int rc = 0;
+    hid_t d = H5Dopen2(f, name, H5P_DEFAULT);
+    if (d < 0) {
+        H5Fclose(f);
+        return fail(LMI_E_IO, "%s: no dataset '%s'", path, name);
+    }
+    hid_t sp = H5Dget_space(d), t = H5Dget_type(d);
+    hsize_t dims[2] = {0, 1};
+    const int rank = H5Sget_simple_extent_ndims(sp);
+    if (rank < 1 || rank > 2 || H5Tget_class(t) != H5T_FLOAT ||
+        H5Tget_order(t) != H5T_ORDER_LE) {
+        rc = fail(LMI_E_INVALID, "%s/%s: need a rank-1/2 little-endian floating dataset", path, name);
+    } else if ((int32_t)H5Tget_size(t) != elem_bytes) {
+        rc = fail(LMI_E_INVALID, "%s/%s: stored element is %d bytes, caller expects %d", path, name,
+                  (int)H5Tget_size(t), (int)elem_bytes);
+    } else {
+        H5Sget_simple_extent_dims(sp, dims, NULL);
+        if ((hsize_t)(row0 + nrows) > dims[0]) {
+            rc = fail(LMI_E_INVALID, "%s/%s: rows [%lld, %lld) past %llu", path, name,
+                      (long long)row0, (long long)(row0 + nrows), (unsigned long long)dims[0]);
+        } else if (nrows > 0) {
+            hsize_t start[2] = {(hsize_t)row0, 0}, count[2] = {(hsize_t)nrows, rank == 2 ? dims[1] : 1};
+            H5Sselect_hyperslab(sp, H5S_SELECT_SET, start, NULL, count, NULL);
+            hid_t mem = H5Screate_simple(rank, count, NULL);
+            // the file's own type as the memory type: the bytes as stored
+            // (IEEE binary16 / 32 / 64, little endian), no conversion
+            if (H5Dread(d, t, mem, sp, H5P_DEFAULT, out) < 0)
+                rc = fail(LMI_E_IO, "%s/%s: read failed", path, name);
+            H5Sclose(mem);
+        }
+    }
+    H5Tclose(t);
+    H5Sclose(sp);
+    H5Dclose(d);
+    H5Fclose(f);
+    return rc;
+}
+
 static int put_str(hid_t obj, const char* key, const char* val) {
     // h5py's Python-str attribute: scalar, variable-length UTF-8
     hid_t t = H5Tcopy(H5T_C_S1);

@@ -46,6 +46,9 @@ struct RefineArgs {
     int64_t n_rows;
     const float* q;
     int32_t ldq;
+    const double* corpus64;  // float64 rows (idx->corpus64) or null
+    const double* q64;       // float64 queries or null
+    int32_t ldq64;
     const int32_t* classes;
     int32_t nq, R, kl, k;
     double eps;
@@ -78,6 +81,13 @@ __device__ inline void load_piece(const TC* row, int piece, int d, double (&v)[4
             for (int j = 0; j < 4; ++j) v[j] = (double)h[j];
             return;
         }
+    } else if constexpr (sizeof(TC) == 8) {
+        if (e0 + 4 <= d) {
+            const double2 a = *reinterpret_cast<const double2*>(row + e0);
+            const double2 b = *reinterpret_cast<const double2*>(row + e0 + 2);
+            v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+            return;
+        }
     } else {
         if (e0 + 4 <= d) {
             const float4 f = *reinterpret_cast<const float4*>(row + e0);
@@ -92,7 +102,8 @@ __device__ inline void load_piece(const TC* row, int piece, int d, double (&v)[4
 constexpr int kMaxPieces = 4;  // d <= 1024 (4 pieces of 4 per lane)
 
 // q^ for this lane's pieces (sklearn normalize of the query row, float64)
-__device__ inline void query_hat(const float* qrow, int d, int nps, double (&qh)[kMaxPieces][4]) {
+template <typename TQ>
+__device__ inline void query_hat(const TQ* qrow, int d, int nps, double (&qh)[kMaxPieces][4]) {
     const int lane = threadIdx.x & 63;
     double ss = 0.0;
 #pragma unroll
@@ -150,7 +161,20 @@ __device__ inline T shfl_slot(const T (&v)[kSlots], int j) {
     return __shfl(x, l);
 }
 
+// the rows the float64 distances are computed from (the stored fp16 / f32
+// rows, or the caller's float64 rows) and the query rows (float32 or float64)
 template <typename TC>
+__device__ inline const TC* rows_of(const RefineArgs& a) {
+    if constexpr (sizeof(TC) == 8) return a.corpus64;
+    else return reinterpret_cast<const TC*>(a.corpus);
+}
+template <typename TQ>
+__device__ inline const TQ* query_of(const RefineArgs& a, int64_t q) {
+    if constexpr (sizeof(TQ) == 8) return a.q64 + (size_t)q * a.ldq64;
+    else return a.q + (size_t)q * a.ldq;
+}
+
+template <typename TC, typename TQ>
 __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t p = (int64_t)blockIdx.x * (kRefT / 64) + (threadIdx.x >> 6);
@@ -192,14 +216,14 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
         if (rj[s] >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);
     const int nps = (a.d + 255) / 256;
     double qh[kMaxPieces][4];
-    query_hat(a.q + (size_t)(p / a.R) * a.ldq, a.d, nps, qh);
+    query_hat(query_of<TQ>(a, p / a.R), a.d, nps, qh);
     double mine[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) mine[s] = __builtin_inf();
     for (int j = 0; j < m; ++j) {
         const int32_t r = shfl_slot(rj, j);
         if (r < 0 || r >= a.n_rows) continue;
-        const TC* row = reinterpret_cast<const TC*>(a.corpus) + (size_t)r * a.d_pad;
+        const TC* row = rows_of<TC>(a) + (size_t)r * a.d_pad;
         const double dv = row_dist64<TC>(row, a.d, nps, qh);
         if (lane == (j & 63)) {
             const int s = j >> 6;
@@ -235,7 +259,7 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
 // shard (a wave per row, kFbRows rows in flight); lane 0 of every wave keeps
 // the wave's top-k in LDS, thread 0 merges the waves' lists.
 constexpr int kFbK = 256;
-template <typename TC>
+template <typename TC, typename TQ>
 __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
     __shared__ double sd[kFbT / 64][kFbK];
     __shared__ int32_t sp[kFbT / 64][kFbK];
@@ -248,7 +272,7 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
         const int c = a.classes[p];  // classes is [nq][R]: pair p = q*R + r
         const int64_t b0 = a.bucket_off[c], b1 = a.bucket_off[c + 1];
         double qh[kMaxPieces][4];
-        query_hat(a.q + (size_t)(p / a.R) * a.ldq, a.d, nps, qh);
+        query_hat(query_of<TQ>(a, p / a.R), a.d, nps, qh);
         double* L = sd[w];
         int32_t* G = sp[w];
         if (lane == 0)
@@ -261,8 +285,7 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
 #pragma unroll
             for (int u = 0; u < kFbRows; ++u) {
                 const int64_t r = r0 + u;
-                const TC* row = reinterpret_cast<const TC*>(a.corpus) +
-                                (size_t)(r < b1 ? r : b0) * a.d_pad;
+                const TC* row = rows_of<TC>(a) + (size_t)(r < b1 ? r : b0) * a.d_pad;
                 dv[u] = row_dist64<TC>(row, a.d, nps, qh);
             }
             if (lane == 0) {
@@ -363,11 +386,37 @@ extern "C" size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_
     return lmi::refine_ws(idx, nq, R, k, qmode).total;
 }
 
+namespace lmi {
+namespace {
+template <typename TC, typename TQ>
+void launch_refine(const RefineArgs& a, dim3 grid, dim3 fgrid, hipStream_t s) {
+    hipLaunchKernelGGL((refine_kernel<TC, TQ>), grid, dim3(kRefT), 0, s, a);
+    // one workgroup per queued pair (the grid strides over the queue; the
+    // queue length is read on the device, usually 0)
+    hipLaunchKernelGGL((fallback_kernel<TC, TQ>), fgrid, dim3(kFbT), 0, s, a);
+}
+template <typename TC>
+void launch_refine_q(const RefineArgs& a, dim3 grid, dim3 fgrid, hipStream_t s) {
+    if (a.q64) launch_refine<TC, double>(a, grid, fgrid, s);
+    else launch_refine<TC, float>(a, grid, fgrid, s);
+}
+}  // namespace
+}  // namespace lmi
+
 extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, int32_t nq,
                                    int32_t ldq, const int32_t* classes, int32_t R, int32_t k,
                                    int32_t qmode, double eps, double* out_d, int32_t* out_pos,
                                    int32_t* status, void* workspace, size_t ws_bytes,
                                    void* stream) {
+    return lmi_bucket_topk_f64q(idx, q, nq, ldq, nullptr, 0, classes, R, k, qmode, eps, out_d,
+                                out_pos, status, workspace, ws_bytes, stream);
+}
+
+extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, int32_t nq,
+                                    int32_t ldq, const double* q64, int32_t ldq64,
+                                    const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
+                                    double eps, double* out_d, int32_t* out_pos, int32_t* status,
+                                    void* workspace, size_t ws_bytes, void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_F64, "k=%d outside [1, %d]", k, LMI_MAX_K_F64);
@@ -377,6 +426,7 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
     LMI_CHECK_ARG(eps >= 0.0 && eps < 1.0, "eps must lie in [0, 1)");
     if (nq == 0) return LMI_OK;
     LMI_CHECK_ARG(q && classes && out_d && out_pos && status && workspace, "null pointer");
+    LMI_CHECK_ARG(q64 == nullptr || ldq64 >= idx->d, "ldq64 < d");
     const RefineWs w = refine_ws(idx, nq, R, k, qmode);
     if (ws_bytes < w.total) {
         set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
@@ -395,6 +445,9 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
     a.n_rows = idx->n_rows;
     a.q = q;
     a.ldq = ldq;
+    a.corpus64 = idx->corpus64;
+    a.q64 = q64;
+    a.ldq64 = ldq64;
     a.classes = classes;
     a.nq = nq;
     a.R = R;
@@ -420,19 +473,14 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
     if (rc != LMI_OK) return rc;
     const int64_t P = (int64_t)nq * R;
     const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));
-    if (idx->dtype == LMI_F16)
-        hipLaunchKernelGGL(refine_kernel<_Float16>, grid, dim3(kRefT), 0, s, a);
-    else
-        hipLaunchKernelGGL(refine_kernel<float>, grid, dim3(kRefT), 0, s, a);
-    LMI_LAUNCH_CHECK("refine_kernel");
-    // one workgroup per queued pair (the grid strides over the queue; the
-    // queue length is read on the device, usually 0)
     const dim3 fgrid((unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref())));
-    if (idx->dtype == LMI_F16)
-        hipLaunchKernelGGL(fallback_kernel<_Float16>, fgrid, dim3(kFbT), 0, s, a);
+    if (idx->corpus64)
+        launch_refine_q<double>(a, grid, fgrid, s);
+    else if (idx->dtype == LMI_F16)
+        launch_refine_q<_Float16>(a, grid, fgrid, s);
     else
-        hipLaunchKernelGGL(fallback_kernel<float>, fgrid, dim3(kFbT), 0, s, a);
-    LMI_LAUNCH_CHECK("fallback_kernel");
+        launch_refine_q<float>(a, grid, fgrid, s);
+    LMI_LAUNCH_CHECK("refine_kernel / fallback_kernel");
     return LMI_OK;
 }
 

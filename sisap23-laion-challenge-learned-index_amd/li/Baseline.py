@@ -23,7 +23,7 @@ class Baseline(Logger):
         self._key = None
 
     def search(self, queries, data, k=10):
-        from .LearnedIndex import content_key, dist_dtype
+        from .LearnedIndex import _upload_queries, content_key, dist_dtype
         from .index import DeviceIndex, Searcher
         s = time.time()
         key = content_key(data)
@@ -32,7 +32,7 @@ class Baseline(Logger):
             self._index = DeviceIndex(data, np.zeros(n, np.int64), 1)
             self._key = key
         ix = self._index
-        q = torch.from_numpy(np.ascontiguousarray(queries, dtype=np.float32)).to(ix.device)
+        q = _upload_queries(queries, ix.device)
         classes = torch.zeros((q.shape[0], 1), dtype=torch.int32, device=ix.device)
         dist = dist_dtype(data, queries)
         _, d, pos, st = Searcher(ix, None).lists(None, q, 1, k, classes=classes, dist=dist)

@@ -52,6 +52,7 @@ EXPORTS = (
     "lmi_merge_topk",
     "lmi_scan_f64_workspace_bytes",
     "lmi_bucket_topk_f64",
+    "lmi_bucket_topk_f64q",
     "lmi_refine_fallback_count",
     "lmi_merge_topk_f64",
     "lmi_packed_rank_words",
@@ -69,6 +70,7 @@ EXPORTS = (
     "lmi_last_error",
     "lmi_abi_version",
     "lmi_config_reload",
+    "lmi_host_hash64",
 )
 
 
@@ -91,7 +93,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class IndexDesc(C.Structure):
@@ -110,6 +112,7 @@ class IndexDesc(C.Structure):
         ("n_chunks", C.c_int32),
         ("max_chunks", C.c_int32),
         ("chunk_centroid", C.c_void_p),  # ABI 2
+        ("corpus64", C.c_void_p),        # ABI 6
     ]
 
 
@@ -127,6 +130,8 @@ _SIGNATURES = {
     "lmi_scan_f64_workspace_bytes": (C.c_size_t, [C.POINTER(IndexDesc), _I32, _I32, _I32, _I32]),
     "lmi_bucket_topk_f64": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _I32, _I32,
                                       C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
+    "lmi_bucket_topk_f64q": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _P, _I32,
+                                       _I32, _I32, C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,
                                             _P]),
     "lmi_merge_topk_f64": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),
@@ -149,6 +154,7 @@ _SIGNATURES = {
     "lmi_last_error": (C.c_char_p, []),
     "lmi_abi_version": (C.c_int32, []),
     "lmi_config_reload": (C.c_int, []),
+    "lmi_host_hash64": (C.c_uint64, [_P, C.c_uint64, _I32]),
 }
 
 _lock = threading.Lock()

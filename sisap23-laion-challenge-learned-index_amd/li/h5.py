@@ -2,7 +2,9 @@
 hot path, native over the image's libhdf5 (h5py is not installed here).
 
   read_dataset(path, key)        np.array(h5py.File(path, "r")[key])
-                                 (search.py:48-49, :79-87), as float32
+                                 (search.py:48-49, :79-87): the stored floating
+                                 type (float16 'emb' stays float16), or
+                                 converted by HDF5 with dtype=np.float32
   write_results(dst, ...)        store_results (utils.py:85-97), eval/'s format
   write_dataset(path, key, x)    lay synthetic data out as data/<kind>/<size>/*.h5
 """
@@ -15,8 +17,8 @@ import numpy as np
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblmi_h5.so")
 F32, F16, F64, U32, I64 = 0, 1, 2, 3, 4
-EXPORTS = ("lmi_h5_dataset_info", "lmi_h5_read_f32", "lmi_h5_write_results", "lmi_h5_write_f32",
-           "lmi_h5_last_error")
+EXPORTS = ("lmi_h5_dataset_info", "lmi_h5_read_f32", "lmi_h5_read_stored", "lmi_h5_write_results",
+           "lmi_h5_write_f32", "lmi_h5_last_error")
 _lib = None
 
 
@@ -28,6 +30,8 @@ def load():
         lib = C.CDLL(LIB_PATH)
         lib.lmi_h5_dataset_info.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p, C.c_void_p]
         lib.lmi_h5_read_f32.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int64, C.c_void_p]
+        lib.lmi_h5_read_stored.argtypes = [C.c_char_p, C.c_char_p, C.c_int64, C.c_int64, C.c_int32,
+                                           C.c_void_p]
         lib.lmi_h5_write_results.argtypes = [C.c_char_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
                                              C.c_char_p, C.c_char_p, C.c_double, C.c_double,
                                              C.c_char_p, C.c_char_p]
@@ -56,11 +60,23 @@ def dataset_info(path: str, key: str):
     return (int(dims[0]), int(dims[1])), dt.value
 
 
-def read_dataset(path: str, key: str, row0: int = 0, nrows: int = None) -> np.ndarray:
-    """Rows of a floating dataset as float32 [nrows, cols] (fp16 'emb' widened
-    exactly by HDF5's conversion)."""
-    (n, d), _ = dataset_info(path, key)
+_STORED = {F16: np.float16, F32: np.float32, F64: np.float64}
+
+
+def read_dataset(path: str, key: str, row0: int = 0, nrows: int = None, dtype=None) -> np.ndarray:
+    """Rows of a floating dataset [nrows, cols] in its stored type, as
+    np.array(h5py.File(path)[key]) gives them (the fp16 clip768 'emb' stays
+    float16: the reference then computes float64 distances, utils.py:11);
+    dtype=np.float32 converts through HDF5 instead (fp16 widened exactly)."""
+    (n, d), code = dataset_info(path, key)
     nrows = n - row0 if nrows is None else nrows
+    if dtype is None and code in _STORED:
+        out = np.empty((nrows, d), _STORED[code])
+        _check(load().lmi_h5_read_stored(_b(path), _b(key), row0, nrows, out.itemsize,
+                                         out.ctypes.data), f"{path}[{key}]")
+        return out
+    if dtype not in (None, np.float32):
+        raise ValueError("read_dataset: dtype must be None (stored) or np.float32")
     out = np.empty((nrows, d), np.float32)
     _check(load().lmi_h5_read_f32(_b(path), _b(key), row0, nrows, out.ctypes.data),
            f"{path}[{key}]")

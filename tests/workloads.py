@@ -73,3 +73,20 @@ def clustered(n=6000, d=768, nq=200, C=16, arch="MLP", seed=7, label_mode="route
         xn[dst] = xn[src]
         labels[dst] = labels[src]
     return dict(x=x, xn=xn, q=q, qn=qn, layers=layers, labels=labels, C=C)
+
+
+def float64_inputs(w, seed, rel=2e-10):
+    """Float64 corpus and queries for the reference's float64 branch on float64
+    inputs (utils.py:11: sklearn computes in float64 unless both operands are
+    float32): the float32 values plus a seeded relative perturbation below
+    half a float32 ulp, so rounding them to float32 gives back w['x'] / w['q']
+    exactly -- rows that are exact duplicates in float32 differ in float64,
+    and any float32 shortcut orders them by position instead of by the float64
+    distances the reference sees."""
+    rng = np.random.Generator(np.random.PCG64(seed + 64))
+    x64 = w["x"].astype(np.float64)
+    q64 = w["q"].astype(np.float64)
+    x64 *= 1.0 + rel * rng.standard_normal(x64.shape)
+    q64 *= 1.0 + rel * rng.standard_normal(q64.shape)
+    assert np.array_equal(x64.astype(np.float32), w["x"]) and np.array_equal(q64.astype(np.float32), w["q"])
+    return x64, q64
