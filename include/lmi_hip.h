@@ -54,6 +54,16 @@ extern "C" {
 
 #define LMI_Q_F16 0 /* queries are fp16-representable: exact fp16 MFMA path        */
 #define LMI_Q_F32 1 /* general queries: exact-fp32 MFMA path (16x the MFMA time)   */
+/* ABI 6, a flag OR-ed into qmode (lmi_bucket_topk / lmi_bucket_topk_f64*, k <=
+ * LMI_MAX_K): the lists of probes r >= 1 are needed only below the pair's
+ * round-0 k-th distance -- the reference's thresholded rounds compare every
+ * later-round object with the running k-th distance, which is never larger
+ * than round 0's (LearnedIndex.py:71-75, utils.py:23; the merges only lower
+ * it, :86-97) -- so the scan starts every (q, r >= 1) pair with the bound of
+ * pair (q, 0) (plus 2 eps in the float64 mode) and its list holds the top-k of
+ * the objects at or under that bound.  Only for the replay with thresholds
+ * (use_threshold); the lists of r = 0 are unchanged. */
+#define LMI_Q_SEED_ROUND0 0x100
 
 #define LMI_MAX_LAYERS 8
 #define LMI_MAX_K 16          /* largest k of one scan pass (and of K3 / the float32 ABI 1 lists) */

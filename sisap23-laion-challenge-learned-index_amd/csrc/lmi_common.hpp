@@ -123,12 +123,14 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // lo_g (nullable, device [nq*R]): keep only objects after the (distance,
 // global position) key of their pair (the passes of k > 16); ldo: entries per
 // pair in the outputs (default k); prefill: write (+inf, -1) over all R*ldo
-// entries first (the first pass).
+// entries first (the first pass).  seed_r0: LMI_Q_SEED_ROUND0 (pairs r >= 1
+// start from the bound of pair (q, 0), + seed_margin in distance).
 int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                      const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                      int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                      size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g = nullptr,
-                     int32_t ldo = 0, bool prefill = true);
+                     int32_t ldo = 0, bool prefill = true, bool seed_r0 = false,
+                     float seed_margin = 0.0f);
 size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
                             int32_t qmode, bool lo = false);
 // k > LMI_MAX_K: passes_of() passes of kp-entry lists; bucket_topk_passes fills

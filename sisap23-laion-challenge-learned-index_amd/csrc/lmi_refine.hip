@@ -382,6 +382,7 @@ int num_cus_ref() {
 
 extern "C" size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                                int32_t k, int32_t qmode) {
+    qmode &= ~LMI_Q_SEED_ROUND0;
     if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_F64) return 0;
     return lmi::refine_ws(idx, nq, R, k, qmode).total;
 }
@@ -418,6 +419,8 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
                                     double eps, double* out_d, int32_t* out_pos, int32_t* status,
                                     void* workspace, size_t ws_bytes, void* stream) {
     using namespace lmi;
+    const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
+    qmode &= ~LMI_Q_SEED_ROUND0;
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_F64, "k=%d outside [1, %d]", k, LMI_MAX_K_F64);
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
@@ -469,7 +472,8 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
                              ws + w.scan, w.total - w.scan, s)
         : bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
                            (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
-                           ws + w.scan, w.total - w.scan, s);
+                           ws + w.scan, w.total - w.scan, s, nullptr, 0, true, seed,
+                           (float)(2.0 * eps));
     if (rc != LMI_OK) return rc;
     const int64_t P = (int64_t)nq * R;
     const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));
@@ -489,7 +493,7 @@ extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_
                                          int32_t* count_out, void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(workspace && idx && count_out, "null pointer");
-    const RefineWs w = refine_ws(idx, nq, R, k, qmode);
+    const RefineWs w = refine_ws(idx, nq, R, k, qmode & ~LMI_Q_SEED_ROUND0);
     LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + w.nfailed, 4,
                                hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
     LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));

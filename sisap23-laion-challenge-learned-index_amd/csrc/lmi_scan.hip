@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
     const int32_t* __restrict__ classes, int32_t P, int32_t C, const int32_t* __restrict__ counts,
     const int32_t* __restrict__ chunk_first, int32_t QB, int32_t* __restrict__ pair_q,
     int32_t* __restrict__ pair_bucket, Tile* __restrict__ tiles, int32_t* __restrict__ meta,
-    int32_t* __restrict__ work, int32_t ng) {
+    int32_t* __restrict__ work, int32_t ng, int32_t* __restrict__ pair_pos) {
     __shared__ int sh[kPlanThreads / 64];
     __shared__ int wcnt[kPlanThreads / 64];
     __shared__ int g0_all[kGroups], gr_all[kGroups], g0_lt[kGroups], gr_lt[kGroups];
@@ -289,6 +289,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
                 if (v[u] == c) {
                     pair_q[o + __popcll(m & lt)] = e0 + 64 * u + lane;
                     pair_bucket[o + __popcll(m & lt)] = c;
+                    if (pair_pos) pair_pos[e0 + 64 * u + lane] = o + __popcll(m & lt);
                 }
                 o += __popcll(m);
             }
@@ -856,7 +857,26 @@ struct Scan2Args {
     int32_t lag;                // extra ring stages waited for (tuning knob, 0)
     const int32_t* gpos;        // LO: global positions of the rows
     const unsigned long long* lo_g;  // LO: [nq*R] lower-bound key (d, gpos) per pair id
+    const int32_t* pair_pos;    // LMI_Q_SEED_ROUND0: [nq*R] grouped position of each pair id, else null
+    float seed_margin;          //   (distance added to the seed: 2 eps in the float64 mode)
 };
+
+// The seed of a pair (q, r >= 1) under LMI_Q_SEED_ROUND0: the current bound of
+// pair (q, 0) -- an upper bound of its final k-th distance, which bounds every
+// later round's threshold -- as a distance ordinal (+ seed_margin), or
+// 0xffffffff (no bound yet / not seeded).
+__device__ __forceinline__ uint32_t round0_seed(const Scan2Args& a, int p) {
+    const int r = p % a.R;
+    if (r == 0) return 0xffffffffu;
+    const int pp0 = a.pair_pos[p - r];
+    if (pp0 < 0) return 0xffffffffu;
+    const uint32_t s = (uint32_t)(__hip_atomic_load(&a.thr_g[pp0], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT) >> 32);
+    if (s == 0xffffffffu || a.seed_margin == 0.0f) return s;
+    // (+1: the next float up, whatever the rounding of the sum)
+    const uint32_t m = f2ord(ord2f(s) + a.seed_margin) + 1u;
+    return m == 0u ? 0xffffffffu : m;
+}
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
 // expcnt [6:4], lgkmcnt [11:8]); other counters left at their maximum.
@@ -1611,6 +1631,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             for (int s = 0; s < NQF; ++s) qf[s] = (live || ABL == 57) ? qrow[2 * s] : z;
             // dead slots (and exhausted pairs) reject everything
             thr = live && !done ? (uint32_t)(a.thr_g[pp] >> 32) : 0u;
+            if (a.pair_pos && live && !done) thr = std::min(thr, round0_seed(a, a.pair_q[pp]));
             my_invq = live ? a.invq[q] : 0.0f;
         }
         {
@@ -1828,8 +1849,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             // bound and take the global one back (tiles of the same pair on
             // other chunks run concurrently); the returning atomic is consumed
             // in the next epilogue, behind this block's MFMAs
-            if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live)
+            if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live) {
                 xg_carry = std::min(xg_carry, (uint32_t)(atomicMin(&a.thr_g[pp], ((unsigned long long)thr << 32) | 0xffffffffull) >> 32));
+                if (a.pair_pos) xg_carry = std::min(xg_carry, round0_seed(a, a.pair_q[pp]));
+            }
             if (kDmaOnly || !wave_live) {
                 // (no MFMA stream: a branch out of the middle of one would
                 // join its accumulators to a path without the drain)
@@ -2037,6 +2060,7 @@ struct WsLayout {
     size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, tiles_tmp, ntiles, work, partial, thr_g, pref,
         pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
+    size_t pair_pos;  // LMI_Q_SEED_ROUND0: grouped position of every pair id
     int32_t qb;      // queries per tile
     bool use_v2;     // scan2_kernel
     bool use_v3;     // scan3_kernel
@@ -2100,6 +2124,7 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     w.pref_tmp = take(P * 4);
     w.pref_tmp2 = take(P * 4);
     w.n_seed = take((size_t)idx->n_buckets * 4);
+    w.pair_pos = take(P * 4);
     w.total = off;
     return w;
 }
@@ -2301,6 +2326,7 @@ size_t lmi::scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t 
 extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                            int32_t k, int32_t qmode) {
     using namespace lmi;
+    qmode &= ~LMI_Q_SEED_ROUND0;
     if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_PASSES) return 0;
     if (k <= LMI_MAX_K) return scan_workspace_bytes(idx, nq, R, k, qmode);
     int kp;
@@ -2319,9 +2345,11 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
                                size_t ws_bytes, void* stream) {
     using namespace lmi;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
+    qmode &= ~LMI_Q_SEED_ROUND0;
     if (k <= LMI_MAX_K)
         return bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
-                                status, workspace, ws_bytes, s);
+                                status, workspace, ws_bytes, s, nullptr, 0, true, seed);
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(k <= LMI_MAX_K_PASSES, "k=%d outside [1, %d]", k, LMI_MAX_K_PASSES);
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
@@ -2351,7 +2379,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                           const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                           int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                           size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g, int32_t ldo,
-                          bool prefill) {
+                          bool prefill, bool seed_r0, float seed_margin) {
     using namespace lmi;
     if (ldo <= 0) ldo = k;
     LMI_CHECK_ARG(idx != nullptr, "null index");
@@ -2407,8 +2435,13 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     LMI_HIP_TRY(hipMemsetAsync(pair_bucket, 0xff, (size_t)P * 4, s));
     hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, counts);
     LMI_LAUNCH_CHECK("plan_count_kernel");
+    // (the seed reads the pair position of every (q, 0); pairs whose class is
+    // out of range keep -1)
+    const bool seed = seed_r0 && w.use_v3 && !LOP && R > 1;
+    int32_t* pair_pos = seed ? (int32_t*)(ws + w.pair_pos) : nullptr;
+    if (seed) LMI_HIP_TRY(hipMemsetAsync(pair_pos, 0xff, (size_t)P * 4, s));
     hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
-                       idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng);
+                       idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
     if (!nearest_first && env_config().scan_order != 0) {
@@ -2471,6 +2504,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
         b.gpos = idx->gpos;
         b.lo_g = lo_g;
+        b.pair_pos = pair_pos;
+        b.seed_margin = seed_margin;
         b.ng = ng;
         b.lag = std::max(0, std::min(3, env_config().scan_lag));
 #ifdef LMI_ABLATION

@@ -34,6 +34,7 @@ LMI_ROUTER_TOPR = 0
 LMI_ROUTER_ARGMAX = 1
 LMI_Q_F16 = 0
 LMI_Q_F32 = 1
+LMI_Q_SEED_ROUND0 = 0x100
 LMI_MAX_LAYERS = 8
 LMI_MAX_K = 16
 LMI_MAX_K_PASSES = 1024

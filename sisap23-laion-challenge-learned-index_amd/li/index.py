@@ -32,6 +32,9 @@ from . import _lib
 from ._lib import check, ptr
 
 DEFAULT_CHUNK_ROWS = 8192
+# LMI_Q_SEED_ROUND0 in the thresholded reference replay (LMI_NO_SEED=1: off,
+# for A/B measurements; results are the same either way)
+_SEED_ROUND0 = __import__("os").environ.get("LMI_NO_SEED") != "1"
 
 
 def _as_torch(x, device=None, dtype=None) -> torch.Tensor:
@@ -481,12 +484,14 @@ def _workspace(ws, need: int, what: str) -> torch.Tensor:
 
 
 def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
-                qmode: Optional[int] = None, stream=None, out=None, ws=None):
+                qmode: Optional[int] = None, stream=None, out=None, ws=None,
+                seed_round0: bool = False):
     """K2 on one shard.  Returns (d [nq,R,k] f32, pos [nq,R,k] int32, status int32 tensor);
     `out` = such a triple to write into (the status word zeroed by the caller);
     `ws` = a caller-owned uint8 workspace (default: the index's cached one,
     which a later call with a larger batch may replace — a captured graph
-    passes its own)."""
+    passes its own).  `seed_round0` (LMI_Q_SEED_ROUND0, the thresholded
+    replay only): probes r >= 1 keep only objects under the round-0 bound."""
     lib = _lib.load()
     q = _rows_f32(q, index.device)
     classes = _as_torch(classes, index.device, torch.int32)
@@ -506,15 +511,16 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
     else:
         _workspace(ws, lib.lmi_scan_workspace_bytes(C.byref(index.desc), nq, R, k, qmode), "scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
+    flags = _lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0
     check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(index.desc), ptr(q), nq, q.stride(0),
-                                                 ptr(classes), R, k, qmode, ptr(out_d),
+                                                 ptr(classes), R, k, qmode | flags, ptr(out_d),
                                                  ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
     return out_d, out_pos, status
 
 
 def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
                     qmode: Optional[int] = None, eps: Optional[float] = None, stream=None,
-                    fallback_count: bool = False, out=None, ws=None):
+                    fallback_count: bool = False, out=None, ws=None, seed_round0: bool = False):
     """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
     arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
     (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback]);
@@ -554,10 +560,11 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     else:
         _workspace(ws, need, "float64 scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
+    flags = _lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0
     check("lmi_bucket_topk_f64q", lib.lmi_bucket_topk_f64q(
         C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
-        ptr(classes), R, k, qmode, float(eps), ptr(out_d), ptr(out_pos), ptr(status), ptr(ws),
-        ws.numel(), s))
+        ptr(classes), R, k, qmode | flags, float(eps), ptr(out_d), ptr(out_pos), ptr(status),
+        ptr(ws), ws.numel(), s))
     if not fallback_count:
         return out_d, out_pos, status
     n = C.c_int32(0)
@@ -718,7 +725,7 @@ class Searcher:
         return mode
 
     def _scan(self, q_search, classes, k_list: int, qmode: int, f64: bool, lap=None,
-              status_out=None, ws=None):
+              status_out=None, ws=None, seed_round0: bool = False):
         """K2 on this shard (+ all-gather and K3 for G > 1 ranks, the status
         words riding along so every rank sees every rank's bits).  `lap`
         (measurement only) is called after the scan and after the exchange.
@@ -740,10 +747,10 @@ class Searcher:
             out = (dv.view(nq, R, k_list), pv.view(nq, R, k_list), sv)
         if f64:
             d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode,
-                                             out=out, ws=ws)
+                                             out=out, ws=ws, seed_round0=seed_round0)
         else:
             d, pos, status = bucket_topk(self.index, q_search, classes, k_list, qmode=qmode, out=out,
-                                         ws=ws)
+                                         ws=ws, seed_round0=seed_round0)
         if lap:
             lap("scan")
         if self.index.world > 1:
@@ -856,8 +863,13 @@ class Searcher:
             # the answer and both status words in one buffer: one D2H copy
             w_ans = k_round if classes.shape[1] == 1 else k
             ans = answer_buffer(nq, w_ans, dev)
+        # (valid while the merged width k is at most the round lists' k_round:
+        # the running threshold then never exceeds round 0's k-th distance;
+        # with k > k_round the first merge pads with 10000s)
+        seed = semantics == "reference" and use_threshold and k <= k_round and _SEED_ROUND0
         d, pos, status = self._scan(q_search, classes, k_list, qmode, f64, lap_at if sync else None,
-                                    status_out=None if ans is None else ans[3][0:1])
+                                    status_out=None if ans is None else ans[3][0:1],
+                                    seed_round0=seed)
         t0 = tl[0]
         h_st = self._host("st", (2,), torch.int32)
 
@@ -921,7 +933,7 @@ class Searcher:
             if check_status(st0, st1):
                 ans = answer_buffer(nq, w_ans, dev)
                 d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64,
-                                            status_out=ans[3][0:1])
+                                            status_out=ans[3][0:1], seed_round0=seed)
                 h = run_replay(d, pos, ans)
                 torch.cuda.current_stream(dev).synchronize()
                 hd, ha, st0, st1 = answer_views(h, nq, w_ans)
@@ -937,7 +949,8 @@ class Searcher:
         torch.cuda.current_stream(dev).synchronize()
         t0 = lap("d2h", t0)
         if check_status(int(h_st[0])):
-            d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64)
+            d, pos, status = self._scan(q_search, classes, k_list, _lib.LMI_Q_F32, f64,
+                                        seed_round0=seed)
             h_d.copy_(d)
             h_pos.copy_(pos)
             h_st[0:1].copy_(status)
@@ -1064,7 +1077,7 @@ class GraphedSearch:
                 q = self.q32[:nq]
                 classes = self.cls[:nq]
             d_, pos, _ = s._scan(q, classes, k_round, self.qmode, f64, status_out=ans[3][0:1],
-                                 ws=self.ws)
+                                 ws=self.ws, seed_round0=use_threshold and k <= k_round and _SEED_ROUND0)
             replay_device(classes, d_, pos, k_round=k_round, k_final=k, bucket_size=bsz,
                           pos_to_id=p2id, use_threshold=use_threshold,
                           out=(ans[1], ans[2], ans[3][1:2]))
