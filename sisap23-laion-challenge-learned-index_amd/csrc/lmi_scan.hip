@@ -857,7 +857,7 @@ struct Scan2Args {
     int32_t lag;                // extra ring stages waited for (tuning knob, 0)
     const int32_t* gpos;        // LO: global positions of the rows
     const unsigned long long* lo_g;  // LO: [nq*R] lower-bound key (d, gpos) per pair id
-    const int32_t* pair_pos;    // LMI_Q_SEED_ROUND0: [nq*R] grouped position of each pair id, else null
+    const int32_t* pair_pos;    // LMI_Q_SEED_ROUND0: [P] grouped position of the pair's (q, 0), -1 if none; else null
     float seed_margin;          //   (distance added to the seed: 2 eps in the float64 mode)
 };
 
@@ -865,10 +865,8 @@ struct Scan2Args {
 // pair (q, 0) -- an upper bound of its final k-th distance, which bounds every
 // later round's threshold -- as a distance ordinal (+ seed_margin), or
 // 0xffffffff (no bound yet / not seeded).
-__device__ __forceinline__ uint32_t round0_seed(const Scan2Args& a, int p) {
-    const int r = p % a.R;
-    if (r == 0) return 0xffffffffu;
-    const int pp0 = a.pair_pos[p - r];
+__device__ __forceinline__ uint32_t round0_seed(const Scan2Args& a, int pp) {
+    const int pp0 = a.pair_pos[pp];  // (seed_pos_kernel: -1 for r = 0 pairs)
     if (pp0 < 0) return 0xffffffffu;
     const uint32_t s = (uint32_t)(__hip_atomic_load(&a.thr_g[pp0], __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT) >> 32);
@@ -876,6 +874,20 @@ __device__ __forceinline__ uint32_t round0_seed(const Scan2Args& a, int p) {
     // (+1: the next float up, whatever the rounding of the sum)
     const uint32_t m = f2ord(ord2f(s) + a.seed_margin) + 1u;
     return m == 0u ? 0xffffffffu : m;
+}
+
+// LMI_Q_SEED_ROUND0: per grouped pair position pp, the grouped position of
+// its round-0 pair (q, 0), or -1 for r = 0 pairs (pair_pos: grouped position
+// of every pair id, plan_fill_kernel; pairs of out-of-range classes keep -1)
+__global__ __launch_bounds__(256) void seed_pos_kernel(const int32_t* __restrict__ pair_q,
+                                                       const int32_t* __restrict__ pair_pos,
+                                                       int32_t P, int32_t R,
+                                                       int32_t* __restrict__ seed_pos) {
+    const int pp = blockIdx.x * 256 + threadIdx.x;
+    if (pp >= P) return;
+    const int p = pair_q[pp];
+    const int r = p % R;
+    seed_pos[pp] = (r == 0 || p < 0) ? -1 : pair_pos[p - r];
 }
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
@@ -1631,7 +1643,9 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             for (int s = 0; s < NQF; ++s) qf[s] = (live || ABL == 57) ? qrow[2 * s] : z;
             // dead slots (and exhausted pairs) reject everything
             thr = live && !done ? (uint32_t)(a.thr_g[pp] >> 32) : 0u;
-            if (a.pair_pos && live && !done) thr = std::min(thr, round0_seed(a, a.pair_q[pp]));
+            if constexpr (!LO) {  // (the k > 16 passes are never seeded)
+                if (a.pair_pos && live) thr = std::min(thr, round0_seed(a, pp));
+            }
             my_invq = live ? a.invq[q] : 0.0f;
         }
         {
@@ -1851,7 +1865,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             // in the next epilogue, behind this block's MFMAs
             if (kXch > 0 && (blk & (kXch - 1)) == kXch - 1 && live) {
                 xg_carry = std::min(xg_carry, (uint32_t)(atomicMin(&a.thr_g[pp], ((unsigned long long)thr << 32) | 0xffffffffull) >> 32));
-                if (a.pair_pos) xg_carry = std::min(xg_carry, round0_seed(a, a.pair_q[pp]));
+
             }
             if (kDmaOnly || !wave_live) {
                 // (no MFMA stream: a branch out of the middle of one would
@@ -2061,6 +2075,7 @@ struct WsLayout {
         pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
     size_t pair_pos;  // LMI_Q_SEED_ROUND0: grouped position of every pair id
+    size_t seed_pos;  //   and of every grouped pair's (q, 0)
     int32_t qb;      // queries per tile
     bool use_v2;     // scan2_kernel
     bool use_v3;     // scan3_kernel
@@ -2125,6 +2140,7 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     w.pref_tmp2 = take(P * 4);
     w.n_seed = take((size_t)idx->n_buckets * 4);
     w.pair_pos = take(P * 4);
+    w.seed_pos = take(P * 4);
     w.total = off;
     return w;
 }
@@ -2443,6 +2459,12 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
                        idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
+    int32_t* seed_pos = seed ? (int32_t*)(ws + w.seed_pos) : nullptr;
+    if (seed) {
+        hipLaunchKernelGGL(seed_pos_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pair_q, pair_pos,
+                           P, R, seed_pos);
+        LMI_LAUNCH_CHECK("seed_pos_kernel");
+    }
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
     if (!nearest_first && env_config().scan_order != 0) {
         hipLaunchKernelGGL(tile_order_kernel, dim3(ng), dim3(1024), 0, s, tiles, (Tile*)(ws + w.tiles_tmp),
@@ -2504,7 +2526,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         b.thr_g = reinterpret_cast<unsigned long long*>(ws + w.thr_g);
         b.gpos = idx->gpos;
         b.lo_g = lo_g;
-        b.pair_pos = pair_pos;
+        b.pair_pos = seed_pos;
         b.seed_margin = seed_margin;
         b.ng = ng;
         b.lag = std::max(0, std::min(3, env_config().scan_lag));
