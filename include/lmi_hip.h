@@ -163,7 +163,11 @@ int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32
 
 /* Merge G per-shard lists of the same rows (K3): in
  * device [G][rows][k] (d f32, pos int32, -1 = empty), out device [rows][k] =
- * the k smallest by (d, pos).  Used after the RCCL all-gather of a G-GPU index. */
+ * the k smallest by (d, pos).  Used after the RCCL all-gather of a G-GPU index.
+ * 1 <= k <= LMI_MAX_K_PASSES (ABI 6; k > LMI_MAX_K merges by rank: the wide
+ * lists of k > 16 at G > 1, search_single(k) / Baseline(k) on the R == 1 path,
+ * LearnedIndex.py:103-111, Baseline.py:14-19).  The same range for
+ * lmi_merge_topk_f64 and lmi_merge_topk_packed. */
 int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
                    int32_t k, float* out_d, int32_t* out_pos, void* stream);
 

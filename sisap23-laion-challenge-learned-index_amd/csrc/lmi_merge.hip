@@ -117,6 +117,63 @@ __global__ __launch_bounds__(kThreads) void merge_f64_kernel(const double* __res
     }
 }
 
+// k > LMI_MAX_K (the wide lists of the lower-bound passes, up to
+// LMI_MAX_K_PASSES entries; k > 16 at G > 1 and the exact semantics over R
+// wide lists): merge by rank, one thread per INPUT entry (g, row, i).  Its
+// rank in the row's merged order is i plus, for every other list g', the
+// number of entries of g' that come before it (a binary search: lists ascend
+// by (distance, position); keys repeat only for empty slots (+inf, -1), and
+// those order by list index g); entries of rank < k land at out[row][rank].
+// The ranks of a row are a permutation of [0, G k), so out[row][0..k) is
+// written exactly once.  Deterministic, no atomics.
+template <typename T>
+__device__ inline bool key_lt(T a, uint32_t pa, T b, uint32_t pb) {
+    return a < b || (a == b && pa < pb);
+}
+template <typename T>
+__global__ __launch_bounds__(kThreads) void merge_wide_kernel(const T* __restrict__ d_in,
+                                                              const int32_t* __restrict__ pos_in,
+                                                              int32_t G, int64_t rows, int32_t k,
+                                                              int64_t gs_d, int64_t gs_p,
+                                                              const int32_t* __restrict__ st_in,
+                                                              int64_t gs_st, int32_t* __restrict__ st_out,
+                                                              T* __restrict__ out_d,
+                                                              int32_t* __restrict__ out_pos) {
+    or_status(st_in, gs_st, G, st_out);
+    const int64_t per_g = rows * k;
+    const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (e >= per_g * G) return;
+    const int g = (int)(e / per_g);
+    const int64_t rem = e - (int64_t)g * per_g;
+    const int64_t row = rem / k;
+    const int i = (int)(rem - row * k);
+    const int32_t p = pos_in[(size_t)g * gs_p + rem];
+    const uint32_t u = (uint32_t)p;  // -1 (empty) sorts last
+    const T x = p < 0 ? (T)__builtin_inf() : d_in[(size_t)g * gs_d + rem];
+    int64_t rank = i;
+    for (int g2 = 0; g2 < G; ++g2) {
+        if (g2 == g) continue;
+        const T* dl = d_in + (size_t)g2 * gs_d + (size_t)row * k;
+        const int32_t* pl = pos_in + (size_t)g2 * gs_p + (size_t)row * k;
+        // first j whose entry does not come before (x, u, g)
+        int lo = 0, hi = k;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            const int32_t pm = pl[mid];
+            const uint32_t um = (uint32_t)pm;
+            const T xm = pm < 0 ? (T)__builtin_inf() : dl[mid];
+            const bool before = key_lt<T>(xm, um, x, u) || (xm == x && um == u && g2 < g);
+            if (before) lo = mid + 1;
+            else hi = mid;
+        }
+        rank += lo;
+    }
+    if (rank < k) {
+        out_d[(size_t)row * k + rank] = x;
+        out_pos[(size_t)row * k + rank] = p < 0 ? -1 : p;
+    }
+}
+
 }  // namespace
 }  // namespace lmi
 
@@ -125,6 +182,20 @@ namespace {
 int launch_merge(const void* d_in, const int32_t* pos_in, int32_t G, int64_t rows, int32_t k,
                  bool f64, int64_t gs_d, int64_t gs_p, const int32_t* st_in, int64_t gs_st,
                  int32_t* st_out, void* out_d, int32_t* out_pos, hipStream_t s) {
+    if (k > LMI_MAX_K) {
+        const int64_t n = (int64_t)G * rows * k;
+        const dim3 wgrid((unsigned)std::max<int64_t>(1, (n + kThreads - 1) / kThreads));
+        if (f64)
+            hipLaunchKernelGGL(merge_wide_kernel<double>, wgrid, dim3(kThreads), 0, s,
+                               (const double*)d_in, pos_in, G, rows, k, gs_d, gs_p, st_in, gs_st,
+                               st_out, (double*)out_d, out_pos);
+        else
+            hipLaunchKernelGGL(merge_wide_kernel<float>, wgrid, dim3(kThreads), 0, s,
+                               (const float*)d_in, pos_in, G, rows, k, gs_d, gs_p, st_in, gs_st,
+                               st_out, (float*)out_d, out_pos);
+        LMI_LAUNCH_CHECK("merge_wide_kernel");
+        return LMI_OK;
+    }
     const dim3 grid((unsigned)std::max<int64_t>(1, (rows + kThreads - 1) / kThreads));
     if (f64) {
         auto* kp = k <= 10 ? merge_f64_kernel<10> : merge_f64_kernel<16>;
@@ -147,7 +218,7 @@ extern "C" int lmi_merge_topk_f64(const double* d_in, const int32_t* pos_in, int
                                   void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(G >= 1 && rows >= 0, "bad G/rows");
-    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_PASSES, "k=%d outside [1, %d]", k, LMI_MAX_K_PASSES);
     if (rows == 0) return LMI_OK;
     LMI_CHECK_ARG(d_in && pos_in && out_d && out_pos, "null pointer");
     return launch_merge(d_in, pos_in, G, rows, k, true, rows * k, rows * k, nullptr, 0, nullptr,
@@ -158,7 +229,7 @@ extern "C" int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t 
                               int32_t k, float* out_d, int32_t* out_pos, void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(G >= 1 && rows >= 0, "bad G/rows");
-    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_PASSES, "k=%d outside [1, %d]", k, LMI_MAX_K_PASSES);
     if (rows == 0) return LMI_OK;
     LMI_CHECK_ARG(d_in && pos_in && out_d && out_pos, "null pointer");
     return launch_merge(d_in, pos_in, G, rows, k, false, rows * k, rows * k, nullptr, 0, nullptr,
@@ -175,7 +246,7 @@ extern "C" int lmi_merge_topk_packed(const int32_t* gathered, int32_t G, int64_t
                                      int32_t* out_pos, int32_t* out_status, void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(G >= 1 && rows >= 0, "bad G/rows");
-    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_PASSES, "k=%d outside [1, %d]", k, LMI_MAX_K_PASSES);
     LMI_CHECK_ARG(rank_words >= lmi_packed_rank_words(rows, k, dist_f64) && rank_words % 2 == 0,
                   "rank_words %lld < lmi_packed_rank_words() or odd", (long long)rank_words);
     LMI_CHECK_ARG(gathered && out_status && (rows == 0 || (out_d && out_pos)), "null pointer");

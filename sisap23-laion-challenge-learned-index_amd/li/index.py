@@ -830,9 +830,6 @@ class Searcher:
         kmax = _lib.LMI_MAX_K_F64 if f64 else _lib.LMI_MAX_K_PASSES
         if k_list > kmax:
             raise ValueError(f"k={k_list} > {kmax}")
-        if k_list > _lib.LMI_MAX_K and (semantics == "exact" or self.index.world > 1):
-            raise ValueError(f"k={k_list} > {_lib.LMI_MAX_K} needs semantics='reference' on one GPU "
-                             f"(the K3 list merge holds {_lib.LMI_MAX_K} entries)")
         if k_round > _lib.LMI_REPLAY_DEVICE_MAX_KR or k > _lib.LMI_REPLAY_DEVICE_MAX_K:
             replay_on = "host"  # the device replay holds rows of <= 32 / 64 entries
         dev = self.index.device

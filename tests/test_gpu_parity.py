@@ -84,19 +84,18 @@ def test_shard_merge_equals_single_gpu():
         assert torch.equal(dm, d1) and torch.equal(pm, p1)
 
 
-@pytest.mark.parametrize("f64", [False, True])
-@pytest.mark.parametrize("k", [10, 16])
+@pytest.mark.parametrize("f64,k", [(False, 10), (False, 16), (True, 10), (False, 40),
+                                   (True, 30)])
 def test_packed_merge_equals_single_gpu(f64, k):
     """The G > 1 product path: every shard's K2 writes its lists and status word
     into its packed send buffer (li.dist.packed_lists), the buffers are
     gathered (here by concatenation, as all_gather_into_tensor lays them out)
     and K3 merges them in place (lmi_merge_topk_packed): bitwise the
-    single-shard lists, and the OR of the ranks' status words."""
+    single-shard lists, and the OR of the ranks' status words.  k > 16: the
+    lower-bound passes' wide lists and K3's merge by rank."""
     from li import _lib
     from li.dist import packed_lists
     from li.index import bucket_topk_f64, check, ptr
-    if f64 and k > 10:
-        pytest.skip("float64 lists of k <= 10 here (k = 16 is the float32 K3 width)")
     w = workloads.clustered(n=5000, nq=150, C=16, seed=3, label_mode="skewed")
     R = 3
     classes = torch.from_numpy(
@@ -269,3 +268,29 @@ def test_full_size_10m_properties():
     dd = (1.0 - (y * qh[:, None, :]).sum(2)).double().cpu().numpy()
     live = anns[qs] > 0
     np.testing.assert_allclose(dists[qs][live], dd[live], atol=1e-5)
+
+
+@pytest.mark.parametrize("dist,k", [("f32", 30), ("f64", 24)])
+def test_exact_semantics_wide_k_matches_oracle(dist, k):
+    """semantics='exact' with k > 16: the R wide lists of a query merged by
+    K3's rank merge = the exact top-k of the union of its probed buckets."""
+    w = workloads.clustered(n=6000, nq=200, C=16, seed=83, label_mode="skewed")
+    R = 4
+    s = Searcher(DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=512), DeviceRouter(w["layers"]))
+    d, a = s.search(torch.from_numpy(w["qn"]).cuda(), torch.from_numpy(w["q"]).cuda(), R, k=k,
+                    k_round=10, semantics="exact", dist=dist)
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    x = w["x"] if dist == "f32" else w["x"].astype(np.float16)
+    q = w["q"] if dist == "f32" else w["q"].astype(np.float16)
+    order, off = O.layout(w["labels"], w["C"])
+    ids = np.arange(1, w["x"].shape[0] + 1)
+    ref_d = np.full((200, k), 10000.0)
+    ref_a = np.zeros((200, k), np.int64)
+    for i in range(200):
+        pos = np.concatenate([np.arange(off[c], off[c + 1]) for c in classes[i]])
+        D = O.pairwise_cosine(q[i:i + 1], x[order[pos]])[0]
+        o = np.lexsort((pos, D))[:k]
+        ref_d[i, :o.size] = D[o]
+        ref_a[i, :o.size] = ids[order[pos[o]]]
+    tie, atol = (1e-6, 1e-5) if dist == "f32" else (1e-12, 1e-12)
+    assert O.compare_lists(ref_d, ref_a, d, a, atol=atol, tie=tie) == 0

@@ -28,8 +28,10 @@ def test_invalid_arguments_fail_loudly_without_a_device():
     rc = lib.lmi_merge_topk(None, None, 0, 10, 10, None, None, None)
     assert rc == _lib.LMI_E_INVALID
     assert b"bad G" in lib.lmi_last_error()
-    rc = lib.lmi_merge_topk(None, None, 2, 10, 17, None, None, None)
-    assert rc == _lib.LMI_E_INVALID and b"k=17" in lib.lmi_last_error()
+    rc = lib.lmi_merge_topk(None, None, 2, 10, _lib.LMI_MAX_K_PASSES + 1, None, None, None)
+    assert rc == _lib.LMI_E_INVALID and b"k=1025" in lib.lmi_last_error()
+    rc = lib.lmi_merge_topk(None, None, 2, 10, 17, None, None, None)   # wide merge: k > 16 is valid
+    assert rc == _lib.LMI_E_INVALID and b"null pointer" in lib.lmi_last_error()
     d = _lib.IndexDesc()
     rc = lib.lmi_bucket_topk(C.byref(d), None, 4, 768, None, 2, 10, 0, None, None, None, None, 0, None)
     assert rc == _lib.LMI_E_INVALID
