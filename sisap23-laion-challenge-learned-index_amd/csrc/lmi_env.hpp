@@ -20,6 +20,7 @@ struct EnvConfig {
     bool router_fma;     // LMI_ROUTER_FMA: FMA-chain router instead of MFMA
     int router_qg;       // LMI_ROUTER_QG: 1/2/4 query groups per workgroup, 0 = auto
     int replay_abl;      // LMI_REPLAY_ABL (diagnostic builds)
+    bool replay_rounds;  // LMI_REPLAY_ROUNDS: the replay as per-round launches (not one dataflow launch)
 };
 const EnvConfig& env_config();
 

@@ -14,7 +14,23 @@ from li.index import replay, replay_device
 pytestmark = pytest.mark.gpu
 
 
-def _random_lists(seed, nq, R, C, kl, tiny=(), empty=()):
+@pytest.fixture(params=["flow", "rounds"], autouse=True)
+def replay_path(request, monkeypatch):
+    """Every test on both device paths: the one-launch dataflow replay
+    (replay_flow_kernel, the default) and the per-round launches
+    (LMI_REPLAY_ROUNDS=1)."""
+    from li import _lib
+    if request.param == "rounds":
+        monkeypatch.setenv("LMI_REPLAY_ROUNDS", "1")
+    else:
+        monkeypatch.delenv("LMI_REPLAY_ROUNDS", raising=False)
+    _lib.load().lmi_config_reload()
+    yield request.param
+    monkeypatch.undo()
+    _lib.load().lmi_config_reload()
+
+
+def _random_lists(seed, nq, R, C, kl, tiny=(), empty=(), probe_empty=False):
     rng = np.random.default_rng(seed)
     size = rng.integers(40, 400, C).astype(np.int64)
     for c in tiny:
@@ -22,7 +38,9 @@ def _random_lists(seed, nq, R, C, kl, tiny=(), empty=()):
     for c in empty:
         size[c] = 0
     off = np.concatenate([[0], np.cumsum(size)])
-    live = np.nonzero(size > 0)[0]
+    # probe_empty: the router may rank a category without objects among a
+    # query's top R (a group the reference's groupby never visits)
+    live = np.arange(C) if probe_empty else np.nonzero(size > 0)[0]
     p = rng.dirichlet(np.full(live.size, 0.5))
     classes = np.stack([rng.choice(live, R, replace=False, p=p) for _ in range(nq)]).astype(np.int32)
     d = np.full((nq, R, kl), np.inf, np.float32)
@@ -39,12 +57,12 @@ def _random_lists(seed, nq, R, C, kl, tiny=(), empty=()):
     return classes, d, pos, size, ids
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(8))
 @pytest.mark.parametrize("use_threshold", [True, False])
 def test_device_replay_equals_host_replay(seed, use_threshold):
     R = 1 + seed % 4
     classes, d, pos, size, ids = _random_lists(seed, nq=700, R=R, C=24, kl=10, tiny=(3, 7),
-                                               empty=(5,))
+                                               empty=(5, 11), probe_empty=seed >= 4)
     for k_final in ([10] if R == 1 else [10, 14]):
         if R > 1 and k_final > 10 * R:
             continue
