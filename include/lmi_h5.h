@@ -61,6 +61,13 @@ int lmi_h5_write_results(const char* path, const uint32_t* knns, const double* d
 int lmi_h5_write_f32(const char* path, const char* name, int32_t dtype, int64_t rows,
                      int64_t cols, const float* buf, int32_t append);
 
+/* The same with the caller's bytes stored unconverted: elem_bytes 2 (IEEE
+ * binary16, e.g. a float16 'emb' array), 4 or 8 (little-endian IEEE).  HDF5's
+ * software float32 -> float16 conversion of lmi_h5_write_f32 is slow at
+ * 10M x 768; this writes at file speed. */
+int lmi_h5_write_stored(const char* path, const char* name, int32_t elem_bytes, int64_t rows,
+                        int64_t cols, const void* buf, int32_t append);
+
 const char* lmi_h5_last_error(void);
 
 #ifdef __cplusplus

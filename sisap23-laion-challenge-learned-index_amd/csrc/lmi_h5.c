@@ -235,3 +235,32 @@ int lmi_h5_write_f32(const char* path, const char* name, int32_t dtype, int64_t 
     if (H5Fclose(f) < 0 || !ok) return fail(LMI_E_IO, "%s/%s: write failed", path, name);
     return 0;
 }
+
+int lmi_h5_write_stored(const char* path, const char* name, int32_t elem_bytes, int64_t rows,
+                        int64_t cols, const void* buf, int32_t append) {
+    if (!path || !name || rows < 0 || cols < 1 || (!buf && rows > 0) ||
+        (elem_bytes != 2 && elem_bytes != 4 && elem_bytes != 8))
+        return fail(LMI_E_INVALID, "bad argument");
+    quiet();
+    hid_t f = append ? H5Fopen(path, H5F_ACC_RDWR, H5P_DEFAULT)
+                     : H5Fcreate(path, H5F_ACC_TRUNC, H5P_DEFAULT, H5P_DEFAULT);
+    if (f < 0) return fail(LMI_E_IO, "cannot %s %s", append ? "open" : "create", path);
+    hid_t ft = elem_bytes == 8 ? H5T_IEEE_F64LE : H5T_IEEE_F32LE, own = -1;
+    if (elem_bytes == 2) {  // IEEE binary16, as lmi_h5_write_f32 lays it out
+        own = H5Tcopy(H5T_IEEE_F32LE);
+        H5Tset_fields(own, 15, 10, 5, 0, 10);
+        H5Tset_size(own, 2);
+        H5Tset_ebias(own, 15);
+        ft = own;
+    }
+    hsize_t dims[2] = {(hsize_t)rows, (hsize_t)cols};
+    hid_t sp = H5Screate_simple(2, dims, NULL);
+    hid_t d = H5Dcreate2(f, name, ft, sp, H5P_DEFAULT, H5P_DEFAULT, H5P_DEFAULT);
+    // the memory type is the file type: the bytes go out unconverted
+    const int ok = d >= 0 && (rows == 0 || H5Dwrite(d, ft, H5S_ALL, H5S_ALL, H5P_DEFAULT, buf) >= 0);
+    if (d >= 0) H5Dclose(d);
+    H5Sclose(sp);
+    if (own >= 0) H5Tclose(own);
+    if (H5Fclose(f) < 0 || !ok) return fail(LMI_E_IO, "%s/%s: write failed", path, name);
+    return 0;
+}

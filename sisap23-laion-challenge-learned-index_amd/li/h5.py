@@ -18,7 +18,7 @@ import numpy as np
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblmi_h5.so")
 F32, F16, F64, U32, I64 = 0, 1, 2, 3, 4
 EXPORTS = ("lmi_h5_dataset_info", "lmi_h5_read_f32", "lmi_h5_read_stored", "lmi_h5_write_results",
-           "lmi_h5_write_f32", "lmi_h5_last_error")
+           "lmi_h5_write_f32", "lmi_h5_write_stored", "lmi_h5_last_error")
 _lib = None
 
 
@@ -37,6 +37,8 @@ def load():
                                              C.c_char_p, C.c_char_p]
         lib.lmi_h5_write_f32.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, C.c_int64, C.c_int64,
                                          C.c_void_p, C.c_int32]
+        lib.lmi_h5_write_stored.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, C.c_int64, C.c_int64,
+                                            C.c_void_p, C.c_int32]
         lib.lmi_h5_last_error.restype = C.c_char_p
         _lib = lib
     return _lib
@@ -84,6 +86,15 @@ def read_dataset(path: str, key: str, row0: int = 0, nrows: int = None, dtype=No
 
 
 def write_dataset(path: str, key: str, x: np.ndarray, *, fp16: bool, append: bool = False):
+    """A rank-2 dataset stored as float16 (fp16=True) or float32; a float16
+    array with fp16=True is written as it is (no conversion)."""
+    if fp16 and np.asarray(x).dtype == np.float16:
+        x = np.ascontiguousarray(x)
+        if x.ndim != 2:
+            raise ValueError("write_dataset: 2-D arrays only")
+        _check(load().lmi_h5_write_stored(_b(path), _b(key), 2, x.shape[0], x.shape[1], x.ctypes.data,
+                                          int(append)), f"{path}[{key}]")
+        return
     x = np.ascontiguousarray(x, dtype=np.float32)
     if x.ndim != 2:
         raise ValueError("write_dataset: 2-D arrays only")

@@ -50,7 +50,9 @@ def test_seeded_lists_hold_every_object_under_the_round0_bound():
     """The seeded lists of probes r >= 1 equal the unseeded ones on every entry
     below the pair's round-0 k-th distance (what the replay reads)."""
     w = workloads.clustered(n=8000, nq=300, C=16, seed=79, label_mode="skewed")
-    ix = I.DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=512, device="cuda")
+    # many chunks per bucket: the seed applies from a pair's first tile that
+    # starts after its round-0 pair published a bound
+    ix = I.DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=64, device="cuda")
     classes = torch.from_numpy(np.ascontiguousarray(
         O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :4], dtype=np.int32)).cuda()
     q = torch.from_numpy(w["q"]).cuda()

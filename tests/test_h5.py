@@ -69,6 +69,12 @@ def test_dataset_roundtrip_fp16_and_f32(tmp_path):
     np.testing.assert_array_equal(h5.read_dataset(p, "emb", 10, 5), emb[10:15].astype(np.float16))
     np.testing.assert_array_equal(h5.read_dataset(p, "pca96", 100, 50), pca[100:150])
     assert h5.read_dataset(p, "pca96").dtype == np.float32
+    # a float16 array is stored as it is (no conversion), same file layout
+    p2 = str(tmp_path / "stored.h5")
+    h5.write_dataset(p2, "emb", emb.astype(np.float16), fp16=True)
+    assert h5.dataset_info(p2, "emb") == ((300, 768), h5.F16)
+    np.testing.assert_array_equal(h5.read_dataset(p2, "emb"), emb.astype(np.float16))
+    np.testing.assert_array_equal(h5.read_dataset(p2, "emb", dtype=np.float32), emb)
     with pytest.raises(OSError, match="no dataset"):
         h5.read_dataset(p, "missing")
     with pytest.raises(OSError, match="past"):

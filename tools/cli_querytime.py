@@ -44,8 +44,9 @@ def gen(n, work):
                                       ("clip768v2", "emb", x, q, True)):
         d = os.path.join(work, "data", kind, "10M")
         os.makedirs(d, exist_ok=True)
-        h5.write_dataset(os.path.join(d, "query.h5"), key, qq.float().cpu().numpy(), fp16=fp16)
-        h5.write_dataset(os.path.join(d, "dataset.h5"), key, data.float().cpu().numpy(), fp16=fp16)
+        host = (lambda t: t.half().cpu().numpy()) if fp16 else (lambda t: t.float().cpu().numpy())
+        h5.write_dataset(os.path.join(d, "query.h5"), key, host(qq), fp16=fp16)
+        h5.write_dataset(os.path.join(d, "dataset.h5"), key, host(data), fp16=fp16)
         print(f"[gen] {kind} written ({time.time() - t0:.1f}s)", flush=True)
     nn = NeuralNetwork(input_dim=96, output_dim=122, lr=0.009, model_type="MLP-5")
     lin = [m for m in nn.model.layers if isinstance(m, torch.nn.Linear)]
@@ -61,18 +62,27 @@ def gen(n, work):
     print(f"[gen] done in {time.time() - t0:.1f}s", flush=True)
 
 
+def _child(cmd, cwd, env, log_path):
+    """Run a child with its output streamed into log_path (gpurun_out/: the
+    box sees progress) and a heartbeat on stdout every 20 s."""
+    t0 = time.time()
+    with open(log_path, "w") as f:
+        p = subprocess.Popen(cmd, cwd=cwd, env=env, stdout=f, stderr=subprocess.STDOUT)
+        while p.poll() is None:
+            time.sleep(1)
+            if int(time.time() - t0) % 20 == 0:
+                print(f"[cli_querytime] {os.path.basename(log_path)}: {time.time() - t0:.0f}s", flush=True)
+    with open(log_path) as f:
+        return p.returncode, f.read(), time.time() - t0
+
+
 def run_cli(work, bp, env_extra, label):
     env = dict(os.environ, **env_extra)
-    cmd = [sys.executable, os.path.join(PKG, "search.py"), "--size", "10M", "-bp", *bp,
+    cmd = [sys.executable, "-u", os.path.join(PKG, "search.py"), "--size", "10M", "-bp", *bp,
            "--index", os.path.join(work, "models", "lmi.pkl")]
-    t0 = time.time()
-    r = subprocess.run(cmd, cwd=work, env=env, capture_output=True, text=True)
-    wall = time.time() - t0
-    log = r.stdout + r.stderr
-    with open(os.path.join(ROOT, "gpurun_out", f"cli_{label}.log"), "w") as f:
-        f.write(log)
-    if r.returncode != 0:
-        raise SystemExit(f"cli {label} failed ({r.returncode}):\n{log[-3000:]}")
+    rc, log, wall = _child(cmd, work, env, os.path.join(ROOT, "gpurun_out", f"cli_{label}.log"))
+    if rc != 0:
+        raise SystemExit(f"cli {label} failed ({rc}):\n{log[-3000:]}")
     rs = [int(v) for v in re.findall(r"Searching with (\d+) buckets", log)]
     ts = [float(v) for v in re.findall(r"Search time: ([0-9.eE+-]+)", log)]
     return {"wall_s": round(wall, 1), "querytime_s": {str(R): t for R, t in zip(rs, ts)},
@@ -92,10 +102,11 @@ def main():
     os.makedirs(a.work, exist_ok=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     t0 = time.time()
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", "gen", "--n", str(a.n),
-                        "--work", a.work])
-    if r.returncode != 0:
-        raise SystemExit(f"gen failed ({r.returncode})")
+    rc, log, _ = _child([sys.executable, "-u", os.path.abspath(__file__), "--child", "gen", "--n",
+                         str(a.n), "--work", a.work], ROOT, dict(os.environ),
+                        os.path.join(ROOT, "gpurun_out", "cli_gen.log"))
+    if rc != 0:
+        raise SystemExit(f"gen failed ({rc}):\n{log[-3000:]}")
     gen_s = time.time() - t0
     out = {"what": "search.py (the CLI) querytime = the span search.py:116-141, per bucket count "
                    "(-bp -> R = int(bp/100*122)), from H5 files: pca96 float32, clip768v2 'emb' "
