@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Would an exact low-precision prefilter cut K2's MFMA work?  (VERDICT r2,
+next-round item 3c.)  Measured on the bench's own 10M workload, no kernel
+written: for sampled (query, probe) pairs, the int8 distance of every row of
+the probed bucket with a RIGOROUS bound on its error, and how many rows the
+bound cannot exclude.
+
+An int8 scan (v_mfma_i32_32x32x32_i8: 2x the fp16 MFMA rate, exact int32
+accumulation) of rows quantised per row, y~ = round(y / s_y) * s_y with
+s_y = max|y| / 127, and of queries quantised per query the same way, gives
+dot~ = <q~, y~> exactly; with e_y = y - y~ (|e_y,i| <= s_y / 2) and e_q:
+    |<q, y> - dot~| <= sum |q_i| |e_y,i| + sum |y~_i| |e_q,i|
+                    <= (s_y / 2) ||q||_1 + (s_q / 2) ||y~||_1     (bound_abs)
+so |d - d~| <= bound_abs / (||q|| ||y||) with d~ = 1 - dot~ / (||q|| ||y||).
+A row can be dropped exactly only when d~ - bound > the pair's final k-th
+distance (the best case for the prefilter: the final threshold known from
+the start).  The survivors must then be rescored in fp16; a tile of 256
+pairs re-reads every row that survives for ANY of its pairs.  (fp8 e4m3
+carries 3 mantissa bits against int8's 7 at the row's largest element: its
+bound is wider still.)
+
+    python tools/prefilter_study.py [--pairs 256] [--scale 10M]
+Writes profiles/r03_prefilter_study.json (run on the GPU box: torch on the
+device for the float64 distances)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
+
+
+def main():
+    import numpy as np
+    import torch
+    from li import synth
+    from li.index import BucketLayout, DeviceRouter
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=256)
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--k", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    t0 = time.time()
+    x, q, qn, xn, layers = synth.build_lmi_workload(a.n, 10_000, 122, "MLP-5", dev)
+    router = DeviceRouter(layers, device=dev)
+    labels = router.argmax(xn).cpu().numpy()
+    del xn
+    classes = router.topr(qn, 4)[0].cpu().numpy()
+    lay = BucketLayout.from_labels(labels, 122)
+    order = torch.from_numpy(lay.order).to(dev)
+    rng = np.random.default_rng(1)
+    # the pairs of one popular bucket (a tile's worth) and random pairs
+    c_pop = int(np.bincount(classes.ravel(), minlength=122).argmax())
+    qs_pop = np.nonzero((classes == c_pop).any(axis=1))[0][: a.pairs]
+    res = {"what": __doc__.split("\n\n")[0], "n": a.n, "k": a.k, "workload": "bench.py 10M synthetic",
+           "build_s": round(time.time() - t0, 1)}
+
+    def study(q_idx, c_of):
+        stats = {"pairs": 0, "rows": 0, "int8_survivors": 0}
+        union8 = {}
+        cache = {}
+        for qi in q_idx:
+            c = int(c_of(qi))
+            a0, b0 = int(lay.bucket_off[c]), int(lay.bucket_off[c + 1])
+            if c not in cache:
+                cache.clear()
+                y = x[order[a0:b0]].double()                  # fp16 values, exact
+                sy = y.abs().amax(dim=1) / 127                # int8 per-row scale
+                yi = torch.round(y / sy[:, None])
+                cache[c] = (y, y.norm(dim=1), sy, yi, (yi * sy[:, None]).abs().sum(dim=1))
+            y, ny, sy, yi, y8l1 = cache[c]
+            qq = q[qi].double()
+            nq_ = qq.norm()
+            d = 1 - (y @ qq) / (ny * nq_)
+            thr = torch.topk(d, a.k, largest=False).values[-1]
+            # int8 per-row / per-query quantisation, exact integer dot
+            sq = qq.abs().max() / 127
+            qi8 = torch.round(qq / sq)
+            dot8 = (yi @ qi8) * sy * sq
+            bound = (sy / 2) * qq.abs().sum() + (sq / 2) * y8l1
+            d8 = 1 - dot8 / (ny * nq_)
+            surv8 = (d8 - bound / (ny * nq_)) <= thr
+            stats["pairs"] += 1
+            stats["rows"] += b0 - a0
+            stats["int8_survivors"] += int(surv8.sum())
+            u = union8.setdefault(c, torch.zeros(b0 - a0, dtype=torch.bool, device=dev))
+            u |= surv8
+        stats["int8_survivor_frac"] = stats["int8_survivors"] / max(stats["rows"], 1)
+        tot = sum(int(v.numel()) for v in union8.values())
+        stats["rows_surviving_for_any_pair_of_the_sample"] = sum(int(v.sum()) for v in union8.values())
+        stats["union_frac"] = stats["rows_surviving_for_any_pair_of_the_sample"] / max(tot, 1)
+        return stats
+
+    res["tile_of_popular_bucket"] = {"bucket": c_pop, **study(qs_pop, lambda qi: c_pop)}
+    rnd = rng.choice(10_000, a.pairs, replace=False)
+    rr = rng.integers(0, 4, a.pairs)
+    res["random_pairs"] = study(rnd, lambda qi: classes[qi, rr[list(rnd).index(qi)]])
+    print(json.dumps(res, indent=1))
+    with open(os.path.join(ROOT, "profiles", "r03_prefilter_study.json"), "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
