@@ -998,7 +998,8 @@ class GraphedSearch:
     of the graph's pinned output buffer, valid until the next run."""
 
     def __init__(self, searcher: "Searcher", q_nav, q_search, R: int,
-                 k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32"):
+                 k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
+                 capture: bool = True):
         s = searcher
         ix = s.index
         dev = ix.device
@@ -1006,8 +1007,10 @@ class GraphedSearch:
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
         self.use_threshold, self.dist = use_threshold, dist
         G = ix.world
-        if k_round > _lib.LMI_MAX_K or (G > 1 and torch.distributed.get_backend(s.group) != "nccl"):
-            raise ValueError("graph capture needs k_round <= 16 and RCCL collectives")
+        if k_round > _lib.LMI_MAX_K or (capture and G > 1 and
+                                       torch.distributed.get_backend(s.group) != "nccl"):
+            raise ValueError("graph capture needs k_round <= 16 and RCCL collectives "
+                             "(capture=False runs the same step eagerly, e.g. over gloo)")
         nav = _host_array(q_nav)
         qs = _host_array(q_search)
         nq, d, dn = int(qs.shape[0]), ix.d, int(nav.shape[1])
@@ -1086,6 +1089,16 @@ class GraphedSearch:
         # raised before entering a collective would otherwise leave the others
         # waiting in the next one; a rank that fails inside a collective is
         # ended by the process group's timeout, li.dist.init_from_env)
+        self._step = None
+        if not capture:
+            # the same step, launched eagerly per run (the multi-process gloo
+            # rehearsal of the sharded upload on one GPU: tests/test_gpu_dist.py)
+            buf = step()
+            torch.cuda.synchronize(dev)
+            self.h = torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
+            self.graph = None
+            self._step = step
+            return
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         err = None
@@ -1160,7 +1173,10 @@ class GraphedSearch:
                 raise ValueError("stage both q_nav and q_search")
             if not self.stage(q_nav, q_search):
                 return self._eager(q_nav, q_search)
-        self.graph.replay()
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.h.copy_(self._step(), non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
         hd, ha, st, rst = answer_views(self.h, self.nq, self.w)
         if st & _lib.LMI_STATUS_INTERNAL or rst:

@@ -39,6 +39,13 @@ def main(out_path):
         res[f"{dist_}_lists_st"] = np.array([int(st.item())])
     d, a = s.search(qn, q, 4, k=10, semantics="exact")
     res["exact_d"], res["exact_a"] = d, a
+    # the graphed step's G > 1 path (each rank uploads its block, routes it,
+    # one all-gather of queries + classes), run eagerly: gloo cannot be
+    # captured; RCCL runs the same step as a graph on the 8-GPU node
+    for dist_ in ("f32", "f64"):
+        g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_, capture=False)
+        d, a = g.run()
+        res[f"graph_{dist_}_d"], res[f"graph_{dist_}_a"] = d.copy(), a.copy()
     if rank == 0:
         np.savez(out_path, **res)
     dist.barrier()

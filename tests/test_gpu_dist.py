@@ -60,3 +60,7 @@ def test_two_process_product_path_equals_one_process(world, tmp_path):
     d, a = s.search(qn, q, 4, k=10, semantics="exact")
     np.testing.assert_array_equal(got["exact_d"], d)
     np.testing.assert_array_equal(got["exact_a"], a)
+    for dist_ in ("f32", "f64"):
+        d, a = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_).run()
+        np.testing.assert_array_equal(got[f"graph_{dist_}_d"], d)
+        np.testing.assert_array_equal(got[f"graph_{dist_}_a"], a)
