@@ -272,7 +272,7 @@ def h2d_ms(gs, reps=10):
     """The step's host -> device upload alone (this rank's staged block), HIP
     events on the current stream: ms per copy and GB/s."""
     dev = gs.searcher.index.device
-    g = gs.searcher.index.rank
+    g = gs.rank_in_group
     dst = torch.empty_like(gs.d_blk)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     dst.copy_(gs.h_blk[g], non_blocking=True)

@@ -1022,10 +1022,17 @@ class GraphedSearch:
             qs.dtype == np.float16 or _np_fp16_exact(qs))
         self.qmode = _lib.LMI_Q_F16 if self.f16_up else _lib.LMI_Q_F32
         f64 = dist == "f64"
+        # the batch is shared over the ranks of the process group (the index's
+        # world is the stripe count; they differ only in a one-process
+        # rehearsal of one stripe, tools/shard_step.py)
+        Gi = G
+        G = torch.distributed.get_world_size(s.group) if Gi > 1 else 1
+        g = torch.distributed.get_rank(s.group) if Gi > 1 else 0
         self.per = per = -(-nq // G)
         self.wq = wq = d // 2 if self.f16_up else d          # int32 words per staged row
         self.bw = bw = per * dn + per * wq + (per * R if G > 1 else 0)
         pin = torch.cuda.is_available()
+        self.bw_all = bw
         self.h_blk = torch.zeros((G, bw), dtype=torch.int32, pin_memory=pin)
         if not self.stage(nav, qs):
             raise ValueError("staging failed")
@@ -1039,7 +1046,7 @@ class GraphedSearch:
         self.cls = torch.empty((G * per, R), dtype=torch.int32, device=dev) if G > 1 else None
         bsz, p2id = s._device_tables()
         self.w = k_round if R == 1 else k
-        g = ix.rank
+        self.rank_in_group = g
         copy_stream = torch.cuda.Stream(dev)
 
         def step():
@@ -1110,7 +1117,7 @@ class GraphedSearch:
             torch.cuda.synchronize(dev)
         except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
             err = e
-        if G > 1:
+        if Gi > 1:
             ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
             torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
             if int(ok.item()) == 0:

@@ -48,8 +48,25 @@ for W in map(int, a.worlds.split(",")):
     for _ in range(a.steps):
         g.run()
     torch.cuda.synchronize(); elg = (time.perf_counter() - t0) / a.steps * 1e3
+    # the graph uploads the whole batch here (a one-process group); on W GPUs
+    # each rank uploads 1/W of it and the ranks all-gather it over xGMI
+    # (not measurable on one GPU): the projection swaps the whole-batch H2D
+    # for the 1/W one, all-gather excluded
+    full = g.h_blk[0]
+    part = full[: full.numel() // W]
+    dst = torch.empty(full.numel(), dtype=torch.int32, device=dev)
+    def h2d(src, n=20):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dst[: src.numel()].copy_(src, non_blocking=True); e0.record()
+        for _ in range(n):
+            dst[: src.numel()].copy_(src, non_blocking=True)
+        e1.record(); torch.cuda.synchronize(); return e0.elapsed_time(e1) / n
+    h_full, h_part = h2d(full), h2d(part)
     del g
-    print(f"world {W} chunk {ck}: step {el:.3f} ms eager, {elg:.3f} ms graph -> "
-          f"{10000 / min(el, elg) * 1e3:.0f} q/s per rank-step; breakdown {br}", flush=True)
+    proj = elg - h_full + h_part
+    print(f"world {W} chunk {ck}: step {el:.3f} ms eager (device-resident queries), {elg:.3f} ms graph "
+          f"(whole-batch H2D {h_full:.3f} ms); with the 1/{W} upload ({h_part:.3f} ms): {proj:.3f} ms "
+          f"-> {10000 / proj * 1e3 * W:.0f} q/s on {W} GPUs (all-gathers over xGMI excluded); "
+          f"breakdown {br}", flush=True)
     del ix, s; torch.cuda.empty_cache()
 dist.destroy_process_group()
