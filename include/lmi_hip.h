@@ -271,8 +271,10 @@ int lmi_replay_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list
  * (checked bit for bit by tests/test_gpu_replay.py), no host round trip.
  * classes, lists_d, lists_pos, bucket_size, pos_to_id, thr_round0 (nullable),
  * dists_out, anns_out are device pointers; status (device int32, caller
- * zeroes it) is OR-ed with nonzero bits on an internal inconsistency (a list
- * shorter than its bucket, a position out of range).  k_list >= k_round,
+ * zeroes it) is OR-ed with nonzero bits on an internal inconsistency (1, 2: a
+ * list shorter than its bucket; 4: a position out of range; 8: a round's group
+ * never completed in the one-launch replay, which then drains instead of
+ * waiting forever).  k_list >= k_round,
  * k_round <= 32, k_final <= 64.  Asynchronous on `stream`; workspace of
  * lmi_replay_device_workspace_bytes bytes. */
 size_t lmi_replay_device_workspace_bytes(int32_t nq, int32_t R, int32_t k_list, int32_t k_round,

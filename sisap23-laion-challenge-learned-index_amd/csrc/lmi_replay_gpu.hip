@@ -661,9 +661,19 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
             }
             __syncthreads();
         } else {
-            if (tid == 0)
-                while (__hip_atomic_load(&f.done[item], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < g1 - g0)
+            if (tid == 0) {
+                // bounded (seconds): a group count that never completes would be
+                // a layout bug; flag it (status 8) and drain rather than hang
+                for (uint32_t spins = 0;
+                     __hip_atomic_load(&f.done[item], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < g1 - g0;
+                     ++spins) {
+                    if (spins >= (1u << 22)) {
+                        atomicOr(f.base.status, 8);
+                        break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
+                }
+            }
             __syncthreads();
         }
         RoundArgs a = f.base;
