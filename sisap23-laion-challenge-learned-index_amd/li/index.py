@@ -23,6 +23,8 @@ from __future__ import annotations
 
 import ctypes as C
 import dataclasses
+import os
+import time
 from typing import Optional, Sequence
 
 import numpy as np
@@ -1047,6 +1049,10 @@ class GraphedSearch:
         bsz, p2id = s._device_tables()
         self.w = k_round if R == 1 else k
         self.rank_in_group = g
+        self.G = G
+        # collectives inside a replayed graph are GPU work the process group's
+        # watchdog does not track: run() bounds its own wait instead
+        self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
         copy_stream = torch.cuda.Stream(dev)
 
         def step():
@@ -1184,7 +1190,10 @@ class GraphedSearch:
             self.graph.replay()
         else:
             self.h.copy_(self._step(), non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
+        if self.G > 1 and self.graph is not None:
+            _wait_with_deadline(dev, self.timeout_s)
+        else:
+            torch.cuda.current_stream(dev).synchronize()
         hd, ha, st, rst = answer_views(self.h, self.nq, self.w)
         if st & _lib.LMI_STATUS_INTERNAL or rst:
             raise RuntimeError(f"search: internal status {st}/{rst}")
@@ -1197,6 +1206,25 @@ class GraphedSearch:
                                     _as_torch(_host_array(q_search), dev, torch.float32),
                                     self.R, k=self.k, k_round=self.k_round,
                                     use_threshold=self.use_threshold, dist=self.dist)
+
+
+def _wait_with_deadline(dev, timeout_s: float) -> None:
+    """Wait for the current stream's work, raising after `timeout_s`: a graph
+    replay whose all-gather waits for a rank that died never completes, and
+    RCCL kernels captured in a graph are outside the process group's watchdog
+    (li.dist.init_from_env).  The caller should end the process: the stalled
+    kernels stay queued on the device until its context is torn down."""
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    deadline = time.monotonic() + timeout_s
+    spins = 0
+    while not ev.query():
+        spins += 1
+        if spins > 1000:
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"search step not finished after {timeout_s:.0f} s: a peer rank "
+                                   "stopped inside the step's collectives; end this process")
+            time.sleep(1e-4)
 
 
 def _np_fp16_exact(x: np.ndarray) -> bool:
