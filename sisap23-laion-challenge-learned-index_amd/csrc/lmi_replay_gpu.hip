@@ -664,15 +664,19 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
             if (tid == 0) {
                 // bounded (seconds): a group count that never completes would be
                 // a layout bug; flag it (status 8) and drain rather than hang
+                // (relaxed polls, one acquire fence after: an acquire load per
+                //  poll invalidates the XCD's L2 every time, which measured the
+                //  replay 5x slower than its per-round launches)
                 for (uint32_t spins = 0;
-                     __hip_atomic_load(&f.done[item], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < g1 - g0;
+                     __hip_atomic_load(&f.done[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g1 - g0;
                      ++spins) {
                     if (spins >= (1u << 22)) {
                         atomicOr(f.base.status, 8);
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    __builtin_amdgcn_s_sleep(2);
                 }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             }
             __syncthreads();
         }

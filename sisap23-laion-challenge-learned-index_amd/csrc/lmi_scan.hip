@@ -1476,7 +1476,9 @@ int num_cus() {
         if (hipGetDevice(&dev) != hipSuccess) dev = 0;
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 256;
     });
-    return n > 0 ? n : 256;
+    const int cus = n > 0 ? n : 256;
+    const int w = env_config().scan_wgs;
+    return w > 0 ? std::min(w, cus) : cus;
 }
 
 // ---- optional event timing of the scan kernel ------------------------------

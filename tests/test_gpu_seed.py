@@ -46,7 +46,20 @@ def test_seeded_search_equals_unseeded(mode, R, k, dist, monkeypatch):
     assert O.compare_lists(rd, ra, d1, a1, atol=atol, tie=tie) == 0
 
 
-def test_seeded_lists_hold_every_object_under_the_round0_bound():
+@pytest.fixture
+def few_scan_workgroups(monkeypatch):
+    """Two persistent scan workgroups (LMI_SCAN_WGS): tiles run in turn, so
+    later tiles start after round-0 pairs published their bounds (with one
+    workgroup per CU every tile of a small test starts at once)."""
+    from li import _lib
+    monkeypatch.setenv("LMI_SCAN_WGS", "2")
+    _lib.load().lmi_config_reload()
+    yield
+    monkeypatch.delenv("LMI_SCAN_WGS")
+    _lib.load().lmi_config_reload()
+
+
+def test_seeded_lists_hold_every_object_under_the_round0_bound(few_scan_workgroups):
     """The seeded lists of probes r >= 1 equal the unseeded ones on every entry
     below the pair's round-0 k-th distance (what the replay reads)."""
     w = workloads.clustered(n=8000, nq=300, C=16, seed=79, label_mode="skewed")

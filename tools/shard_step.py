@@ -66,7 +66,7 @@ for W in map(int, a.worlds.split(",")):
     proj = elg - h_full + h_part
     print(f"world {W} chunk {ck}: step {el:.3f} ms eager (device-resident queries), {elg:.3f} ms graph "
           f"(whole-batch H2D {h_full:.3f} ms); with the 1/{W} upload ({h_part:.3f} ms): {proj:.3f} ms "
-          f"-> {10000 / proj * 1e3 * W:.0f} q/s on {W} GPUs (all-gathers over xGMI excluded); "
+          f"-> {10000 / proj * 1e3:.0f} q/s on {W} GPUs (all-gathers over xGMI excluded); "
           f"breakdown {br}", flush=True)
     del ix, s; torch.cuda.empty_cache()
 dist.destroy_process_group()
