@@ -804,10 +804,11 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     // bytes, 96 MFMAs of 16 cycles per wave-block: timing of the shape only),
     // 67 = the full kernel without the epilogue, 68 = 67 with 16x16x32
     constexpr bool kM16 = ABL == 66 || ABL == 68;
-    constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6 || ABL == 66;
-    constexpr bool kNoEpi = kDmaOnly || ABL == 5 || ABL == 6 || ABL == 66 || ABL == 67 || ABL == 68;
+    constexpr bool kNoDma = ABL == 3 || ABL == 4 || ABL == 5 || ABL == 6 || ABL == 66 || ABL == 69 || ABL == 70;
+    constexpr bool kNoEpi = kDmaOnly || ABL == 5 || ABL == 6 || ABL == 66 || ABL == 67 || ABL == 68 ||
+                            ABL == 69 || ABL == 70;
     constexpr bool kNoIns = ABL == 1 || ABL == 4;
-    constexpr bool kNoBar = ABL == 6 || ABL == 66 || ABL == 21;
+    constexpr bool kNoBar = ABL == 6 || ABL == 66 || ABL == 21 || ABL == 69 || ABL == 70;
     // bound exchange period in blocks (diagnostic: 40 none, 41 every 4, 42 every 8, 43 every 16)
     constexpr int kXch = ABL == 40 ? 0 : ABL == 41 ? 4 : ABL == 42 ? 8 : ABL == 43 ? 16 : 32;
     // (ABL 53, round 1's placement: an LDS-DMA issue holds its wave for ~45-60
@@ -1220,7 +1221,12 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 for (int tt = 0; tt < 3; ++tt) af[tt] = LMI_A3(tt);
 #pragma unroll
                 for (int tt = 0; tt < 16; ++tt) {
-                    if (tt + 3 < 16) af[tt + 3] = LMI_A3(tt + 3);
+                    // (ABL 69: every other A fragment re-used instead of read;
+                    //  ABL 70: only the first three read: the LDS reads' share
+                    //  of the MFMA stream's power, timing only)
+                    if (tt + 3 < 16)
+                        af[tt + 3] = (ABL == 70 || (ABL == 69 && ((tt + 3) & 1))) ? af[tt + 2 - (ABL == 70 ? 2 : 0)]
+                                                                                   : LMI_A3(tt + 3);
                     acc = (j == 0 && tt == 0)        ? mfma_first_v(af[0], qf[0])
                           : (j == NST - 1 && tt == 15 && ABL != 61) ? mfma_last_v(acc, af[tt], qf[j * 16 + tt])
                                                        : mfma_acc_v(acc, af[tt], qf[j * 16 + tt]);
@@ -1272,6 +1278,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         atomicMin(&lmi_dbg[10], (unsigned long long)rt0);
         atomicMax(&lmi_dbg[11], (unsigned long long)rt1);
         atomicAdd(&lmi_dbg[12], 1ull);
+        atomicMax(&lmi_dbg[13], (unsigned long long)rt0);  // the last workgroup start
+        atomicMin(&lmi_dbg[14], (unsigned long long)rt1);  // the first workgroup end
     }
 #endif
 }
@@ -1560,6 +1568,8 @@ int launch_scan3(const Scan2Args& b, hipStream_t s) {
     if (abl == 66) return launch_scan3_v<KL, 66>(b, s);
     if (abl == 67) return launch_scan3_v<KL, 67>(b, s);
     if (abl == 68) return launch_scan3_v<KL, 68>(b, s);
+    if (abl == 69) return launch_scan3_v<KL, 69>(b, s);
+    if (abl == 70) return launch_scan3_v<KL, 70>(b, s);
     if (abl == 61) return launch_scan3_v<KL, 61>(b, s);
     if (abl == 62) return launch_scan3_v<KL, 62>(b, s);
     if (abl == 64) return launch_scan3_v<KL, 64>(b, s);
@@ -1905,6 +1915,7 @@ extern "C" int lmi_debug_counters(unsigned long long* out16) {
     unsigned long long z[16] = {};
     if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(lmi::lmi_dbg), sizeof(z)) != hipSuccess) return LMI_E_HIP;
     z[10] = ~0ull;
+    z[14] = ~0ull;
     if (hipMemcpyToSymbol(HIP_SYMBOL(lmi::lmi_dbg), z, sizeof(z)) != hipSuccess) return LMI_E_HIP;
     return LMI_OK;
 }
