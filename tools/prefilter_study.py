@@ -74,8 +74,10 @@ def main():
     def study(q_idx, c_of):
         stats = {"pairs": 0, "rows": 0, "int8_survivors": 0, "int8_survivors_self_threshold": 0,
                  "int8_survivors_cs": 0, "int8_survivors_cs_self_threshold": 0,
-                 "bound_median": [], "bound_cs_median": [], "kth_gap_median": []}
+                 "bound_median": [], "bound_cs_median": [], "kth_gap_median": [],
+                 "wave_blocks": 0, "wave_blocks_with_survivor": 0}
         union8 = {}
+        wave, wave_n = {}, {}
         cache = {}
         for qi in q_idx:
             c = int(c_of(qi))
@@ -119,6 +121,18 @@ def main():
             stats["kth_gap_median"].append(float((d.median() - thr)))
             u = union8.setdefault(c, torch.zeros(b0 - a0, dtype=torch.bool, device=dev))
             u |= surv8
+            # a wave's 32 pairs (consecutive pairs of the sample): the 32-row
+            # blocks where at least one of them keeps a survivor (C-S bound,
+            # the final threshold) are the blocks the wave would rescore in fp16
+            wv = wave.setdefault(c, torch.zeros(b0 - a0, dtype=torch.bool, device=dev))
+            wv |= (d8 - bnd_cs) <= thr
+            wave_n[c] = wave_n.get(c, 0) + 1
+            if wave_n[c] == 32:
+                m = wv[: wv.numel() // 32 * 32].view(-1, 32).any(dim=1)
+                stats["wave_blocks"] += int(m.numel())
+                stats["wave_blocks_with_survivor"] += int(m.sum())
+                wave_n[c] = 0
+                wv.zero_()
         stats["int8_survivor_frac"] = stats["int8_survivors"] / max(stats["rows"], 1)
         stats["int8_survivor_frac_self_threshold"] = stats["int8_survivors_self_threshold"] / max(stats["rows"], 1)
         for key in ("int8_survivors_cs", "int8_survivors_cs_self_threshold"):
@@ -131,6 +145,8 @@ def main():
             m = v[: v.numel() // 32 * 32].view(-1, 32).any(dim=1)
             nb += int(m.numel()); nbs += int(m.sum())
         stats["blocks32_with_any_survivor_frac"] = nbs / max(nb, 1)
+        stats["wave32_blocks32_with_survivor_frac"] = (stats["wave_blocks_with_survivor"] /
+                                                       max(stats["wave_blocks"], 1))
         tot = sum(int(v.numel()) for v in union8.values())
         stats["rows_surviving_for_any_pair_of_the_sample"] = sum(int(v.sum()) for v in union8.values())
         stats["union_frac"] = stats["rows_surviving_for_any_pair_of_the_sample"] / max(tot, 1)
