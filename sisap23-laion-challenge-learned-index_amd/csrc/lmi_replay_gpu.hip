@@ -624,6 +624,9 @@ struct FlowArgs {
     int32_t* uraw;            // [R][nq * kl]
     int32_t* done;            // [R][C + 1] merges of round r-1 done per item (zeroed)
     int32_t* work;            // dequeue counter (zeroed)
+    int32_t per_round;        // 1: one launch per round, item = item0 + blockIdx.x, no waits
+                              //    (the kernel boundary orders the rounds)
+    int32_t item0;
     int32_t fs, k_final, w_out;
     const int64_t* pos_to_id;
     int64_t n_total;
@@ -636,8 +639,13 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int C = f.base.C, R = f.base.R, kr = f.base.kr, nq = f.base.nq;
     const int kl_use = min(kr, f.base.kl);
-    for (;;) {
-        if (tid == 0) s_item = atomicAdd(f.work, 1);
+    for (int it = 0;; ++it) {
+        if (f.per_round) {
+            if (it > 0) break;
+            s_item = f.item0 + blockIdx.x;
+        } else if (tid == 0) {
+            s_item = atomicAdd(f.work, 1);
+        }
         __syncthreads();
         const int item = s_item;
         __syncthreads();  // (s_item is rewritten next iteration)
@@ -660,7 +668,7 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
                 if (f.thr_round0) f.thr[q] = f.thr_round0[q];
             }
             __syncthreads();
-        } else {
+        } else if (!f.per_round) {
             if (tid == 0) {
                 // bounded (seconds): a group count that never completes would be
                 // a layout bug; flag it (status 8) and drain rather than hang
@@ -757,6 +765,7 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
                 if (lane == 0) f.thr[q] = thr_next;
             }
         }
+        if (f.per_round) continue;
         __threadfence();
         __syncthreads();
         if (!last) {
@@ -1001,9 +1010,14 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
     hipLaunchKernelGGL(replay_groups_kernel, dim3(C + 1, R), dim3(kTG), 0, st, classes, nq, R, C, groups, gb);
     LMI_LAUNCH_CHECK("replay_groups_kernel");
     if (!env_config().replay_rounds) {
-        // the rounds as one persistent dataflow launch (replay_flow_kernel)
+        // each round's groups and merges in one launch (replay_flow_kernel,
+        // per_round); LMI_REPLAY_FLOW: all rounds in one persistent dataflow
+        // launch, items waiting on the previous round's merges (measured 5x
+        // slower: every agent-scope release / acquire writes back / invalidates
+        // the XCD's L2 on gfx950)
         int32_t* done = (int32_t*)(ws + s.done);
-        LMI_HIP_TRY(hipMemsetAsync(done, 0, (size_t)R * (C + 1) * 4 + 4, st));
+        if (env_config().replay_flow)
+            LMI_HIP_TRY(hipMemsetAsync(done, 0, (size_t)R * (C + 1) * 4 + 4, st));
         FlowArgs f{};
         f.base.classes = classes;
         f.base.nq = nq;
@@ -1040,10 +1054,19 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         f.n_total = n_total;
         f.dists = dists_out;
         f.anns = anns_out;
-        const int items = (C + 1) * R;
-        hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)std::min(items, num_cus_replay())),
-                           dim3(kTG), 0, st, f);
-        LMI_LAUNCH_CHECK("replay_flow_kernel");
+        if (env_config().replay_flow) {
+            const int items = (C + 1) * R;
+            hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)std::min(items, num_cus_replay())),
+                               dim3(kTG), 0, st, f);
+            LMI_LAUNCH_CHECK("replay_flow_kernel");
+            return LMI_OK;
+        }
+        f.per_round = 1;
+        for (int r = 0; r < R; ++r) {
+            f.item0 = r * (C + 1);
+            hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)(C + 1)), dim3(kTG), 0, st, f);
+            LMI_LAUNCH_CHECK("replay_flow_kernel");
+        }
         return LMI_OK;
     }
     int cur = 0;  // F lives in buffer cur; the merge writes the other one
