@@ -42,7 +42,6 @@ EnvConfig read_env() {
     e.router_fma = env_b("LMI_ROUTER_FMA");
     e.router_qg = env_i("LMI_ROUTER_QG", 0);
     e.replay_abl = env_i("LMI_REPLAY_ABL", 0);
-    e.replay_rounds = env_b("LMI_REPLAY_ROUNDS");
     e.replay_flow = env_b("LMI_REPLAY_FLOW");
     return e;
 }

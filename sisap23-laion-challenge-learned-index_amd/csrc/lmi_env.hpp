@@ -22,8 +22,7 @@ struct EnvConfig {
     bool router_fma;     // LMI_ROUTER_FMA: FMA-chain router instead of MFMA
     int router_qg;       // LMI_ROUTER_QG: 1/2/4 query groups per workgroup, 0 = auto
     int replay_abl;      // LMI_REPLAY_ABL (diagnostic builds)
-    bool replay_rounds;  // LMI_REPLAY_ROUNDS: round 2's launches (groups, merge per round)
-    bool replay_flow;    // LMI_REPLAY_FLOW: all rounds as one dataflow launch (slower, kept for study)
+    bool replay_flow;    // LMI_REPLAY_FLOW: all rounds as one dataflow launch (slower, a study)
 };
 const EnvConfig& env_config();
 

@@ -607,8 +607,10 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
 // replay_merge_kernel, one wave per query) and signals the items of round
 // r+1 that hold those queries.  An item only waits for items dequeued before
 // it, which are held by running workgroups, so the grid always drains.
-// Replaces 2R + 1 launches (R groups, R merges, the thresholds / output) and
-// the gaps between them; the results are the same arrays (tests/test_gpu_replay.py).
+// Would replace 2R + 1 launches (R groups, R merges, the thresholds / output)
+// and the gaps between them; the results are the same arrays
+// (tests/test_gpu_replay.py), but it measured 4x slower (LMI_REPLAY_FLOW only,
+// see lmi_replay_device).
 // ---------------------------------------------------------------------------
 struct FlowArgs {
     RoundArgs base;           // classes, nq, R, kl, kr, C, lists, bucket sizes, status
@@ -624,9 +626,6 @@ struct FlowArgs {
     int32_t* uraw;            // [R][nq * kl]
     int32_t* done;            // [R][C + 1] merges of round r-1 done per item (zeroed)
     int32_t* work;            // dequeue counter (zeroed)
-    int32_t per_round;        // 1: one launch per round, item = item0 + blockIdx.x, no waits
-                              //    (the kernel boundary orders the rounds)
-    int32_t item0;
     int32_t fs, k_final, w_out;
     const int64_t* pos_to_id;
     int64_t n_total;
@@ -639,13 +638,8 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int C = f.base.C, R = f.base.R, kr = f.base.kr, nq = f.base.nq;
     const int kl_use = min(kr, f.base.kl);
-    for (int it = 0;; ++it) {
-        if (f.per_round) {
-            if (it > 0) break;
-            s_item = f.item0 + blockIdx.x;
-        } else if (tid == 0) {
-            s_item = atomicAdd(f.work, 1);
-        }
+    for (;;) {
+        if (tid == 0) s_item = atomicAdd(f.work, 1);
         __syncthreads();
         const int item = s_item;
         __syncthreads();  // (s_item is rewritten next iteration)
@@ -668,7 +662,7 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
                 if (f.thr_round0) f.thr[q] = f.thr_round0[q];
             }
             __syncthreads();
-        } else if (!f.per_round) {
+        } else {
             if (tid == 0) {
                 // bounded (seconds): a group count that never completes would be
                 // a layout bug; flag it (status 8) and drain rather than hang
@@ -765,7 +759,6 @@ __global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
                 if (lane == 0) f.thr[q] = thr_next;
             }
         }
-        if (f.per_round) continue;
         __threadfence();
         __syncthreads();
         if (!last) {
@@ -1009,15 +1002,15 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
     // every round's groups in one launch ((C + 1) x R workgroups)
     hipLaunchKernelGGL(replay_groups_kernel, dim3(C + 1, R), dim3(kTG), 0, st, classes, nq, R, C, groups, gb);
     LMI_LAUNCH_CHECK("replay_groups_kernel");
-    if (!env_config().replay_rounds) {
-        // each round's groups and merges in one launch (replay_flow_kernel,
-        // per_round); LMI_REPLAY_FLOW: all rounds in one persistent dataflow
-        // launch, items waiting on the previous round's merges (measured 5x
-        // slower: every agent-scope release / acquire writes back / invalidates
-        // the XCD's L2 on gfx950)
+    if (env_config().replay_flow) {
+        // LMI_REPLAY_FLOW (a study, not the default): all rounds in one
+        // persistent dataflow launch, items waiting on the previous round's
+        // merges.  Measured 4x slower than the per-round launches below (489
+        // vs 117 us on the bench's lists): every agent-scope release / acquire
+        // writes back / invalidates the XCD's L2 on gfx950, and a group's
+        // merges run one wave per query instead of one thread per element.
         int32_t* done = (int32_t*)(ws + s.done);
-        if (env_config().replay_flow)
-            LMI_HIP_TRY(hipMemsetAsync(done, 0, (size_t)R * (C + 1) * 4 + 4, st));
+        LMI_HIP_TRY(hipMemsetAsync(done, 0, (size_t)R * (C + 1) * 4 + 4, st));
         FlowArgs f{};
         f.base.classes = classes;
         f.base.nq = nq;
@@ -1054,19 +1047,10 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         f.n_total = n_total;
         f.dists = dists_out;
         f.anns = anns_out;
-        if (env_config().replay_flow) {
-            const int items = (C + 1) * R;
-            hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)std::min(items, num_cus_replay())),
-                               dim3(kTG), 0, st, f);
-            LMI_LAUNCH_CHECK("replay_flow_kernel");
-            return LMI_OK;
-        }
-        f.per_round = 1;
-        for (int r = 0; r < R; ++r) {
-            f.item0 = r * (C + 1);
-            hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)(C + 1)), dim3(kTG), 0, st, f);
-            LMI_LAUNCH_CHECK("replay_flow_kernel");
-        }
+        const int items = (C + 1) * R;
+        hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)std::min(items, num_cus_replay())),
+                           dim3(kTG), 0, st, f);
+        LMI_LAUNCH_CHECK("replay_flow_kernel");
         return LMI_OK;
     }
     int cur = 0;  // F lives in buffer cur; the merge writes the other one

@@ -14,18 +14,13 @@ from li.index import replay, replay_device
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["fused", "rounds", "flow"], autouse=True)
+@pytest.fixture(params=["rounds", "flow"], autouse=True)
 def replay_path(request, monkeypatch):
-    """Every test on the three device paths: one launch per round of
-    replay_flow_kernel (groups + merges, the default), round 2's separate
-    group / merge launches (LMI_REPLAY_ROUNDS=1) and all rounds as one
-    dataflow launch (LMI_REPLAY_FLOW=1)."""
+    """Every test on both device paths: the per-round launches (the default)
+    and all rounds as one dataflow launch (LMI_REPLAY_FLOW=1, a study)."""
     from li import _lib
-    monkeypatch.delenv("LMI_REPLAY_ROUNDS", raising=False)
     monkeypatch.delenv("LMI_REPLAY_FLOW", raising=False)
-    if request.param == "rounds":
-        monkeypatch.setenv("LMI_REPLAY_ROUNDS", "1")
-    elif request.param == "flow":
+    if request.param == "flow":
         monkeypatch.setenv("LMI_REPLAY_FLOW", "1")
     _lib.load().lmi_config_reload()
     yield request.param
