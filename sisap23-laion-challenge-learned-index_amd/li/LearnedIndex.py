@@ -119,6 +119,7 @@ class LearnedIndex(Logger):
     _trusted = None
     _searcher = None
     _attached_labels = None
+    _cat_written = None
 
     def __init__(self):
         self.model = None
@@ -131,7 +132,7 @@ class LearnedIndex(Logger):
         """Pickle (save_as_pickle, utils.py:46-60) what the reference pickles:
         the model; the HBM index and its caches stay out of the file."""
         st = dict(self.__dict__)
-        for key in ("_index", "_cache_key", "_trusted", "_searcher", "_attached_labels"):
+        for key in ("_index", "_cache_key", "_trusted", "_searcher", "_attached_labels", "_cat_written"):
             st.pop(key, None)
         return st
 
@@ -148,6 +149,7 @@ class LearnedIndex(Logger):
         place afterwards (or must call attach again).  An addition; the
         reference has no such step (it re-gathers every bucket per call)."""
         self._trusted = None
+        self._cat_written = None
         self._device_index(data_navigation, data_search, pred_categories)
         self._trusted = (self._identity(data_navigation, data_search, pred_categories),
                          self._cache_key)
@@ -157,6 +159,7 @@ class LearnedIndex(Logger):
     def detach(self):
         """Stop trusting the attached objects (the next call hashes them)."""
         self._trusted = None
+        self._cat_written = None
 
     def _device_index(self, data_navigation, data_search, labels):
         """DeviceIndex of data_search rows in data_navigation order."""
@@ -214,7 +217,7 @@ class LearnedIndex(Logger):
         `semantics="exact"` (an addition; default off) returns the exact top-k of
         the union of the probed buckets instead of the reference's round merge."""
         assert self.model is not None, 'Model is not trained, call `build` first.'
-        data_navigation['category'] = pred_categories   # :67 (caller-visible side effect)
+        self._set_category(data_navigation, pred_categories)   # :67 (caller-visible side effect)
         index = self._device_index(data_navigation, data_search, pred_categories)
         q_nav = data_X_to_torch(queries_navigation).to(index.device)
         return self._get_searcher(index).search(q_nav, _upload_queries(queries_search, index.device),
@@ -252,6 +255,24 @@ class LearnedIndex(Logger):
         if int(rst.item()):
             raise RuntimeError(f"search_single: replay status {int(rst.item())}")
         return dd.cpu().numpy(), aa.cpu().numpy().view(np.uint32)
+
+    def _set_category(self, data_navigation, pred_categories):
+        """data_navigation['category'] = pred_categories (LearnedIndex.py:67),
+        except when this call would rewrite the very values the previous call
+        wrote: the frame and the labels are the attached objects (attach's
+        contract: not changed in place) and the column still holds the array
+        written then.  At 10M rows the assignment copies 80 MB inside pandas
+        (~10-30 ms), a third of the CLI's querytime."""
+        col = lambda: (id(data_navigation),
+                       np.asarray(data_navigation["category"]).__array_interface__["data"][0])
+        mark = (identity_key(pred_categories), identity_key(data_navigation.index))
+        if self._trusted is not None and self._cat_written is not None and \
+                pred_categories is self._attached_labels and \
+                "category" in getattr(data_navigation, "columns", ()) and \
+                self._cat_written == (mark, col()):
+            return
+        data_navigation['category'] = pred_categories
+        self._cat_written = (mark, col()) if self._trusted is not None else None
 
     def _labels_of(self, data_navigation):
         """data_navigation['category'] as search_single reads it (:143), but
