@@ -36,7 +36,7 @@ from ._lib import check, ptr
 DEFAULT_CHUNK_ROWS = 8192
 # LMI_Q_SEED_ROUND0 in the thresholded reference replay (LMI_NO_SEED=1: off,
 # for A/B measurements; results are the same either way)
-_SEED_ROUND0 = __import__("os").environ.get("LMI_NO_SEED") != "1"
+_SEED_ROUND0 = os.environ.get("LMI_NO_SEED") != "1"
 
 
 def _as_torch(x, device=None, dtype=None) -> torch.Tensor:
