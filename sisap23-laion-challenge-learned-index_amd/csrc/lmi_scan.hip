@@ -340,6 +340,76 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ til
     for (int i = tid; i < light_off; i += 1024) tiles[base + heavy_off + i] = tmp[i];
 }
 
+// Tail split (scan v3; LMI_SCAN_SPLIT): the last K tiles of every group queue
+// (K = the queue's share of the persistent grid) are replaced by their two
+// row halves, so the launch ends on half-size tiles (the idle tail of one
+// launch was 4.4% at G = 1 and 7.5% at G = 8 with whole tiles).  The scan
+// kernel is unchanged: a half is an ordinary tile whose bucket is a virtual
+// entry of an extended bucket table, chosen so that the scan's own
+//     row0 = off[c] + chunk * chunk_rows,  rows = min(chunk_rows, off[c + 1] - row0)
+// give the half's rows, and whose chunk is its partial-list slot: the first
+// half keeps the chunk's slot, the second writes the pair's extra slot X
+// (the stride's last); flag[pp] = 1 tells the chunk merge to read it.  One
+// split per (bucket, query block), so one extra slot per pair suffices.
+__global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict__ tin,
+                                                         Tile* __restrict__ tout,
+                                                         int32_t* __restrict__ meta,
+                                                         const int64_t* __restrict__ bucket_off,
+                                                         int64_t* __restrict__ ext_off, int32_t C,
+                                                         int32_t chunk_rows, int32_t X, int32_t K,
+                                                         int32_t* __restrict__ flag) {
+    __shared__ int wsp[4];
+    const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (x == 0)
+        for (int i = tid; i <= C; i += 256) ext_off[i] = bucket_off[i];
+    const int o = meta[x], n = meta[kGroups + x];
+    const int seeds = meta[2 * kGroups + 1 + x];
+    const int k2 = max(0, min(K, n - seeds));  // the candidates: the queue's last k2 tiles
+    const int no = o + x * K;                  // (every queue grows by at most K)
+    for (int i = tid; i < n - k2; i += 256) tout[no + i] = tin[o + i];
+    Tile t{};
+    int64_t rs = 0, re = 0;
+    bool sp = false;
+    if (tid < k2) {
+        t = tin[o + n - k2 + tid];
+        rs = bucket_off[t.c] + (int64_t)t.chunk * chunk_rows;
+        re = min(rs + (int64_t)chunk_rows, bucket_off[t.c + 1]);
+        if (re - rs >= 4 * 32 && atomicCAS(&flag[t.pp0], 0, 1) == 0) {
+            sp = true;
+            for (int i = 1; i < t.np; ++i) flag[t.pp0 + i] = 1;
+        }
+    }
+    const uint64_t m = __ballot(sp);
+    if (lane == 0) wsp[w] = __popcll(m);
+    __syncthreads();
+    int before = __popcll(m & ((1ull << lane) - 1ull)), total = 0;
+    for (int v = 0; v < 4; ++v) {
+        before += (v < w) ? wsp[v] : 0;
+        total += wsp[v];
+    }
+    if (tid < k2) {
+        const int at = no + (n - k2) + tid + before;
+        if (!sp) {
+            tout[at] = t;
+        } else {
+            const int hr = (int)((re - rs) / 64) * 32;
+            const int v = C + 1 + 4 * (x * K + tid);
+            ext_off[v] = rs - (int64_t)t.chunk * chunk_rows;
+            ext_off[v + 1] = rs + hr;
+            ext_off[v + 2] = rs + hr - (int64_t)X * chunk_rows;
+            ext_off[v + 3] = re;
+            tout[at] = Tile{v, t.pp0, t.np, t.chunk};
+            tout[at + 1] = Tile{v + 2, t.pp0, t.np, X};
+        }
+    }
+    __syncthreads();  // (every thread read meta[x] above)
+    if (tid == 0) {
+        meta[x] = no;
+        meta[kGroups + x] = n + total;
+        atomicAdd(&meta[2 * kGroups], total);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // nearest-chunk-first plan (scan v3, index with chunk centroids)
 //
@@ -1293,7 +1363,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, int64_t n_rows,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, const int32_t* __restrict__ split_flag) {
     // one thread per pair, 64-thread blocks (spread over every CU); each
     // chunk list is read with all its loads in flight, then its global
     // positions gathered the same way, then merged into a register list
@@ -1302,7 +1372,10 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     if (pp >= P) return;
     const int c = pair_bucket[pp];
     if (c < 0) return;
-    const int nch = chunk_first[c + 1] - chunk_first[c];
+    const int nch_c = chunk_first[c + 1] - chunk_first[c];
+    // (+1: a tail split's second half, in the pair's extra slot, the stride's last)
+    const int nch = nch_c + ((split_flag != nullptr && split_flag[pp] != 0) ? 1 : 0);
+    auto slot_of = [&](int j) { return j < nch_c ? j : max_chunks - 1; };
     uint64_t M[KL];
     int32_t W[KL];
     list_clear<KL>(M);
@@ -1325,7 +1398,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
 #pragma unroll
         for (int i = 0; i < KL; ++i) K[i] = Kn[i];
         if (j + 1 < nch) {
-            const uint64_t* src = partial + ((size_t)pp * max_chunks + j + 1) * KL;
+            const uint64_t* src = partial + ((size_t)pp * max_chunks + slot_of(j + 1)) * KL;
 #pragma unroll
             for (int i = 0; i < KL; ++i) Kn[i] = src[i];
         }
@@ -1403,6 +1476,7 @@ struct WsLayout {
     size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, tiles_tmp, ntiles, work, partial, thr_g, pref,
         pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
+    size_t tiles_split, ext_off, split_flag;  // tail split (scan v3)
     size_t pair_pos;  // LMI_Q_SEED_ROUND0: grouped position of every pair id
     size_t seed_pos;  //   and of every grouped pair's (q, 0)
     int32_t qb;      // queries per tile
@@ -1462,7 +1536,11 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     w.tiles_tmp = take((size_t)w.max_tiles * sizeof(Tile));
     w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));
-    w.partial = take(P * (size_t)std::max(idx->max_chunks, 1) * KL * sizeof(uint64_t));
+    // (+ 1 slot per pair: the second half of a tail-split tile)
+    w.partial = take(P * (size_t)(std::max(idx->max_chunks, 1) + 1) * KL * sizeof(uint64_t));
+    w.tiles_split = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK) * sizeof(Tile));
+    w.ext_off = take(((size_t)idx->n_buckets + 1 + 4 * (size_t)kGroups * kSplitMaxK) * 8);
+    w.split_flag = take(P * 4);
     w.thr_g = take(P * sizeof(uint64_t));
     w.pref = take(P * 4);
     w.pref_tmp = take(P * 4);
@@ -1761,13 +1839,30 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         ng = 1;  // one queue: seed tiles strictly first
     }
 
+    // tail split (scan v3): K = the queue's share of the grid
+    int32_t* split_flag = (int32_t*)(ws + w.split_flag);
+    LMI_HIP_TRY(hipMemsetAsync(split_flag, 0, (size_t)P * 4, s));
+    // (not after the nearest-chunk-first plan: its queue has no seed count)
+    const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
+                        : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
+                                                                            : (num_cus() + ng - 1) / ng);
+    const int64_t* scan_off = idx->bucket_off;
+    if (split_k > 0) {
+        hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, (Tile*)(ws + w.tiles_split),
+                           meta, idx->bucket_off, (int64_t*)(ws + w.ext_off), C, idx->chunk_rows,
+                           std::max(idx->max_chunks, 1), split_k, split_flag);
+        LMI_LAUNCH_CHECK("tail_split_kernel");
+        tiles = (Tile*)(ws + w.tiles_split);
+        scan_off = (const int64_t*)(ws + w.ext_off);
+    }
+
     ScanArgs a{};
     a.corpus = idx->corpus;
     a.d_pad = idx->d_pad;
     a.inv_norm = idx->inv_norm;
     a.bucket_off = idx->bucket_off;
     a.chunk_rows = idx->chunk_rows;
-    a.max_chunks = std::max(idx->max_chunks, 1);
+    a.max_chunks = std::max(idx->max_chunks, 1) + 1;  // the partial-list stride (+ the split slot)
     a.qbuf = ws + w.qbuf;
     a.invq = (const float*)(ws + w.invq);
     a.pair_q = pair_q;
@@ -1784,7 +1879,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         Scan2Args b{};
         b.corpus = reinterpret_cast<const _Float16*>(idx->corpus);
         b.inv_norm = idx->inv_norm;
-        b.bucket_off = idx->bucket_off;
+        b.bucket_off = scan_off;
         b.chunk_rows = idx->chunk_rows;
         b.max_chunks = a.max_chunks;
         b.qbuf = reinterpret_cast<const _Float16*>(ws + w.qbuf);
@@ -1845,7 +1940,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
 #define LMI_CM(KLV, ROWSV)                                                                         \
     hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
                        a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo,  \
-                       out_d, out_pos, out_row, idx->n_rows, status)
+                       out_d, out_pos, out_row, idx->n_rows, status, split_flag)
     if (KL == 10) {
         if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
     } else if (KL == 15) {

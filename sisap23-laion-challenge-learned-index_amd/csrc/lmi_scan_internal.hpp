@@ -47,6 +47,8 @@ struct ScanArgs {
 };
 
 
+// tail split: at most this many tiles per queue are halved (tail_split_kernel)
+constexpr int kSplitMaxK = 256;
 // tile groups of the persistent scans' dequeue (XCD round-robin, see
 // plan_fill_kernel in lmi_scan.hip)
 constexpr int kGroups = 8;
