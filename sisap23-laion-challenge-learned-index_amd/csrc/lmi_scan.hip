@@ -341,23 +341,21 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ til
 }
 
 // Tail split (scan v3; LMI_SCAN_SPLIT): the last K tiles of every group queue
-// (K = the queue's share of the persistent grid) are replaced by their two
-// row halves, so the launch ends on half-size tiles (the idle tail of one
-// launch was 4.4% at G = 1 and 7.5% at G = 8 with whole tiles).  The scan
-// kernel is unchanged: a half is an ordinary tile whose bucket is a virtual
-// entry of an extended bucket table, chosen so that the scan's own
+// are replaced by their two row halves, so the launch ends on half-size tiles.
+// The scan kernel is unchanged: a half is an ordinary tile whose bucket is a
+// virtual entry of an extended bucket table, chosen so that the scan's own
 //     row0 = off[c] + chunk * chunk_rows,  rows = min(chunk_rows, off[c + 1] - row0)
 // give the half's rows, and whose chunk is its partial-list slot: the first
-// half keeps the chunk's slot, the second writes the pair's extra slot X
-// (the stride's last); flag[pp] = 1 tells the chunk merge to read it.  One
-// split per (bucket, query block), so one extra slot per pair suffices.
+// half keeps chunk j's slot, the second writes slot X + j (X = max_chunks, the
+// stride is 2X); bit j of mask[pp] tells the chunk merge to read it (chunks
+// j < 32 only).
 __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict__ tin,
                                                          Tile* __restrict__ tout,
                                                          int32_t* __restrict__ meta,
                                                          const int64_t* __restrict__ bucket_off,
                                                          int64_t* __restrict__ ext_off, int32_t C,
                                                          int32_t chunk_rows, int32_t X, int32_t K,
-                                                         int32_t* __restrict__ flag) {
+                                                         uint32_t* __restrict__ mask) {
     __shared__ int wsp[4];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (x == 0)
@@ -374,10 +372,9 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
         t = tin[o + n - k2 + tid];
         rs = bucket_off[t.c] + (int64_t)t.chunk * chunk_rows;
         re = min(rs + (int64_t)chunk_rows, bucket_off[t.c + 1]);
-        if (re - rs >= 4 * 32 && atomicCAS(&flag[t.pp0], 0, 1) == 0) {
-            sp = true;
-            for (int i = 1; i < t.np; ++i) flag[t.pp0 + i] = 1;
-        }
+        sp = re - rs >= 4 * 32 && t.chunk < 32;
+        if (sp)
+            for (int i = 0; i < t.np; ++i) atomicOr(&mask[t.pp0 + i], 1u << t.chunk);
     }
     const uint64_t m = __ballot(sp);
     if (lane == 0) wsp[w] = __popcll(m);
@@ -396,10 +393,10 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
             const int v = C + 1 + 4 * (x * K + tid);
             ext_off[v] = rs - (int64_t)t.chunk * chunk_rows;
             ext_off[v + 1] = rs + hr;
-            ext_off[v + 2] = rs + hr - (int64_t)X * chunk_rows;
+            ext_off[v + 2] = rs + hr - (int64_t)(X + t.chunk) * chunk_rows;
             ext_off[v + 3] = re;
             tout[at] = Tile{v, t.pp0, t.np, t.chunk};
-            tout[at + 1] = Tile{v + 2, t.pp0, t.np, X};
+            tout[at + 1] = Tile{v + 2, t.pp0, t.np, X + t.chunk};
         }
     }
     __syncthreads();  // (every thread read meta[x] above)
@@ -1363,7 +1360,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, int64_t n_rows,
-    int32_t* __restrict__ status, const int32_t* __restrict__ split_flag) {
+    int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask) {
     // one thread per pair, 64-thread blocks (spread over every CU); each
     // chunk list is read with all its loads in flight, then its global
     // positions gathered the same way, then merged into a register list
@@ -1373,9 +1370,16 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const int c = pair_bucket[pp];
     if (c < 0) return;
     const int nch_c = chunk_first[c + 1] - chunk_first[c];
-    // (+1: a tail split's second half, in the pair's extra slot, the stride's last)
-    const int nch = nch_c + ((split_flag != nullptr && split_flag[pp] != 0) ? 1 : 0);
-    auto slot_of = [&](int j) { return j < nch_c ? j : max_chunks - 1; };
+    // (+ the second halves of tail-split chunks: slot X + j for bit j of the
+    // pair's mask, X = max_chunks / 2, the stride being 2X)
+    uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
+    const int nch = nch_c + __popc(sm);
+    auto slot_of = [&](int j) {
+        if (j < nch_c) return j;
+        const int b = __builtin_ctz(sm);  // the halves in ascending chunk order
+        sm &= sm - 1u;
+        return max_chunks / 2 + b;
+    };
     uint64_t M[KL];
     int32_t W[KL];
     list_clear<KL>(M);
@@ -1476,7 +1480,7 @@ struct WsLayout {
     size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, tiles_tmp, ntiles, work, partial, thr_g, pref,
         pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
-    size_t tiles_split, ext_off, split_flag;  // tail split (scan v3)
+    size_t tiles_split, ext_off, split_mask;  // tail split (scan v3)
     size_t pair_pos;  // LMI_Q_SEED_ROUND0: grouped position of every pair id
     size_t seed_pos;  //   and of every grouped pair's (q, 0)
     int32_t qb;      // queries per tile
@@ -1536,11 +1540,11 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     w.tiles_tmp = take((size_t)w.max_tiles * sizeof(Tile));
     w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));
-    // (+ 1 slot per pair: the second half of a tail-split tile)
-    w.partial = take(P * (size_t)(std::max(idx->max_chunks, 1) + 1) * KL * sizeof(uint64_t));
+    // (x 2: the second halves of tail-split chunks, slot max_chunks + j)
+    w.partial = take(P * (size_t)(2 * std::max(idx->max_chunks, 1)) * KL * sizeof(uint64_t));
     w.tiles_split = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK) * sizeof(Tile));
     w.ext_off = take(((size_t)idx->n_buckets + 1 + 4 * (size_t)kGroups * kSplitMaxK) * 8);
-    w.split_flag = take(P * 4);
+    w.split_mask = take(P * 4);
     w.thr_g = take(P * sizeof(uint64_t));
     w.pref = take(P * 4);
     w.pref_tmp = take(P * 4);
@@ -1840,8 +1844,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     }
 
     // tail split (scan v3): K = the queue's share of the grid
-    int32_t* split_flag = (int32_t*)(ws + w.split_flag);
-    LMI_HIP_TRY(hipMemsetAsync(split_flag, 0, (size_t)P * 4, s));
+    uint32_t* split_mask = (uint32_t*)(ws + w.split_mask);
+    LMI_HIP_TRY(hipMemsetAsync(split_mask, 0, (size_t)P * 4, s));
     // (not after the nearest-chunk-first plan: its queue has no seed count)
     const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
                         : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
@@ -1850,7 +1854,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     if (split_k > 0) {
         hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, (Tile*)(ws + w.tiles_split),
                            meta, idx->bucket_off, (int64_t*)(ws + w.ext_off), C, idx->chunk_rows,
-                           std::max(idx->max_chunks, 1), split_k, split_flag);
+                           std::max(idx->max_chunks, 1), split_k, split_mask);
         LMI_LAUNCH_CHECK("tail_split_kernel");
         tiles = (Tile*)(ws + w.tiles_split);
         scan_off = (const int64_t*)(ws + w.ext_off);
@@ -1862,7 +1866,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     a.inv_norm = idx->inv_norm;
     a.bucket_off = idx->bucket_off;
     a.chunk_rows = idx->chunk_rows;
-    a.max_chunks = std::max(idx->max_chunks, 1) + 1;  // the partial-list stride (+ the split slot)
+    a.max_chunks = 2 * std::max(idx->max_chunks, 1);  // the partial-list stride (+ split halves)
     a.qbuf = ws + w.qbuf;
     a.invq = (const float*)(ws + w.invq);
     a.pair_q = pair_q;
@@ -1940,7 +1944,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
 #define LMI_CM(KLV, ROWSV)                                                                         \
     hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
                        a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo,  \
-                       out_d, out_pos, out_row, idx->n_rows, status, split_flag)
+                       out_d, out_pos, out_row, idx->n_rows, status, split_mask)
     if (KL == 10) {
         if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
     } else if (KL == 15) {
