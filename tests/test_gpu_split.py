@@ -15,12 +15,13 @@ from li import index as I
 pytestmark = pytest.mark.gpu
 
 
-def _lists(ix, q, classes, k, dist, split):
+def _lists(ix, q, classes, k, dist, split, groups=None):
     import os
-    if split is None:
-        os.environ.pop("LMI_SCAN_SPLIT", None)
-    else:
-        os.environ["LMI_SCAN_SPLIT"] = str(split)
+    for var, val in (("LMI_SCAN_SPLIT", split), ("LMI_SCAN_GROUPS", groups)):
+        if val is None:
+            os.environ.pop(var, None)
+        else:
+            os.environ[var] = str(val)
     _lib.load().lmi_config_reload()
     try:
         r = (I.bucket_topk_f64 if dist == "f64" else I.bucket_topk)(ix, q, classes, k)
@@ -29,6 +30,7 @@ def _lists(ix, q, classes, k, dist, split):
         return d.cpu().numpy(), p.cpu().numpy()
     finally:
         os.environ.pop("LMI_SCAN_SPLIT", None)
+        os.environ.pop("LMI_SCAN_GROUPS", None)
         _lib.load().lmi_config_reload()
 
 
@@ -41,8 +43,11 @@ def test_split_lists_equal_unsplit(k, dist, chunk_rows):
         O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :3], dtype=np.int32)).cuda()
     q = torch.from_numpy(w["q"]).cuda()
     d0, p0 = _lists(ix, q, classes, k, dist, -1)       # off
-    for split in (None, 1, 3, 256):                   # default K, and a few others
-        d1, p1 = _lists(ix, q, classes, k, dist, split)
+    # default K (the queue's share of the grid), a few others, and one queue
+    # (K = 256: nearly every tile of these small workloads is halved, many
+    # chunks of one pair block)
+    for split, groups in ((None, None), (1, None), (3, None), (256, None), (None, 1), (7, 2)):
+        d1, p1 = _lists(ix, q, classes, k, dist, split, groups)
         np.testing.assert_array_equal(p1, p0)
         np.testing.assert_array_equal(d1, d0)
 
