@@ -380,6 +380,9 @@ def main():
     ap.add_argument("--parity-sample", type=int, default=64,
                     help="queries whose lists are checked against a float64 brute force")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="upload each batch inside its own step instead of during the previous "
+                         "step's search (GraphedSearch(pipeline=True), the default)")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager step (every launch from the host) instead of the "
                          "HIP-graph replay of the captured step")
@@ -449,7 +452,7 @@ def main():
         Before timing, the first replay's answer must equal an eager step's bit
         for bit on every rank, else the eager step is timed instead."""
         try:
-            gs = searcher.graph(qn_h, q_h, args.R, k=args.k, dist=dist)
+            gs = searcher.graph(qn_h, q_h, args.R, k=args.k, dist=dist, pipeline=not args.no_pipeline)
             ok = 1
         except Exception as e:  # noqa: BLE001 (reported in the JSON line)
             log(f"[bench] graph capture failed ({e!r}); timing eager launches")
@@ -611,9 +614,13 @@ def main():
         "h2d": None if h2d is None else {"ms": round(h2d[0], 4), "gb_s": round(h2d[1], 1),
                                          "bytes_per_rank": int(4 * (-(-args.nq // world)) * (96 + (384 if q16_exact else 768))),
                                          "queries_staged_as": "f16" if q16_exact else "f32",
-                                         "in_step": True},
+                                         "in_step": True,
+                                         "overlapped_with_previous_step": use_graph and not graph_failed and not args.no_pipeline},
         "dist": args.dist,
-        "step": ("hip-graph replay (H2D of the host batch + search + D2H of the answer)"
+        "step": (("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
+                  "copy stream during the previous step's search (double-buffered), + search + D2H "
+                  "of the answer" if not args.no_pipeline else
+                  "hip-graph replay (H2D of the host batch + search + D2H of the answer)")
                  if use_graph and not graph_failed else
                  "eager launches (H2D of the host batch + search + D2H)" +
                  (f" (graph not used: {graph_failed[0]})" if graph_failed else "")),

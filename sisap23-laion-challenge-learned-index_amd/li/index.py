@@ -1001,7 +1001,7 @@ class GraphedSearch:
 
     def __init__(self, searcher: "Searcher", q_nav, q_search, R: int,
                  k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True):
+                 capture: bool = True, pipeline: bool = False):
         s = searcher
         ix = s.index
         dev = ix.device
@@ -1041,7 +1041,13 @@ class GraphedSearch:
         need = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
             C.byref(ix.desc), nq, R, k_round, self.qmode)
         self.ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
-        self.d_blk = torch.empty((bw,), dtype=torch.int32, device=dev)
+        # pipeline: two device copies of the staged block, each with its own
+        # captured graph; run() uploads the next one on a copy stream while
+        # the current graph runs (the upload leaves the graph)
+        self.pipeline = bool(pipeline) and capture
+        self.d_blks = [torch.empty((bw,), dtype=torch.int32, device=dev)
+                       for _ in range(2 if self.pipeline else 1)]
+        self.d_blk = self.d_blks[0]
         self.d_all = torch.empty((G, bw), dtype=torch.int32, device=dev) if G > 1 else None
         self.q32 = torch.empty((G * per, d), dtype=torch.float32, device=dev) \
             if (self.f16_up or G > 1) else None
@@ -1055,19 +1061,22 @@ class GraphedSearch:
         self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
         copy_stream = torch.cuda.Stream(dev)
 
-        def step():
+        def step(slot=0):
             ans = answer_buffer(nq, self.w, dev)
             main = torch.cuda.current_stream(dev)
+            d_blk = self.d_blks[slot]
             if G == 1:
-                # pca96 rows first; the clip768 rows come in on a second stream
-                # while the router runs
-                self.d_blk[:per * dn].copy_(self.h_blk[0, :per * dn], non_blocking=True)
-                copy_stream.wait_stream(main)
-                with torch.cuda.stream(copy_stream):
-                    self.d_blk[per * dn:].copy_(self.h_blk[0, per * dn:], non_blocking=True)
-                classes = s.router.topr(self.d_blk[:per * dn].view(torch.float32).view(per, dn), R)[0]
-                main.wait_stream(copy_stream)
-                sv = self.d_blk[per * dn:per * dn + per * wq]
+                if not self.pipeline:
+                    # pca96 rows first; the clip768 rows come in on a second
+                    # stream while the router runs
+                    d_blk[:per * dn].copy_(self.h_blk[0, :per * dn], non_blocking=True)
+                    copy_stream.wait_stream(main)
+                    with torch.cuda.stream(copy_stream):
+                        d_blk[per * dn:].copy_(self.h_blk[0, per * dn:], non_blocking=True)
+                classes = s.router.topr(d_blk[:per * dn].view(torch.float32).view(per, dn), R)[0]
+                if not self.pipeline:
+                    main.wait_stream(copy_stream)
+                sv = d_blk[per * dn:per * dn + per * wq]
                 if self.f16_up:
                     q = self.q32
                     q.copy_(sv.view(torch.float16).view(per, d))
@@ -1077,10 +1086,11 @@ class GraphedSearch:
                 # this rank's block: upload, route its queries into the block,
                 # one all-gather of every block (queries + classes)
                 from .dist import _all_gather
-                self.d_blk.copy_(self.h_blk[g], non_blocking=True)
-                s.router.topr(self.d_blk[:per * dn].view(torch.float32).view(per, dn), R,
-                              out=self.d_blk[per * (dn + wq):])
-                _all_gather(self.d_all.view(-1), self.d_blk, s.group)
+                if not self.pipeline:
+                    d_blk.copy_(self.h_blk[g], non_blocking=True)
+                s.router.topr(d_blk[:per * dn].view(torch.float32).view(per, dn), R,
+                              out=d_blk[per * (dn + wq):])
+                _all_gather(self.d_all.view(-1), d_blk, s.group)
                 sv = self.d_all[:, per * dn:per * (dn + wq)]
                 if self.f16_up:
                     self.q32.view(G, per, d).copy_(sv.view(torch.float16).view(G, per, d))
@@ -1112,13 +1122,21 @@ class GraphedSearch:
             self.graph = None
             self._step = step
             return
+        self._cs = copy_stream
+        if self.pipeline:
+            self._up_ev = [torch.cuda.Event() for _ in range(2)]
+            self._done_ev = [torch.cuda.Event() for _ in range(2)]
+            for slot in range(2):
+                self.d_blks[slot].copy_(self.h_blk[g], non_blocking=True)
+            torch.cuda.synchronize(dev)
+        slots = (0, 1) if self.pipeline else (0, 0)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         err = None
         try:
             with torch.cuda.stream(side):
-                for _ in range(2):
-                    buf = step()
+                for slot in slots:
+                    buf = step(slot)
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)
         except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
@@ -1131,11 +1149,17 @@ class GraphedSearch:
         elif err is not None:
             raise err
         self.h = torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            buf = step()
-            self.h.copy_(buf, non_blocking=True)
-        self._keep = buf
+        self.graphs, self._keep = [], []
+        for slot in range(2 if self.pipeline else 1):
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                buf = step(slot)
+                self.h.copy_(buf, non_blocking=True)
+            self.graphs.append(gr)
+            self._keep.append(buf)
+        self.graph = self.graphs[0]
+        self._slot = 0
+        self._fresh = [True, True]   # d_blks[slot] holds the staged batch
         torch.cuda.synchronize(dev)
 
     def stage(self, q_nav, q_search) -> bool:
@@ -1159,6 +1183,11 @@ class GraphedSearch:
             src, sdt = q16, np.float16
         else:
             src, sdt = qs.astype(np.float32, copy=False), np.float32
+        if getattr(self, "pipeline", False):
+            # an upload from the pinned buffer may be in flight (run());
+            # both device copies are stale from now on
+            self._cs.synchronize()
+            self._fresh = [False, False]
         blk = self.h_blk.numpy()
         for g in range(blk.shape[0]):
             lo, hi = min(nq, g * per), min(nq, (g + 1) * per)
@@ -1186,7 +1215,9 @@ class GraphedSearch:
                 raise ValueError("stage both q_nav and q_search")
             if not self.stage(q_nav, q_search):
                 return self._eager(q_nav, q_search)
-        if self.graph is not None:
+        if self.pipeline:
+            self._run_pipelined(dev)
+        elif self.graph is not None:
             self.graph.replay()
         else:
             self.h.copy_(self._step(), non_blocking=True)
@@ -1198,6 +1229,33 @@ class GraphedSearch:
         if st & _lib.LMI_STATUS_INTERNAL or rst:
             raise RuntimeError(f"search: internal status {st}/{rst}")
         return hd, ha
+
+    def _upload(self, slot):
+        """The staged block into d_blks[slot] on the copy stream, once the
+        graph that last read that copy has finished."""
+        cs = self._cs
+        cs.wait_event(self._done_ev[slot])
+        with torch.cuda.stream(cs):
+            self.d_blks[slot].copy_(self.h_blk[self.rank_in_group], non_blocking=True)
+        self._up_ev[slot].record(cs)
+        self._fresh[slot] = True
+
+    def _run_pipelined(self, dev):
+        """Replay the current slot's graph; meanwhile upload the staged batch
+        into the other slot for the next run (a stream of batches: the copy
+        engine moves batch i + 1 while batch i is searched)."""
+        main = torch.cuda.current_stream(dev)
+        slot = self._slot
+        if not self._fresh[slot]:
+            self._upload(slot)
+        main.wait_event(self._up_ev[slot])
+        self.graphs[slot].replay()
+        self._done_ev[slot].record(main)
+        self._fresh[slot] = False
+        nxt = 1 - slot
+        if not self._fresh[nxt]:
+            self._upload(nxt)
+        self._slot = nxt
 
     def _eager(self, q_nav, q_search):
         dev = self.searcher.index.device

@@ -92,3 +92,33 @@ def test_graph_survives_workspace_growth(setup, dist):
     del junk
     np.testing.assert_array_equal(d1, d0)
     np.testing.assert_array_equal(a1, a0)
+
+
+@pytest.mark.parametrize("dist", ["f32", "f64"])
+def test_pipelined_graph_stream_of_batches(setup, dist):
+    """pipeline=True: two device copies of the staged batch, each with its own
+    graph; every run uploads the staged batch into the other copy while its
+    graph runs.  Any sequence of runs and newly staged batches answers like
+    the eager search of that batch."""
+    w, s = setup
+    g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist, pipeline=True)
+    assert g.pipeline and len(g.graphs) == 2
+    d0, a0 = s.search(torch.from_numpy(w["qn"]).cuda(), torch.from_numpy(w["q"]).cuda(), 4, k=10,
+                      dist=dist)
+    for _ in range(5):                         # both slots, several times each
+        d1, a1 = g.run()
+        np.testing.assert_array_equal(d1, d0)
+        np.testing.assert_array_equal(a1, a0)
+    perm = np.random.default_rng(1).permutation(w["q"].shape[0])
+    qn2, q2 = w["qn"][perm], w["q"][perm]
+    e0, b0 = s.search(torch.from_numpy(qn2).cuda(), torch.from_numpy(q2).cuda(), 4, k=10, dist=dist)
+    d2, a2 = g.run(qn2, q2)                    # a new batch: staged, then answered
+    np.testing.assert_array_equal(d2, e0)
+    np.testing.assert_array_equal(a2, b0)
+    for _ in range(3):                         # and streamed again from then on
+        d3, a3 = g.run()
+        np.testing.assert_array_equal(d3, e0)
+        np.testing.assert_array_equal(a3, b0)
+    d4, a4 = g.run(w["qn"], w["q"])            # back to the first batch
+    np.testing.assert_array_equal(d4, d0)
+    np.testing.assert_array_equal(a4, a0)
