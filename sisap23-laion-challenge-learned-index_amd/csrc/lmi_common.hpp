@@ -33,6 +33,12 @@ void set_error(const char* fmt, ...);
         }                                                                        \
     } while (0)
 
+#define LMI_TRY(expr)                                                            \
+    do {                                                                         \
+        const int rc_ = (expr);                                                  \
+        if (rc_ != LMI_OK) return rc_;                                           \
+    } while (0)
+
 #define LMI_LAUNCH_CHECK(name)                                                   \
     do {                                                                         \
         hipError_t e_ = hipGetLastError();                                       \
@@ -141,5 +147,9 @@ int bucket_topk_passes(const lmi_index_desc* idx, const float* q, int32_t nq, in
                        const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                        int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
                        void* workspace, size_t ws_bytes, hipStream_t s);
+// n_words 32-bit words of `value` from p (4-byte aligned) on stream s, by a
+// kernel (lmi_merge.hip): workspace initialisation stays a kernel node when a
+// caller captures the launch sequence in a HIP graph (no memset nodes).
+int fill_u32(void* p, uint32_t value, size_t n_words, hipStream_t s);
 
 }  // namespace lmi

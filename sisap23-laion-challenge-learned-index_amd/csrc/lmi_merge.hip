@@ -257,3 +257,21 @@ extern "C" int lmi_merge_topk_packed(const int32_t* gathered, int32_t G, int64_t
                         gathered + nd + rows * k, rank_words, out_status, out_d, out_pos,
                         reinterpret_cast<hipStream_t>(stream));
 }
+
+namespace lmi {
+namespace {
+__global__ void fill_u32_kernel(uint32_t* __restrict__ p, uint32_t value, size_t n) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = value;
+}
+}  // namespace
+
+int fill_u32(void* p, uint32_t value, size_t n_words, hipStream_t s) {
+    if (n_words == 0) return LMI_OK;
+    const size_t blocks = std::min<size_t>((n_words + 255) / 256, 4096);
+    hipLaunchKernelGGL(fill_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<uint32_t*>(p), value, n_words);
+    LMI_LAUNCH_CHECK("fill_u32_kernel");
+    return LMI_OK;
+}
+}  // namespace lmi

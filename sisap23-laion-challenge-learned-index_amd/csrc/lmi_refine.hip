@@ -465,7 +465,7 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     a.failed = (int32_t*)(ws + w.failed);
     a.n_failed = (int32_t*)(ws + w.nfailed);
     a.status = status;
-    LMI_HIP_TRY(hipMemsetAsync(ws + w.nfailed, 0, 4, s));
+    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
     int rc = w.passes
         ? bucket_topk_passes(idx, q, nq, ldq, classes, R, k + 5, qmode, (float*)(ws + w.ld),
                              (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), kl, status,

@@ -1010,7 +1010,7 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         // writes back / invalidates the XCD's L2 on gfx950, and a group's
         // merges run one wave per query instead of one thread per element.
         int32_t* done = (int32_t*)(ws + s.done);
-        LMI_HIP_TRY(hipMemsetAsync(done, 0, (size_t)R * (C + 1) * 4 + 4, st));
+        LMI_TRY(fill_u32(done, 0u, (size_t)R * (C + 1) + 1, st));
         FlowArgs f{};
         f.base.classes = classes;
         f.base.nq = nq;

@@ -1802,14 +1802,14 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     while (ng & (ng - 1)) ng &= ng - 1;
 
     // pair_bucket = -1 marks pairs whose class is out of range (never filled)
-    LMI_HIP_TRY(hipMemsetAsync(pair_bucket, 0xff, (size_t)P * 4, s));
+    LMI_TRY(fill_u32(pair_bucket, 0xffffffffu, (size_t)P, s));
     hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, counts);
     LMI_LAUNCH_CHECK("plan_count_kernel");
     // (the seed reads the pair position of every (q, 0); pairs whose class is
     // out of range keep -1)
     const bool seed = seed_r0 && w.use_v3 && !LOP && R > 1;
     int32_t* pair_pos = seed ? (int32_t*)(ws + w.pair_pos) : nullptr;
-    if (seed) LMI_HIP_TRY(hipMemsetAsync(pair_pos, 0xff, (size_t)P * 4, s));
+    if (seed) LMI_TRY(fill_u32(pair_pos, 0xffffffffu, (size_t)P, s));
     hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
                        idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
     LMI_LAUNCH_CHECK("plan_fill_kernel");
@@ -1845,7 +1845,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
 
     // tail split (scan v3): K = the queue's share of the grid
     uint32_t* split_mask = (uint32_t*)(ws + w.split_mask);
-    LMI_HIP_TRY(hipMemsetAsync(split_mask, 0, (size_t)P * 4, s));
+    LMI_TRY(fill_u32(split_mask, 0u, (size_t)P, s));
     // (not after the nearest-chunk-first plan: its queue has no seed count)
     const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
                         : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
@@ -1906,7 +1906,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         // seeds when the same batch is repeated) to measure seeding quality
         if (!env_config().scan_keep_thr)
 #endif
-        LMI_HIP_TRY(hipMemsetAsync(ws + w.thr_g, 0xff, (size_t)P * 8, s));
+        LMI_TRY(fill_u32(ws + w.thr_g, 0xffffffffu, (size_t)P * 2, s));
         if (w.use_v3 && LOP) {
             // the passes' lists are 15 entries on v3 (passes_of)
             if (KL != 15) {
@@ -1992,7 +1992,7 @@ int bucket_topk_passes(const lmi_index_desc* idx, const float* q, int32_t nq, in
         set_error("workspace %zu B too small", ws_bytes);
         return LMI_E_WORKSPACE;
     }
-    LMI_HIP_TRY(hipMemsetAsync(lo, 0, P * 8, s));
+    LMI_TRY(fill_u32(lo, 0u, P * 2, s));
     for (int j = 0; j < np; ++j) {
         const int rc = bucket_topk_impl(idx, q, nq, ldq, classes, R, kp, qmode, out_d + (size_t)j * kp,
                                         out_pos + (size_t)j * kp, out_row ? out_row + (size_t)j * kp : nullptr,

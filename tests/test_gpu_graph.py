@@ -122,3 +122,30 @@ def test_pipelined_graph_stream_of_batches(setup, dist):
     d4, a4 = g.run(w["qn"], w["q"])            # back to the first batch
     np.testing.assert_array_equal(d4, d0)
     np.testing.assert_array_equal(a4, a0)
+
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_graph_replays_survive_eager_work_between(setup, pipeline):
+    """Eager work between replays (a search of another batch, clones of the index's
+    tables) leaves the captured graphs' answers unchanged.  Round 3: with the
+    workspace initialised by hipMemsetAsync (memset nodes in the captured
+    graphs), the pipelined pair of graphs answered wrong lists after exactly
+    this sequence; the library initialises its workspace with kernels now."""
+    w, s = setup
+    T = lambda a: torch.from_numpy(a).cuda()
+    perm = np.random.default_rng(3).permutation(w["q"].shape[0])
+    qn2, q2 = w["qn"][perm], w["q"][perm]
+    d0, a0 = s.search(T(w["qn"]), T(w["q"]), 4, k=10)
+    e0, b0 = s.search(T(qn2), T(q2), 4, k=10)
+    g = s.graph(w["qn"], w["q"], 4, k=10, pipeline=pipeline)
+    g.run()
+    junk = [t.clone() for t in vars(s.index).values() if isinstance(t, torch.Tensor) and t.is_cuda]
+    s.search(T(qn2), T(q2), 4, k=10)
+    for _ in range(3):
+        d1, a1 = g.run()
+        np.testing.assert_array_equal(d1, d0)
+        np.testing.assert_array_equal(a1, a0)
+    del junk
+    d2, a2 = g.run(qn2, q2)
+    np.testing.assert_array_equal(d2, e0)
+    np.testing.assert_array_equal(a2, b0)

@@ -186,3 +186,15 @@ def test_host_hash64_threads_and_sensitivity():
         b[pos] ^= 1
     assert lib.lmi_host_hash64(a.ctypes.data, a.nbytes - 1, 4) != h[0]
     assert lib.lmi_host_hash64(None, 0, 1) == lib.lmi_host_hash64(None, 0, 4)
+
+
+def test_search_path_initialises_workspace_with_kernels():
+    """The search step is captured as HIP graphs (li.index.GraphedSearch); round 3
+    measured captured hipMemsetAsync nodes answering wrong lists once eager copies
+    ran between replays of two graphs, so the search path's sources initialise
+    device memory with fill kernels (lmi::fill_u32), never hipMemsetAsync/hipMemset."""
+    csrc = os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd", "csrc")
+    for name in ("lmi_scan.hip", "lmi_scan_v12.hip", "lmi_refine.hip", "lmi_merge.hip",
+                 "lmi_replay_gpu.hip", "lmi_router.hip", "lmi_abi.cpp"):
+        src = open(os.path.join(csrc, name)).read()
+        assert not re.search(r"\bhipMemset\w*\s*\(", src), name
