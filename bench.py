@@ -268,21 +268,32 @@ def list_parity(index, x, q, classes, lists_d, lists_pos, n_sample, f64, seed=5)
 
 
 @torch.no_grad()
-def h2d_ms(gs, reps=10):
-    """The step's host -> device upload alone (this rank's staged block), HIP
-    events on the current stream: ms per copy and GB/s."""
-    dev = gs.searcher.index.device
-    g = gs.rank_in_group
-    dst = torch.empty_like(gs.d_blk)
+def h2d_ms(src, dst, reps=10):
+    """The step's host -> device upload alone (a pinned staged block into its
+    device copy), HIP events on the current stream: ms per copy and GB/s."""
+    dst = torch.empty_like(dst)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    dst.copy_(gs.h_blk[g], non_blocking=True)
+    dst.copy_(src, non_blocking=True)
     e0.record()
     for _ in range(reps):
-        dst.copy_(gs.h_blk[g], non_blocking=True)
+        dst.copy_(src, non_blocking=True)
     e1.record()
-    torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dst.device)
     ms = e0.elapsed_time(e1) / reps
-    return ms, gs.upload_bytes() / (ms * 1e-3) / 1e9
+    return ms, src.numel() * src.element_size() / (ms * 1e-3) / 1e9
+
+
+STEP_TEXT = {
+    "stream": lambda a: ("batch stream (StreamedSearch): one launch of three captured branches per "
+                         "batch -- H2D + router + plan of batch b+2, the scan of b+1, chunk merge + "
+                         "replay + D2H of the answer of b" + (" (+ all-gather + K3)" if a.gpus > 1 else "") +
+                         "; each batch passes every stage, the timed launches answer one batch each"),
+    "graph": lambda a: ("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
+                        "copy stream during the previous step's search (double-buffered), + search + D2H "
+                        "of the answer" if not a.no_pipeline else
+                        "hip-graph replay (H2D of the host batch + search + D2H of the answer)"),
+    "eager": lambda a: "eager launches (H2D of the host batch + search + D2H)",
+}
 
 
 def pmc_traffic(kernel_ms):
@@ -380,6 +391,10 @@ def main():
     ap.add_argument("--parity-sample", type=int, default=64,
                     help="queries whose lists are checked against a float64 brute force")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="time the per-batch step graph (GraphedSearch) instead of the batch stream "
+                         "(StreamedSearch, the default: plan of batch b+2, scan of b+1 and "
+                         "merge/replay/D2H of b in one launch of three captured branches)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="upload each batch inside its own step instead of during the previous "
                          "step's search (GraphedSearch(pipeline=True), the default)")
@@ -409,12 +424,16 @@ def main():
 
     use_graph = not args.no_graph and (world == 1 or torch.distributed.get_backend() == "nccl")
     graph_failed = []
+    stream_failed = []
+    step_mode = {}
     # the batch starts in HOST memory, as the reference's (search.py:49,
     # :85-87): pinned buffers filled once before the timer (like its h5 loads);
     # every timed step uploads it (H2D), searches and copies the answer back
     qn_h = qn.cpu().numpy()
     q_h = q.cpu().numpy()
     q16_exact = index.storage == "f16" and bool(np.array_equal(q_h.astype(np.float16).astype(np.float32), q_h))
+    # the batch stream takes fp16-exact batches on an fp16 index (the phased scan)
+    use_stream = use_graph and not args.no_stream and q16_exact
     qn_pin = torch.from_numpy(qn_h).pin_memory()
     q_pin = torch.from_numpy(q_h.astype(np.float16) if q16_exact else q_h).pin_memory()
     checks = {}
@@ -472,7 +491,7 @@ def main():
             graph_failed.append("first replay differs from the eager step")
             del gs
             return timed_eager(dist)
-        h2d = h2d_ms(gs)
+        h2d = h2d_ms(gs.h_blk[gs.rank_in_group], gs.d_blk) + (gs.upload_bytes(),)
         out = None
         for _ in range(args.warmup):
             out = gs.run()
@@ -488,16 +507,70 @@ def main():
         el = time.perf_counter() - t0
         out = (out[0].copy(), out[1].copy())
         del gs
+        step_mode[dist] = "graph"
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=device)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
         return el, kernel_ms(dist), out, h2d
 
+    def timed_stream(dist):
+        """The step as a stream of batches (Searcher.streamed -> StreamedSearch):
+        every launch plans batch b+2 (H2D, router, plan), scans b+1 and merges,
+        replays and copies out b, on three captured branches; the same batch is
+        staged in every slot, so each launch answers one full batch.  Before
+        timing, a launch's answer must equal an eager step's bit for bit on every
+        rank, else the per-batch step graph is timed instead."""
+        try:
+            ss = searcher.streamed(qn_h, q_h, args.R, k=args.k, dist=dist)
+            ok = 1
+        except Exception as e:  # noqa: BLE001 (reported in the JSON line)
+            log(f"[bench] batch stream failed ({e!r}); timing the step graph")
+            stream_failed.append(repr(e)[:200])
+            ss, ok = None, 0
+        if not agree(ok):
+            if not stream_failed:
+                stream_failed.append("stream set-up failed on another rank")
+            del ss
+            return timed_graph(dist)
+        s_d, s_a = (a.copy() for a in ss.step())
+        e_d, e_a = eager_step(dist)
+        same = agree(np.array_equal(s_d, e_d) and np.array_equal(s_a, e_a))
+        checks[f"stream_vs_eager_{dist}"] = "bitwise equal" if same else "DIFFER"
+        if not same:
+            log(f"[bench] batch stream differs from the eager step ({dist}); timing the step graph")
+            stream_failed.append("stream answer differs from the eager step")
+            del ss
+            return timed_graph(dist)
+        h2d = h2d_ms(ss.h_stage[0], ss.d_blk[0]) + (ss.bw * 4,)
+        out = None
+        for _ in range(args.warmup):
+            out = ss.step()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = ss.step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        out = (out[0].copy(), out[1].copy())
+        del ss
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        step_mode[dist] = "stream"
+        return el, kernel_ms(dist), out, h2d
+
     def timed(dist):
         """W untimed warmup steps, then K steps bracketed by barrier +
         synchronize; returns (max-over-ranks seconds, mean scan-kernel ms,
-        the last step's output, (H2D ms, GB/s) or None)."""
+        the last step's output, (H2D ms, GB/s, bytes) or None)."""
+        if use_stream:
+            return timed_stream(dist)
         if use_graph:
             return timed_graph(dist)
         return timed_eager(dist)
@@ -522,6 +595,7 @@ def main():
         ms = (_lib.C.c_float * max(args.steps, 1))()
         n_ev = lib.lmi_timing_read(ms, args.steps)
         kms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
+        step_mode[dist] = "eager"
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64,
                              device=device if torch.distributed.get_backend() == "nccl" else "cpu")
@@ -531,6 +605,9 @@ def main():
 
     el, scan_ms, (dists, anns), h2d = timed(args.dist)
     ms_step = el / args.steps * 1e3
+    # submission to answer: a streamed batch is answered by the third launch
+    # that sees it (plan, scan, merge/replay), a graph-step batch by its own
+    lat_ms = ms_step * (3 if step_mode.get(args.dist) == "stream" else 1)
     value = args.nq / (el / args.steps)
     # the other arithmetic, timed the same way (float64: the reference's on
     # float16 data, e.g. the real clip768 'emb'; float32: on float32 data)
@@ -612,18 +689,16 @@ def main():
         "recall": round(recall, 4), "recall_exact_semantics": round(recall_x, 4),
         "recall_sample": sample, "breakdown_ms": breakdown, "parity": parity,
         "h2d": None if h2d is None else {"ms": round(h2d[0], 4), "gb_s": round(h2d[1], 1),
-                                         "bytes_per_rank": int(4 * (-(-args.nq // world)) * (96 + (384 if q16_exact else 768))),
+                                         "bytes_per_rank": int(h2d[2]),
                                          "queries_staged_as": "f16" if q16_exact else "f32",
                                          "in_step": True,
-                                         "overlapped_with_previous_step": use_graph and not graph_failed and not args.no_pipeline},
+                                         "overlapped": step_mode.get(args.dist) == "stream" or (
+                                             step_mode.get(args.dist) == "graph" and not args.no_pipeline)},
         "dist": args.dist,
-        "step": (("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
-                  "copy stream during the previous step's search (double-buffered), + search + D2H "
-                  "of the answer" if not args.no_pipeline else
-                  "hip-graph replay (H2D of the host batch + search + D2H of the answer)")
-                 if use_graph and not graph_failed else
-                 "eager launches (H2D of the host batch + search + D2H)" +
-                 (f" (graph not used: {graph_failed[0]})" if graph_failed else "")),
+        "step": STEP_TEXT[step_mode.get(args.dist, "eager")](args) +
+                (f" (batch stream not used: {stream_failed[0]})" if stream_failed and use_stream else "") +
+                (f" (graph not used: {graph_failed[0]})" if graph_failed else ""),
+        "latency_ms_per_batch": round(lat_ms, 3) if lat_ms is not None else None,
         "other_dist": {"dist": other, "value": round(args.nq / (el_o / args.steps), 1),
                        "ms_per_step": round(el_o / args.steps * 1e3, 3),
                        "scan_kernel_ms": round(scan_ms_o, 4),

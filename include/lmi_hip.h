@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 6
+#define LMI_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -64,6 +64,18 @@ extern "C" {
  * the objects at or under that bound.  Only for the replay with thresholds
  * (use_threshold); the lists of r = 0 are unchanged. */
 #define LMI_Q_SEED_ROUND0 0x100
+/* ABI 7, flags OR-ed into qmode (lmi_bucket_topk / lmi_bucket_topk_f64*, k <=
+ * LMI_MAX_K): run only some phases of the call, so that a caller can overlap
+ * one batch's plan with another batch's scan (a stream of batches, each with
+ * its own workspace, lists and status word).  The phases, in order: PLAN (the
+ * queries' fragments and norms, the output prefill, the tile plan, the seed
+ * map, the tail split, the bound reset), SCAN (the scan kernel), MERGE (the
+ * chunk merge; in lmi_bucket_topk_f64* also the float64 refinement).  No phase
+ * flag = all three.  The phase calls of one batch take the same arguments and
+ * run in phase order on streams that order them. */
+#define LMI_Q_PHASE_PLAN 0x200
+#define LMI_Q_PHASE_SCAN 0x400
+#define LMI_Q_PHASE_MERGE 0x800
 
 #define LMI_MAX_LAYERS 8
 #define LMI_MAX_K 16          /* largest k of one scan pass (and of K3 / the float32 ABI 1 lists) */

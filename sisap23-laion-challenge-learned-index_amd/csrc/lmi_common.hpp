@@ -124,6 +124,14 @@ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 
 // ---- internal entry points shared between translation units -------------
+// phases of bucket_topk_impl (LMI_Q_PHASE_* of the ABI, shifted to bits 0..2)
+constexpr int kPhasePlan = 1, kPhaseScan = 2, kPhaseMerge = 4, kPhaseAll = 7;
+// LMI_Q_PHASE_* bits of a qmode -> kPhase* (none set = all); strips them from qmode
+inline int take_phases(int32_t& qmode) {
+    const int p = (qmode >> 9) & 7;
+    qmode &= ~(7 << 9);
+    return p ? p : kPhaseAll;
+}
 // K2 up to the merged per-pair lists (lmi_scan.hip): lmi_bucket_topk with an
 // optional third output, the shard-local row of every entry (-1 = empty).
 // lo_g (nullable, device [nq*R]): keep only objects after the (distance,
@@ -136,7 +144,7 @@ int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int3
                      int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                      size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g = nullptr,
                      int32_t ldo = 0, bool prefill = true, bool seed_r0 = false,
-                     float seed_margin = 0.0f);
+                     float seed_margin = 0.0f, int phases = kPhaseAll);
 size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
                             int32_t qmode, bool lo = false);
 // k > LMI_MAX_K: passes_of() passes of kp-entry lists; bucket_topk_passes fills

@@ -383,6 +383,7 @@ int num_cus_ref() {
 extern "C" size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                                int32_t k, int32_t qmode) {
     qmode &= ~LMI_Q_SEED_ROUND0;
+    lmi::take_phases(qmode);
     if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_F64) return 0;
     return lmi::refine_ws(idx, nq, R, k, qmode).total;
 }
@@ -421,6 +422,7 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     using namespace lmi;
     const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
     qmode &= ~LMI_Q_SEED_ROUND0;
+    const int phases = take_phases(qmode);
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_F64, "k=%d outside [1, %d]", k, LMI_MAX_K_F64);
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
@@ -465,7 +467,11 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     a.failed = (int32_t*)(ws + w.failed);
     a.n_failed = (int32_t*)(ws + w.nfailed);
     a.status = status;
-    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
+    if (w.passes && phases != kPhaseAll) {
+        set_error("phase flags need k + 5 <= %d (one scan pass)", LMI_MAX_K);
+        return LMI_E_UNSUPPORTED;
+    }
+    if (phases & kPhasePlan) LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
     int rc = w.passes
         ? bucket_topk_passes(idx, q, nq, ldq, classes, R, k + 5, qmode, (float*)(ws + w.ld),
                              (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), kl, status,
@@ -473,8 +479,9 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
         : bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
                            (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
                            ws + w.scan, w.total - w.scan, s, nullptr, 0, true, seed,
-                           (float)(2.0 * eps));
+                           (float)(2.0 * eps), phases);
     if (rc != LMI_OK) return rc;
+    if (!(phases & kPhaseMerge)) return LMI_OK;
     const int64_t P = (int64_t)nq * R;
     const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));
     const dim3 fgrid((unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref())));
@@ -493,7 +500,9 @@ extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_
                                          int32_t* count_out, void* stream) {
     using namespace lmi;
     LMI_CHECK_ARG(workspace && idx && count_out, "null pointer");
-    const RefineWs w = refine_ws(idx, nq, R, k, qmode & ~LMI_Q_SEED_ROUND0);
+    qmode &= ~LMI_Q_SEED_ROUND0;
+    take_phases(qmode);
+    const RefineWs w = refine_ws(idx, nq, R, k, qmode);
     LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + w.nfailed, 4,
                                hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
     LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));

@@ -1697,6 +1697,7 @@ extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq
                                            int32_t k, int32_t qmode) {
     using namespace lmi;
     qmode &= ~LMI_Q_SEED_ROUND0;
+    take_phases(qmode);
     if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_PASSES) return 0;
     if (k <= LMI_MAX_K) return scan_workspace_bytes(idx, nq, R, k, qmode);
     int kp;
@@ -1717,9 +1718,14 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
     qmode &= ~LMI_Q_SEED_ROUND0;
+    const int phases = take_phases(qmode);
     if (k <= LMI_MAX_K)
         return bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
-                                status, workspace, ws_bytes, s, nullptr, 0, true, seed);
+                                status, workspace, ws_bytes, s, nullptr, 0, true, seed, 0.0f, phases);
+    if (phases != kPhaseAll) {
+        set_error("phase flags need k <= %d (one scan pass)", LMI_MAX_K);
+        return LMI_E_UNSUPPORTED;
+    }
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(k <= LMI_MAX_K_PASSES, "k=%d outside [1, %d]", k, LMI_MAX_K_PASSES);
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
@@ -1749,7 +1755,9 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                           const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                           int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                           size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g, int32_t ldo,
-                          bool prefill, bool seed_r0, float seed_margin) {
+                          bool prefill, bool seed_r0, float seed_margin, int phases) {
+    const bool do_plan = phases & kPhasePlan, do_scan = phases & kPhaseScan,
+               do_merge = phases & kPhaseMerge;
     using namespace lmi;
     if (ldo <= 0) ldo = k;
     LMI_CHECK_ARG(idx != nullptr, "null index");
@@ -1779,7 +1787,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const int P = nq * R;
     const int KL = pick_kl(idx, qmode, k);
 
-    {
+    if (do_plan) {
         const dim3 pg((nq + kThreads / 64 - 1) / (kThreads / 64));
         const bool vec = ((uintptr_t)q % 16 == 0) && (ldq % 4 == 0);
         auto* kp = f16math ? (vec ? prep_kernel<true, true> : prep_kernel<true, false>)
@@ -1787,8 +1795,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         hipLaunchKernelGGL(kp, pg, dim3(kThreads), 0, s, q, nq, ldq, idx->d, idx->d_pad,
                            (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d, out_pos,
                            out_row, prefill ? R * ldo : 0);
+        LMI_LAUNCH_CHECK("prep_kernel");
     }
-    LMI_LAUNCH_CHECK("prep_kernel");
     if (idx->n_rows == 0) return LMI_OK;
 
     int32_t* counts = (int32_t*)(ws + w.counts);
@@ -1802,31 +1810,35 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     while (ng & (ng - 1)) ng &= ng - 1;
 
     // pair_bucket = -1 marks pairs whose class is out of range (never filled)
-    LMI_TRY(fill_u32(pair_bucket, 0xffffffffu, (size_t)P, s));
-    hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, counts);
-    LMI_LAUNCH_CHECK("plan_count_kernel");
+    if (do_plan) {
+        LMI_TRY(fill_u32(pair_bucket, 0xffffffffu, (size_t)P, s));
+        hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, counts);
+        LMI_LAUNCH_CHECK("plan_count_kernel");
+    }
     // (the seed reads the pair position of every (q, 0); pairs whose class is
     // out of range keep -1)
     const bool seed = seed_r0 && w.use_v3 && !LOP && R > 1;
     int32_t* pair_pos = seed ? (int32_t*)(ws + w.pair_pos) : nullptr;
-    if (seed) LMI_TRY(fill_u32(pair_pos, 0xffffffffu, (size_t)P, s));
-    hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
-                       idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
-    LMI_LAUNCH_CHECK("plan_fill_kernel");
+    if (do_plan) {
+        if (seed) LMI_TRY(fill_u32(pair_pos, 0xffffffffu, (size_t)P, s));
+        hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
+                           idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
+        LMI_LAUNCH_CHECK("plan_fill_kernel");
+    }
     int32_t* seed_pos = seed ? (int32_t*)(ws + w.seed_pos) : nullptr;
-    if (seed) {
+    if (seed && do_plan) {
         hipLaunchKernelGGL(seed_pos_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pair_q, pair_pos,
                            P, R, seed_pos);
         LMI_LAUNCH_CHECK("seed_pos_kernel");
     }
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
-    if (!nearest_first && env_config().scan_order != 0) {
+    if (do_plan && !nearest_first && env_config().scan_order != 0) {
         hipLaunchKernelGGL(tile_order_kernel, dim3(ng), dim3(1024), 0, s, tiles, (Tile*)(ws + w.tiles_tmp),
                            meta, idx->bucket_off, idx->chunk_rows, QB, counts,
                            env_config().scan_order == 2 ? 1 : 0);
         LMI_LAUNCH_CHECK("tile_order_kernel");
     }
-    if (nearest_first) {
+    if (do_plan && nearest_first) {
         int32_t* pref = (int32_t*)(ws + w.pref);
         int32_t* n_seed = (int32_t*)(ws + w.n_seed);
         hipLaunchKernelGGL(pref_kernel, dim3((P + kThreads / 64 - 1) / (kThreads / 64)), dim3(kThreads),
@@ -1840,19 +1852,20 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         hipLaunchKernelGGL(tile3_fill_kernel, dim3(C), dim3(kThreads), 0, s, counts, idx->chunk_first,
                            pref, n_seed, C, QB, tiles, meta, work);
         LMI_LAUNCH_CHECK("tile3_fill_kernel");
-        ng = 1;  // one queue: seed tiles strictly first
     }
+    if (nearest_first) ng = 1;  // one queue: seed tiles strictly first
 
     // tail split (scan v3): K = the queue's share of the grid
     uint32_t* split_mask = (uint32_t*)(ws + w.split_mask);
-    LMI_TRY(fill_u32(split_mask, 0u, (size_t)P, s));
+    if (do_plan) LMI_TRY(fill_u32(split_mask, 0u, (size_t)P, s));
     // (not after the nearest-chunk-first plan: its queue has no seed count)
     const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
                         : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
                                                                             : (num_cus() + ng - 1) / ng);
     const int64_t* scan_off = idx->bucket_off;
     if (split_k > 0) {
-        hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, (Tile*)(ws + w.tiles_split),
+        if (do_plan)
+            hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, (Tile*)(ws + w.tiles_split),
                            meta, idx->bucket_off, (int64_t*)(ws + w.ext_off), C, idx->chunk_rows,
                            std::max(idx->max_chunks, 1), split_k, split_mask);
         LMI_LAUNCH_CHECK("tail_split_kernel");
@@ -1879,6 +1892,10 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     a.lo_g = lo_g;
 
     int rc;
+    if (phases != kPhaseAll && !(w.use_v2 || w.use_v3)) {
+        set_error("phase flags need the fp16 scan (scan v2/v3: fp16 corpus and fp16-exact queries)");
+        return LMI_E_UNSUPPORTED;
+    }
     if (w.use_v2 || w.use_v3) {
         Scan2Args b{};
         b.corpus = reinterpret_cast<const _Float16*>(idx->corpus);
@@ -1906,7 +1923,9 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         // seeds when the same batch is repeated) to measure seeding quality
         if (!env_config().scan_keep_thr)
 #endif
-        LMI_TRY(fill_u32(ws + w.thr_g, 0xffffffffu, (size_t)P * 2, s));
+        if (do_plan) LMI_TRY(fill_u32(ws + w.thr_g, 0xffffffffu, (size_t)P * 2, s));
+        if (!do_scan) rc = LMI_OK;
+        else
         if (w.use_v3 && LOP) {
             // the passes' lists are 15 entries on v3 (passes_of)
             if (KL != 15) {
@@ -1939,6 +1958,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                         : launch_scan<16, false, float>(a, idx->d_pad, s);
     }
     if (rc != LMI_OK) return rc;
+    if (!do_merge) return LMI_OK;
 
     const int grid = (P + 63) / 64;
 #define LMI_CM(KLV, ROWSV)                                                                         \

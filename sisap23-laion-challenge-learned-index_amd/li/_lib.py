@@ -35,6 +35,9 @@ LMI_ROUTER_ARGMAX = 1
 LMI_Q_F16 = 0
 LMI_Q_F32 = 1
 LMI_Q_SEED_ROUND0 = 0x100
+LMI_Q_PHASE_PLAN = 0x200
+LMI_Q_PHASE_SCAN = 0x400
+LMI_Q_PHASE_MERGE = 0x800
 LMI_MAX_LAYERS = 8
 LMI_MAX_K = 16
 LMI_MAX_K_PASSES = 1024
@@ -94,7 +97,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class IndexDesc(C.Structure):

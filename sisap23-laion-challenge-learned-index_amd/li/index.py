@@ -487,13 +487,15 @@ def _workspace(ws, need: int, what: str) -> torch.Tensor:
 
 def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
                 qmode: Optional[int] = None, stream=None, out=None, ws=None,
-                seed_round0: bool = False):
+                seed_round0: bool = False, phases: int = 0):
     """K2 on one shard.  Returns (d [nq,R,k] f32, pos [nq,R,k] int32, status int32 tensor);
     `out` = such a triple to write into (the status word zeroed by the caller);
     `ws` = a caller-owned uint8 workspace (default: the index's cached one,
     which a later call with a larger batch may replace — a captured graph
     passes its own).  `seed_round0` (LMI_Q_SEED_ROUND0, the thresholded
-    replay only): probes r >= 1 keep only objects under the round-0 bound."""
+    replay only): probes r >= 1 keep only objects under the round-0 bound.
+    `phases` (LMI_Q_PHASE_* bits, 0 = all): run only those phases of the call
+    (StreamedSearch overlaps one batch's plan with another's scan)."""
     lib = _lib.load()
     q = _rows_f32(q, index.device)
     classes = _as_torch(classes, index.device, torch.int32)
@@ -513,7 +515,7 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
     else:
         _workspace(ws, lib.lmi_scan_workspace_bytes(C.byref(index.desc), nq, R, k, qmode), "scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
-    flags = _lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0
+    flags = (_lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0) | phases
     check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(index.desc), ptr(q), nq, q.stride(0),
                                                  ptr(classes), R, k, qmode | flags, ptr(out_d),
                                                  ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
@@ -522,7 +524,8 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
 
 def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
                     qmode: Optional[int] = None, eps: Optional[float] = None, stream=None,
-                    fallback_count: bool = False, out=None, ws=None, seed_round0: bool = False):
+                    fallback_count: bool = False, out=None, ws=None, seed_round0: bool = False,
+                    phases: int = 0):
     """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
     arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
     (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback]);
@@ -562,7 +565,7 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     else:
         _workspace(ws, need, "float64 scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
-    flags = _lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0
+    flags = (_lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0) | phases
     check("lmi_bucket_topk_f64q", lib.lmi_bucket_topk_f64q(
         C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
         ptr(classes), R, k, qmode | flags, float(eps), ptr(out_d), ptr(out_pos), ptr(status),
@@ -790,6 +793,11 @@ class Searcher:
                  torch.from_numpy(np.ascontiguousarray(self.index.pos_to_id, dtype=np.int64)).to(dev))
             self._dev_tables = t
         return t
+
+    def streamed(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "StreamedSearch":
+        """The step as a three-stage pipeline of captured graphs over a stream
+        of batches (StreamedSearch); answers equal search(...) per batch."""
+        return StreamedSearch(self, q_nav, q_search, R, k, **kw)
 
     def graph(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "GraphedSearch":
         """The step captured as a HIP graph (GraphedSearch), from the batch in
@@ -1264,6 +1272,277 @@ class GraphedSearch:
                                     _as_torch(_host_array(q_search), dev, torch.float32),
                                     self.R, k=self.k, k_round=self.k_round,
                                     use_threshold=self.use_threshold, dist=self.dist)
+
+
+
+class StreamedSearch:
+    """A stream of query batches through the step as a three-stage pipeline of
+    captured HIP graphs ("Batch stream").  Every launch runs three
+    independent branches, each on its own slot of device buffers:
+
+        P  batch b+2: H2D of its staged host rows -> router (K1) -> plan
+           (lmi_bucket_topk, PLAN phase: query fragments and norms, the tile
+           plan, the seed map, the tail split, the bound reset)
+        S  batch b+1: the scan kernel (SCAN phase)
+        F  batch b:   chunk merge (MERGE phase; + the float64 refinement)
+           [-> all-gather + K3 at G > 1] -> replay (K4) -> D2H of the answer
+
+    so one batch's scan runs while the batch before it is merged, replayed and
+    copied out and the batch after it is uploaded, routed and planned: the
+    latency-bound kernels fill the scan's tail instead of following it.  Every
+    batch passes through every stage (the same kernels as Searcher.search), so
+    each answer equals Searcher.search of its batch bit for bit; a launch
+    answers the batch submitted two launches earlier.
+
+    Three slots of per-batch device state (staged rows, classes, scan
+    workspace, lists, answer) rotate over the launches: launch t runs graph
+    t mod 3 with P on slot t mod 3, S on slot (t+2) mod 3 and F on slot
+    (t+1) mod 3.  A graph is launched only when its S and F slots hold a
+    planned / scanned batch (the fill and drain run the same branch functions
+    eagerly), so no kernel ever reads an unplanned workspace.
+
+    G > 1: every rank uploads and routes the whole batch in P (no collective
+    there, and P is off the critical path); the one collective, the list
+    exchange, runs in F as in Searcher.search.  fp16 index and fp16-exact
+    query batches only (the phased scan is the fp16 scan); other batches go
+    through GraphedSearch / Searcher.search."""
+
+    NS = 3
+
+    def __init__(self, searcher: "Searcher", q_nav, q_search, R: int, k: int = 10, *,
+                 k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
+                 capture: bool = True):
+        s = searcher
+        ix = s.index
+        dev = ix.device
+        lib = _lib.load()
+        self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
+        self.use_threshold, self.dist = use_threshold, dist
+        G = ix.world
+        self.G = torch.distributed.get_world_size(s.group) if G > 1 else 1
+        if k_round > _lib.LMI_MAX_K:
+            raise ValueError("the phased scan needs k_round <= 16")
+        if capture and self.G > 1 and torch.distributed.get_backend(s.group) != "nccl":
+            raise ValueError("graph capture needs RCCL collectives (capture=False runs the "
+                             "branches eagerly, e.g. over gloo)")
+        nav, qs = _host_array(q_nav), _host_array(q_search)
+        nq, d, dn = int(qs.shape[0]), ix.d, int(nav.shape[1])
+        if qs.shape != (nq, d) or nav.shape[0] != nq:
+            raise ValueError("query shapes do not match the index")
+        if not (ix.storage == "f16" and d % 2 == 0):
+            raise ValueError("the batch stream needs an fp16 index with an even d")
+        self.nq, self.d, self.dn = nq, d, dn
+        f64 = dist == "f64"
+        self.w = k_round if R == 1 else k
+        kl = k_round
+        NS = self.NS
+        self.bw = nq * dn + nq * (d // 2)
+        pin = torch.cuda.is_available()
+        self.h_stage = [torch.zeros((self.bw,), dtype=torch.int32, pin_memory=pin) for _ in range(NS)]
+        self.d_blk = [torch.empty((self.bw,), dtype=torch.int32, device=dev) for _ in range(NS)]
+        self.q32 = [torch.empty((nq, d), dtype=torch.float32, device=dev) for _ in range(NS)]
+        self.cls = [torch.empty((nq, R), dtype=torch.int32, device=dev) for _ in range(NS)]
+        wsb = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
+            C.byref(ix.desc), nq, R, kl, _lib.LMI_Q_F16)
+        self.ws = [torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=dev) for _ in range(NS)]
+        self.ans = [answer_buffer(nq, self.w, dev) for _ in range(NS)]
+        self.h_ans = [torch.empty((3 * nq * self.w + 2,), dtype=torch.int32, pin_memory=pin)
+                      for _ in range(NS)]
+        ldt = torch.float64 if f64 else torch.float32
+        if self.G > 1:
+            from .dist import packed_lists
+            self.pk = [packed_lists(nq * R, kl, f64, dev) for _ in range(NS)]
+            self.lists = [(b[1].view(nq, R, kl), b[2].view(nq, R, kl), b[3]) for b in self.pk]
+        else:
+            self.pk = None
+            self.lists = [(torch.empty((nq, R, kl), dtype=ldt, device=dev),
+                           torch.empty((nq, R, kl), dtype=torch.int32, device=dev),
+                           self.ans[j][3][0:1]) for j in range(NS)]
+        bsz, p2id = s._device_tables()
+        seed = use_threshold and k <= k_round and _SEED_ROUND0
+        scan_fn = bucket_topk_f64 if f64 else bucket_topk
+        self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
+
+        def phase(j, ph):
+            dl, pl, st = self.lists[j]
+            scan_fn(ix, self.q32[j], self.cls[j], kl, qmode=_lib.LMI_Q_F16, out=(dl, pl, st),
+                    ws=self.ws[j], seed_round0=seed, phases=ph)
+
+        def plan(j):
+            self.lists[j][2].zero_()
+            blk = self.d_blk[j]
+            blk.copy_(self.h_stage[j], non_blocking=True)
+            s.router.topr(blk[:nq * dn].view(torch.float32).view(nq, dn), R, out=self.cls[j])
+            self.q32[j].copy_(blk[nq * dn:].view(torch.float16).view(nq, d))
+            phase(j, _lib.LMI_Q_PHASE_PLAN)
+
+        def scan(j):
+            phase(j, _lib.LMI_Q_PHASE_SCAN)
+
+        def finish(j):
+            phase(j, _lib.LMI_Q_PHASE_MERGE)
+            buf, ad, aa, ast = self.ans[j]
+            ast[1:2].zero_()
+            if self.G > 1:
+                from .dist import gather_merge_packed
+                dd, pp, _ = gather_merge_packed(self.pk[j][0], nq * R, kl, f64, s.group,
+                                                status_out=ast[0:1])
+                dd, pp = dd.view(nq, R, kl), pp.view(nq, R, kl)
+            else:
+                dd, pp = self.lists[j][0], self.lists[j][1]
+            replay_device(self.cls[j], dd, pp, k_round=k_round, k_final=k, bucket_size=bsz,
+                          pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]))
+            self.h_ans[j].copy_(buf, non_blocking=True)
+
+        self._plan, self._scan, self._finish = plan, scan, finish
+        self._side = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+
+        def launch_body(g):
+            # S first (the persistent scan takes the CUs first; P and F fill in
+            # beside it and in its tail), then P and F on forked streams
+            main = torch.cuda.current_stream(dev)
+            b1, b2 = self._side
+            b1.wait_stream(main)
+            b2.wait_stream(main)
+            scan((g + 2) % NS)
+            with torch.cuda.stream(b1):
+                plan(g)
+            with torch.cuda.stream(b2):
+                finish((g + 1) % NS)
+            main.wait_stream(b1)
+            main.wait_stream(b2)
+
+        self._body = launch_body
+        self.graphs = None
+        self._t = None  # launch counter once primed
+        if not self.stage(nav, qs):
+            raise ValueError("the batch stream needs fp16-exact query batches")
+        for j in range(NS):
+            self.h_stage[j].copy_(self.h_stage[0])
+        # warm-up: one eager pass of every branch on every slot (allocations,
+        # kernel attributes, communicators), in pipeline order, on a side stream
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        err = None
+        try:
+            with torch.cuda.stream(side):
+                for j in range(NS):
+                    plan(j)
+                    scan(j)
+                    finish(j)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+        except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
+            err = e
+        if self.G > 1:
+            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
+            if int(ok.item()) == 0:
+                raise RuntimeError(f"stream warm-up failed on some rank: {err!r}")
+        elif err is not None:
+            raise err
+        if capture:
+            self.graphs = []
+            for g in range(NS):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    launch_body(g)
+                self.graphs.append(gr)
+            torch.cuda.synchronize(dev)
+
+    def stage(self, q_nav, q_search, slot: Optional[int] = None) -> bool:
+        """Write a batch into the pinned staging rows of `slot` (default: the
+        slot the next launch plans).  False if a clip768 value is not
+        fp16-representable (the stream cannot take that batch)."""
+        nav = _host_array(q_nav).astype(np.float32, copy=False)
+        qs = _host_array(q_search)
+        nq, d, dn = self.nq, self.d, self.dn
+        if nav.shape != (nq, dn) or qs.shape != (nq, d):
+            raise ValueError("a staged batch must have the stream's shape")
+        if qs.dtype == np.float16:
+            q16 = qs
+        else:
+            q32 = qs.astype(np.float32, copy=False)
+            q16 = q32.astype(np.float16)
+            if not np.array_equal(q16.astype(np.float32), q32):
+                return False
+        if slot is None:
+            slot = (self._t or 0) % self.NS
+        blk = self.h_stage[slot].numpy()
+        blk[:nq * dn].view(np.float32).reshape(nq, dn)[:] = nav
+        blk[nq * dn:].view(np.float16).reshape(nq, d)[:] = q16
+        return True
+
+    def prime(self):
+        """Fill the pipeline with the staged rows of slots 1 and 2 (eagerly:
+        plan + scan of slot 1, plan of slot 2): the next launch answers slot 1."""
+        dev = self.searcher.index.device
+        self._plan(1)
+        self._scan(1)
+        self._plan(2)
+        torch.cuda.current_stream(dev).synchronize()
+        self._t = 0
+
+    def step(self):
+        """One launch -> (dists f64 [nq, w], anns uint32 [nq, w]) of the batch
+        it finished (numpy views, valid for the next two launches).  Plans the
+        rows staged in slot t mod 3 (stage() before step() to stream a new
+        batch; without it the slot's previous rows are planned again)."""
+        if self._t is None:
+            self.prime()
+        dev = self.searcher.index.device
+        g = self._t % self.NS
+        if self.graphs is not None:
+            self.graphs[g].replay()
+        else:
+            self._body(g)
+        self._t += 1
+        if self.G > 1 and self.graphs is not None:
+            _wait_with_deadline(dev, self.timeout_s)
+        else:
+            torch.cuda.current_stream(dev).synchronize()
+        return self._answer((g + 1) % self.NS)
+
+    def _answer(self, j):
+        hd, ha, st, rst = answer_views(self.h_ans[j], self.nq, self.w)
+        if st & (_lib.LMI_STATUS_INTERNAL | _lib.LMI_STATUS_QUERY_NOT_F16) or rst:
+            raise RuntimeError(f"stream: status {st}/{rst}")
+        return hd, ha
+
+    def stream(self, batches):
+        """Answer an iterable of (q_nav, q_search) batches in order, yielding
+        (dists, anns) copies per batch: two batches fill the pipeline, then one
+        launch per batch, then the last two finish eagerly."""
+        dev = self.searcher.index.device
+        sync = lambda: torch.cuda.current_stream(dev).synchronize()
+        it = iter(batches)
+        first = []
+        for b in it:
+            first.append(b)
+            if len(first) == 2:
+                break
+        for j, b in zip((1, 2), first):
+            if not self.stage(*b, slot=j):
+                raise ValueError("the batch stream needs fp16-exact query batches")
+        if len(first) < 2:
+            for j in (1, 2)[:len(first)]:
+                self._plan(j); self._scan(j); self._finish(j); sync()
+                yield tuple(a.copy() for a in self._answer(j))
+            return
+        self.prime()
+        for b in it:
+            if not self.stage(*b, slot=self._t % self.NS):
+                raise ValueError("the batch stream needs fp16-exact query batches")
+            yield tuple(a.copy() for a in self.step())
+        # drain: slot (t+1)%3 holds the scanned last-but-one batch, slot
+        # (t+2)%3 the planned last one (launch t-1 planned it)
+        t = self._t
+        jf, js = (t + 1) % self.NS, (t + 2) % self.NS
+        self._finish(jf); sync()
+        yield tuple(a.copy() for a in self._answer(jf))
+        self._scan(js); self._finish(js); sync()
+        yield tuple(a.copy() for a in self._answer(js))
+        self._t = None
 
 
 def _wait_with_deadline(dev, timeout_s: float) -> None:

@@ -1,0 +1,100 @@
+"""StreamedSearch (the step as a three-stage pipeline of captured graphs over a
+stream of batches: plan of batch b+2, scan of b+1, merge/replay/D2H of b in
+one launch) answers every batch exactly as Searcher.search does; the phase
+flags of lmi_bucket_topk (ABI 7) compose to the one-call result."""
+import numpy as np
+import pytest
+import torch
+
+import workloads
+from li import _lib
+from li.index import DeviceIndex, DeviceRouter, Searcher, bucket_topk, bucket_topk_f64
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup():
+    w = workloads.clustered(n=6000, nq=300, C=16, seed=61, label_mode="near")
+    s = Searcher(DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=512, device="cuda"),
+                 DeviceRouter(w["layers"], device="cuda"))
+    return w, s
+
+
+def _batches(w, n, seed=0):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        p = rng.permutation(w["q"].shape[0])
+        out.append((w["qn"][p], w["q"][p]))
+    return out
+
+
+T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("dist", ["f32", "f64"])
+@pytest.mark.parametrize("k", [10, 7])
+def test_phases_compose_to_one_call(setup, dist, k):
+    w, s = setup
+    ix = s.index
+    q = T(w["q"])
+    cls = s.router.topr(T(w["qn"]), 4)[0]
+    fn = bucket_topk_f64 if dist == "f64" else bucket_topk
+    d0, p0, st0 = fn(ix, q, cls, k, qmode=_lib.LMI_Q_F16)
+    ws = torch.empty_like(ix._ws["f64"] if dist == "f64" else ix._ws["buf"])
+    outd = torch.empty_like(d0)
+    outp = torch.empty_like(p0)
+    st = torch.zeros((1,), dtype=torch.int32, device="cuda")
+    for ph in (_lib.LMI_Q_PHASE_PLAN, _lib.LMI_Q_PHASE_SCAN, _lib.LMI_Q_PHASE_MERGE):
+        fn(ix, q, cls, k, qmode=_lib.LMI_Q_F16, out=(outd, outp, st), ws=ws, phases=ph)
+    assert torch.equal(outd, d0) and torch.equal(outp, p0) and int(st.item()) == int(st0.item())
+
+
+@pytest.mark.parametrize("dist,R", [("f32", 4), ("f64", 4), ("f32", 1), ("f32", 7)])
+def test_stream_of_batches_equals_search(setup, dist, R):
+    w, s = setup
+    bs = _batches(w, 6, seed=R)
+    ref = [s.search(T(a), T(b), R, k=10, dist=dist) for a, b in bs]
+    st = s.streamed(w["qn"], w["q"], R, k=10, dist=dist)
+    got = list(st.stream(bs))
+    assert len(got) == len(bs)
+    for (d, a), (d0, a0) in zip(got, ref):
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_short_streams(setup, n):
+    w, s = setup
+    bs = _batches(w, n, seed=10 + n)
+    ref = [s.search(T(a), T(b), 4, k=10) for a, b in bs]
+    got = list(s.streamed(w["qn"], w["q"], 4, k=10).stream(bs))
+    assert len(got) == n
+    for (d, a), (d0, a0) in zip(got, ref):
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+
+
+def test_steps_on_one_staged_batch(setup):
+    """The bench's use: one batch staged in every slot, step() after step(),
+    with eager work between launches."""
+    w, s = setup
+    d0, a0 = s.search(T(w["qn"]), T(w["q"]), 4, k=10)
+    st = s.streamed(w["qn"], w["q"], 4, k=10)
+    for i in range(7):
+        d, a = st.step()
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+        if i == 3:
+            junk = [t.clone() for t in vars(s.index).values() if isinstance(t, torch.Tensor) and t.is_cuda]
+            s.search(T(w["qn"][::-1].copy()), T(w["q"][::-1].copy()), 4, k=10)
+            del junk
+
+
+def test_stream_rejects_inexact_batches(setup):
+    w, s = setup
+    st = s.streamed(w["qn"], w["q"], 4, k=10)
+    assert not st.stage(w["qn"], w["q"] + np.float32(1e-5))
+    with pytest.raises(ValueError):
+        s.streamed(w["qn"], w["q"] + np.float32(1e-5), 4, k=10)

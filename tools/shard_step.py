@@ -64,9 +64,21 @@ for W in map(int, a.worlds.split(",")):
     h_full, h_part = h2d(full), h2d(part)
     del g
     proj = elg - h_full + h_part
+    # the batch stream (StreamedSearch): every rank uploads and routes the
+    # whole batch in the plan branch, beside the scan; the list all-gather + K3
+    # (rank 0 of W here: a one-process group, so none) runs in the F branch
+    st = s.streamed(qn, q, 4, k=10)
+    for _ in range(3):
+        st.step()
+    torch.cuda.synchronize(); t0 = time.perf_counter()
+    for _ in range(a.steps):
+        st.step()
+    torch.cuda.synchronize(); els = (time.perf_counter() - t0) / a.steps * 1e3
+    del st
     print(f"world {W} chunk {ck}: step {el:.3f} ms eager (device-resident queries), {elg:.3f} ms graph "
           f"(whole-batch H2D {h_full:.3f} ms); with the 1/{W} upload ({h_part:.3f} ms): {proj:.3f} ms "
           f"-> {10000 / proj * 1e3:.0f} q/s on {W} GPUs (all-gathers over xGMI excluded); "
-          f"breakdown {br}", flush=True)
+          f"batch stream {els:.3f} ms/launch (whole-batch H2D, list all-gather excluded) -> "
+          f"{10000 / els * 1e3:.0f} q/s; breakdown {br}", flush=True)
     del ix, s; torch.cuda.empty_cache()
 dist.destroy_process_group()
