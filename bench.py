@@ -391,10 +391,11 @@ def main():
     ap.add_argument("--parity-sample", type=int, default=64,
                     help="queries whose lists are checked against a float64 brute force")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-stream", action="store_true",
-                    help="time the per-batch step graph (GraphedSearch) instead of the batch stream "
-                         "(StreamedSearch, the default: plan of batch b+2, scan of b+1 and "
-                         "merge/replay/D2H of b in one launch of three captured branches)")
+    ap.add_argument("--stream", action="store_true",
+                    help="time the batch stream (StreamedSearch: plan of batch b+2, scan of b+1 and "
+                         "merge/replay/D2H of b in one launch of three captured branches) instead of "
+                         "the per-batch step graph with the upload pipelined (the default; measured "
+                         "equal at G = 1 and faster at G = 8, DESIGN.md §5)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="upload each batch inside its own step instead of during the previous "
                          "step's search (GraphedSearch(pipeline=True), the default)")
@@ -433,7 +434,7 @@ def main():
     q_h = q.cpu().numpy()
     q16_exact = index.storage == "f16" and bool(np.array_equal(q_h.astype(np.float16).astype(np.float32), q_h))
     # the batch stream takes fp16-exact batches on an fp16 index (the phased scan)
-    use_stream = use_graph and not args.no_stream and q16_exact
+    use_stream = use_graph and args.stream and q16_exact
     qn_pin = torch.from_numpy(qn_h).pin_memory()
     q_pin = torch.from_numpy(q_h.astype(np.float16) if q16_exact else q_h).pin_memory()
     checks = {}

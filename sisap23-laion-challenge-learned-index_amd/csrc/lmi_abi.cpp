@@ -37,6 +37,7 @@ EnvConfig read_env() {
     e.scan_order = env_i("LMI_SCAN_ORDER", 0);
     e.scan_lag = env_i("LMI_SCAN_LAG", 0);
     e.scan_split = env_i("LMI_SCAN_SPLIT", 0);
+    e.scan_split_parts = env_i("LMI_SCAN_SPLIT_PARTS", 2);
     e.scan_wgs = env_i("LMI_SCAN_WGS", 0);
     e.scan_no_pref = env_b("LMI_SCAN_NO_PREF");
     e.scan_keep_thr = env_b("LMI_SCAN_KEEP_THR");

@@ -15,8 +15,9 @@ struct EnvConfig {
     int scan_groups;     // LMI_SCAN_GROUPS: tile queues (power of two <= 8), 0 = default
     int scan_order;      // LMI_SCAN_ORDER: 0 plan order (default), 1 heavy-first per tile, 2 per chunk
     int scan_lag;        // LMI_SCAN_LAG
-    int scan_split;      // LMI_SCAN_SPLIT: halve the last K tiles of every queue (0: K = the
+    int scan_split;      // LMI_SCAN_SPLIT: split the last K tiles of every queue (0: K = the
                          //   queue's share of the grid, the default; -1: off)
+    int scan_split_parts;// LMI_SCAN_SPLIT_PARTS: row parts of a split tile (2..8, default 2)
     int scan_wgs;        // LMI_SCAN_WGS: persistent scan workgroups (0 = one per CU; tests
                          //   use a few to make tiles run after others have published bounds)
     bool scan_no_pref;   // LMI_SCAN_NO_PREF

@@ -341,21 +341,23 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ til
 }
 
 // Tail split (scan v3; LMI_SCAN_SPLIT): the last K tiles of every group queue
-// are replaced by their two row halves, so the launch ends on half-size tiles.
-// The scan kernel is unchanged: a half is an ordinary tile whose bucket is a
-// virtual entry of an extended bucket table, chosen so that the scan's own
+// are replaced by S row parts each (LMI_SCAN_SPLIT_PARTS, default 2), so the
+// launch ends on small tiles.  The scan kernel is unchanged: a part is an
+// ordinary tile whose bucket is a virtual entry of an extended bucket table,
+// chosen so that the scan's own
 //     row0 = off[c] + chunk * chunk_rows,  rows = min(chunk_rows, off[c + 1] - row0)
-// give the half's rows, and whose chunk is its partial-list slot: the first
-// half keeps chunk j's slot, the second writes slot X + j (X = max_chunks, the
-// stride is 2X); bit j of mask[pp] tells the chunk merge to read it (chunks
-// j < 32 only).
+// give the part's rows, and whose chunk is its partial-list slot: part s of
+// chunk j writes slot s*X + j (X = max_chunks, the stride is S*X; part 0 keeps
+// chunk j's slot); bit j of mask[pp] tells the chunk merge to read slots
+// X + j .. (S-1)*X + j too (chunks j < 32 only).  Every part but the last has
+// a whole number of 32-row blocks, and at least two.
 __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict__ tin,
                                                          Tile* __restrict__ tout,
                                                          int32_t* __restrict__ meta,
                                                          const int64_t* __restrict__ bucket_off,
                                                          int64_t* __restrict__ ext_off, int32_t C,
                                                          int32_t chunk_rows, int32_t X, int32_t K,
-                                                         uint32_t* __restrict__ mask) {
+                                                         int32_t S, uint32_t* __restrict__ mask) {
     __shared__ int wsp[4];
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (x == 0)
@@ -363,7 +365,7 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
     const int o = meta[x], n = meta[kGroups + x];
     const int seeds = meta[2 * kGroups + 1 + x];
     const int k2 = max(0, min(K, n - seeds));  // the candidates: the queue's last k2 tiles
-    const int no = o + x * K;                  // (every queue grows by at most K)
+    const int no = o + x * K * (S - 1);        // (every queue grows by at most K (S - 1))
     for (int i = tid; i < n - k2; i += 256) tout[no + i] = tin[o + i];
     Tile t{};
     int64_t rs = 0, re = 0;
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
         t = tin[o + n - k2 + tid];
         rs = bucket_off[t.c] + (int64_t)t.chunk * chunk_rows;
         re = min(rs + (int64_t)chunk_rows, bucket_off[t.c + 1]);
-        sp = re - rs >= 4 * 32 && t.chunk < 32;
+        sp = re - rs >= 2 * 32 * S && t.chunk < 32;
         if (sp)
             for (int i = 0; i < t.np; ++i) atomicOr(&mask[t.pp0 + i], 1u << t.chunk);
     }
@@ -385,25 +387,26 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
         total += wsp[v];
     }
     if (tid < k2) {
-        const int at = no + (n - k2) + tid + before;
+        const int at = no + (n - k2) + tid + before * (S - 1);
         if (!sp) {
             tout[at] = t;
         } else {
-            const int hr = (int)((re - rs) / 64) * 32;
-            const int v = C + 1 + 4 * (x * K + tid);
-            ext_off[v] = rs - (int64_t)t.chunk * chunk_rows;
-            ext_off[v + 1] = rs + hr;
-            ext_off[v + 2] = rs + hr - (int64_t)(X + t.chunk) * chunk_rows;
-            ext_off[v + 3] = re;
-            tout[at] = Tile{v, t.pp0, t.np, t.chunk};
-            tout[at + 1] = Tile{v + 2, t.pp0, t.np, X + t.chunk};
+            const int pr = (int)((re - rs) / (32 * S)) * 32;  // rows of every part but the last
+            const int v = C + 1 + 2 * S * (x * K + tid);
+            for (int p = 0; p < S; ++p) {
+                const int64_t a0 = rs + (int64_t)p * pr;
+                const int slot = p * X + t.chunk;
+                ext_off[v + 2 * p] = a0 - (int64_t)slot * chunk_rows;
+                ext_off[v + 2 * p + 1] = (p == S - 1) ? re : a0 + pr;
+                tout[at + p] = Tile{v + 2 * p, t.pp0, t.np, slot};
+            }
         }
     }
     __syncthreads();  // (every thread read meta[x] above)
     if (tid == 0) {
         meta[x] = no;
-        meta[kGroups + x] = n + total;
-        atomicAdd(&meta[2 * kGroups], total);
+        meta[kGroups + x] = n + total * (S - 1);
+        atomicAdd(&meta[2 * kGroups], total * (S - 1));
     }
 }
 
@@ -1360,7 +1363,7 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, int64_t n_rows,
-    int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask) {
+    int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask, int32_t S) {
     // one thread per pair, 64-thread blocks (spread over every CU); each
     // chunk list is read with all its loads in flight, then its global
     // positions gathered the same way, then merged into a register list
@@ -1370,15 +1373,21 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     const int c = pair_bucket[pp];
     if (c < 0) return;
     const int nch_c = chunk_first[c + 1] - chunk_first[c];
-    // (+ the second halves of tail-split chunks: slot X + j for bit j of the
-    // pair's mask, X = max_chunks / 2, the stride being 2X)
+    // (+ the other parts of tail-split chunks: slots s*X + j, s = 1..S-1, for
+    // bit j of the pair's mask, X = max_chunks / S, the stride being S*X)
     uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
-    const int nch = nch_c + __popc(sm);
+    const int nch = nch_c + (S - 1) * __popc(sm);
+    const int X = max_chunks / S;
+    int part = S;  // part of the current split chunk (S: take the next bit)
+    int bit = 0;
     auto slot_of = [&](int j) {
         if (j < nch_c) return j;
-        const int b = __builtin_ctz(sm);  // the halves in ascending chunk order
-        sm &= sm - 1u;
-        return max_chunks / 2 + b;
+        if (part == S) {
+            bit = __builtin_ctz(sm);  // split chunks in ascending order, parts 1..S-1
+            sm &= sm - 1u;
+            part = 1;
+        }
+        return (part++) * X + bit;
     };
     uint64_t M[KL];
     int32_t W[KL];
@@ -1540,10 +1549,11 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     w.tiles_tmp = take((size_t)w.max_tiles * sizeof(Tile));
     w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));
-    // (x 2: the second halves of tail-split chunks, slot max_chunks + j)
-    w.partial = take(P * (size_t)(2 * std::max(idx->max_chunks, 1)) * KL * sizeof(uint64_t));
-    w.tiles_split = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK) * sizeof(Tile));
-    w.ext_off = take(((size_t)idx->n_buckets + 1 + 4 * (size_t)kGroups * kSplitMaxK) * 8);
+    // (x S: the other parts of tail-split chunks, slot s * max_chunks + j)
+    const size_t S = (size_t)split_parts();
+    w.partial = take(P * (size_t)(S * std::max(idx->max_chunks, 1)) * KL * sizeof(uint64_t));
+    w.tiles_split = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK * (S - 1)) * sizeof(Tile));
+    w.ext_off = take(((size_t)idx->n_buckets + 1 + 2 * S * (size_t)kGroups * kSplitMaxK) * 8);
     w.split_mask = take(P * 4);
     w.thr_g = take(P * sizeof(uint64_t));
     w.pref = take(P * 4);
@@ -1557,6 +1567,10 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
 }
 
 }  // namespace
+
+int split_parts() {
+    return std::max(2, std::min(kSplitMaxParts, env_config().scan_split_parts));
+}
 
 int num_cus() {
     static int n = 0;
@@ -1867,7 +1881,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         if (do_plan)
             hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, (Tile*)(ws + w.tiles_split),
                            meta, idx->bucket_off, (int64_t*)(ws + w.ext_off), C, idx->chunk_rows,
-                           std::max(idx->max_chunks, 1), split_k, split_mask);
+                           std::max(idx->max_chunks, 1), split_k, split_parts(), split_mask);
         LMI_LAUNCH_CHECK("tail_split_kernel");
         tiles = (Tile*)(ws + w.tiles_split);
         scan_off = (const int64_t*)(ws + w.ext_off);
@@ -1879,7 +1893,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     a.inv_norm = idx->inv_norm;
     a.bucket_off = idx->bucket_off;
     a.chunk_rows = idx->chunk_rows;
-    a.max_chunks = 2 * std::max(idx->max_chunks, 1);  // the partial-list stride (+ split halves)
+    a.max_chunks = split_parts() * std::max(idx->max_chunks, 1);  // the partial-list stride (+ split parts)
     a.qbuf = ws + w.qbuf;
     a.invq = (const float*)(ws + w.invq);
     a.pair_q = pair_q;
@@ -1964,7 +1978,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
 #define LMI_CM(KLV, ROWSV)                                                                         \
     hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
                        a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo,  \
-                       out_d, out_pos, out_row, idx->n_rows, status, split_mask)
+                       out_d, out_pos, out_row, idx->n_rows, status, split_mask, split_parts())
     if (KL == 10) {
         if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
     } else if (KL == 15) {

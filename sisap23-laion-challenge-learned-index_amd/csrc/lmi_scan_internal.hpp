@@ -49,6 +49,9 @@ struct ScanArgs {
 
 // tail split: at most this many tiles per queue are halved (tail_split_kernel)
 constexpr int kSplitMaxK = 256;
+constexpr int kSplitMaxParts = 8;
+// row parts of a tail-split tile (LMI_SCAN_SPLIT_PARTS, clamped to [2, kSplitMaxParts])
+int split_parts();
 // tile groups of the persistent scans' dequeue (XCD round-robin, see
 // plan_fill_kernel in lmi_scan.hip)
 constexpr int kGroups = 8;

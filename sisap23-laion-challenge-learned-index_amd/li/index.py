@@ -1017,7 +1017,8 @@ class GraphedSearch:
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
         self.use_threshold, self.dist = use_threshold, dist
         G = ix.world
-        if k_round > _lib.LMI_MAX_K or (capture and G > 1 and
+        grouped = G > 1 and torch.distributed.is_initialized()
+        if k_round > _lib.LMI_MAX_K or (capture and grouped and
                                        torch.distributed.get_backend(s.group) != "nccl"):
             raise ValueError("graph capture needs k_round <= 16 and RCCL collectives "
                              "(capture=False runs the same step eagerly, e.g. over gloo)")
@@ -1035,7 +1036,7 @@ class GraphedSearch:
         # the batch is shared over the ranks of the process group (the index's
         # world is the stripe count; they differ only in a one-process
         # rehearsal of one stripe, tools/shard_step.py)
-        Gi = G
+        Gi = G if grouped else 1
         G = torch.distributed.get_world_size(s.group) if Gi > 1 else 1
         g = torch.distributed.get_rank(s.group) if Gi > 1 else 0
         self.per = per = -(-nq // G)
@@ -1319,7 +1320,10 @@ class StreamedSearch:
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
         self.use_threshold, self.dist = use_threshold, dist
         G = ix.world
-        self.G = torch.distributed.get_world_size(s.group) if G > 1 else 1
+        # the list exchange spans the process group's ranks (a stripe of a
+        # G-way index in a process without a group: the rank's own lists)
+        self.G = torch.distributed.get_world_size(s.group) if (
+            G > 1 and torch.distributed.is_initialized()) else 1
         if k_round > _lib.LMI_MAX_K:
             raise ValueError("the phased scan needs k_round <= 16")
         if capture and self.G > 1 and torch.distributed.get_backend(s.group) != "nccl":

@@ -1,5 +1,5 @@
-"""Tail split (tail_split_kernel, LMI_SCAN_SPLIT): the last tiles of every
-scan queue replaced by their row halves must not change a single list entry
+"""Tail split (tail_split_kernel, LMI_SCAN_SPLIT / LMI_SCAN_SPLIT_PARTS): the last
+tiles of every scan queue replaced by S row parts must not change a single list entry
 -- bitwise equal to the unsplit scan, in both arithmetics, for k <= 10, the
 float64 mode's 15-entry lists and the k > 16 lower-bound passes, and equal to
 the oracle."""
@@ -15,9 +15,10 @@ from li import index as I
 pytestmark = pytest.mark.gpu
 
 
-def _lists(ix, q, classes, k, dist, split, groups=None):
+def _lists(ix, q, classes, k, dist, split, groups=None, parts=None):
     import os
-    for var, val in (("LMI_SCAN_SPLIT", split), ("LMI_SCAN_GROUPS", groups)):
+    for var, val in (("LMI_SCAN_SPLIT", split), ("LMI_SCAN_GROUPS", groups),
+                     ("LMI_SCAN_SPLIT_PARTS", parts)):
         if val is None:
             os.environ.pop(var, None)
         else:
@@ -31,6 +32,7 @@ def _lists(ix, q, classes, k, dist, split, groups=None):
     finally:
         os.environ.pop("LMI_SCAN_SPLIT", None)
         os.environ.pop("LMI_SCAN_GROUPS", None)
+        os.environ.pop("LMI_SCAN_SPLIT_PARTS", None)
         _lib.load().lmi_config_reload()
 
 
@@ -50,6 +52,12 @@ def test_split_lists_equal_unsplit(k, dist, chunk_rows):
         d1, p1 = _lists(ix, q, classes, k, dist, split, groups)
         np.testing.assert_array_equal(p1, p0)
         np.testing.assert_array_equal(d1, d0)
+    # S row parts per split tile (3, 4, 8), default K and every tile split
+    for parts in (3, 4, 8):
+        for split in (None, 256):
+            d1, p1 = _lists(ix, q, classes, k, dist, split, None, parts)
+            np.testing.assert_array_equal(p1, p0)
+            np.testing.assert_array_equal(d1, d0)
 
 
 def test_split_search_matches_oracle():

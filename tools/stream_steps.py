@@ -1,0 +1,45 @@
+"""Rank 0's batch-stream launches (StreamedSearch) of a W-way striped 10M index on
+one GPU, for kernel traces (tools/gpu_stream_trace.sh): builds the bench workload,
+runs `--steps` launches per world and prints ms per launch."""
+import argparse, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
+import torch
+from li import synth
+from li.index import DeviceIndex, DeviceRouter, Searcher
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--worlds", default="1,8")
+ap.add_argument("--steps", type=int, default=20)
+ap.add_argument("--eager", action="store_true", help="launch the three branches eagerly on three streams")
+ap.add_argument("--modes", default="stream", help="comma list of stream, stream-eager, graph-pipe, graph")
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+import torch.distributed as dist
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1"); os.environ.setdefault("MASTER_PORT", "29534")
+dist.init_process_group("nccl", rank=0, world_size=1)   # a one-process group: rank 0 of W
+x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
+router = DeviceRouter(layers)
+labels = router.argmax(xn); del xn
+for W in map(int, a.worlds.split(",")):
+    ck = 8192 if W == 1 else 4096 if W <= 4 else 2048
+    ix = DeviceIndex(x, labels, 122, chunk_rows=ck, rank=0, world=W)
+    s = Searcher(ix, router)
+    for mode in a.modes.split(","):
+        if mode.startswith("stream"):
+            st = s.streamed(qn, q, 4, k=10, capture=not (a.eager or mode == "stream-eager"))
+            fn = st.step
+        else:
+            st = s.graph(qn, q, 4, k=10, pipeline=mode == "graph-pipe")
+            fn = st.run
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(); t0 = time.perf_counter()
+        for _ in range(a.steps):
+            fn()
+        torch.cuda.synchronize()
+        print(f"world {W} chunk {ck}: {mode} {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step "
+              f"(scan WGs {os.environ.get('LMI_SCAN_WGS', 'all CUs')})", flush=True)
+        del st, fn
+    del s, ix; torch.cuda.empty_cache()
