@@ -50,6 +50,16 @@ namespace {
 // 10k queries; round 1's 256-thread workgroup per query took 19 us, most of
 // it workgroup launch and block reductions): each lane takes runs of 4
 // consecutive elements, float4 loads when the rows allow (VEC).
+// Word fills of the plan's per-pair arrays, folded into prep (one kernel
+// launch instead of one per array): array f gets value v[f] in words
+// [row * per_q[f], (row + 1) * per_q[f]) from the wave of query `row`.
+struct PrepFills {
+    uint32_t* p[4];
+    uint32_t v[4];
+    int32_t per_q[4];
+    int32_t n;
+};
+
 template <bool F16, bool VEC>
 __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict__ q, int32_t nq,
                                                         int32_t ldq, int32_t d, int32_t d_pad,
@@ -59,7 +69,7 @@ __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict_
                                                         float* __restrict__ out_d,
                                                         int32_t* __restrict__ out_pos,
                                                         int32_t* __restrict__ out_row,
-                                                        int32_t out_per_q) {
+                                                        int32_t out_per_q, PrepFills fills) {
     const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= nq) return;  // (wave-uniform; no block-wide barrier below)
@@ -107,6 +117,9 @@ __global__ __launch_bounds__(kThreads) void prep_kernel(const float* __restrict_
         out_pos[(size_t)row * out_per_q + e] = -1;
         if (out_row) out_row[(size_t)row * out_per_q + e] = -1;
     }
+    for (int f = 0; f < fills.n; ++f)
+        for (int e = lane; e < fills.per_q[f]; e += 64)
+            fills.p[f][(size_t)row * fills.per_q[f] + e] = fills.v[f];
 }
 
 // ---------------------------------------------------------------------------
@@ -1801,6 +1814,29 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const int P = nq * R;
     const int KL = pick_kl(idx, qmode, k);
 
+    // the plan's per-pair initial values, written by prep: pair_bucket = -1
+    // (pairs whose class is out of range are never filled), pair_pos = -1 (the
+    // seed), split_mask = 0, the per-pair bounds thr_g = all ones (scan v2/v3)
+    PrepFills fills{};
+    const bool seed_plan = seed_r0 && w.use_v3 && !(lo_g != nullptr) && R > 1;
+    if (idx->n_rows > 0) {
+        auto add = [&](void* ptr, uint32_t v, int per_q) {
+            fills.p[fills.n] = reinterpret_cast<uint32_t*>(ptr);
+            fills.v[fills.n] = v;
+            fills.per_q[fills.n] = per_q;
+            ++fills.n;
+        };
+        add(ws + w.pair_bucket, 0xffffffffu, R);
+        if (seed_plan) add(ws + w.pair_pos, 0xffffffffu, R);
+        add(ws + w.split_mask, 0u, R);
+        bool reset_thr = w.use_v2 || w.use_v3;
+#ifdef LMI_ABLATION
+        // diagnostic: keep the previous call's per-pair bounds (near-final
+        // seeds when the same batch is repeated) to measure seeding quality
+        reset_thr = reset_thr && !env_config().scan_keep_thr;
+#endif
+        if (reset_thr) add(ws + w.thr_g, 0xffffffffu, 2 * R);
+    }
     if (do_plan) {
         const dim3 pg((nq + kThreads / 64 - 1) / (kThreads / 64));
         const bool vec = ((uintptr_t)q % 16 == 0) && (ldq % 4 == 0);
@@ -1808,7 +1844,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                            : (vec ? prep_kernel<false, true> : prep_kernel<false, false>);
         hipLaunchKernelGGL(kp, pg, dim3(kThreads), 0, s, q, nq, ldq, idx->d, idx->d_pad,
                            (void*)(ws + w.qbuf), (float*)(ws + w.invq), status, out_d, out_pos,
-                           out_row, prefill ? R * ldo : 0);
+                           out_row, prefill ? R * ldo : 0, fills);
         LMI_LAUNCH_CHECK("prep_kernel");
     }
     if (idx->n_rows == 0) return LMI_OK;
@@ -1823,18 +1859,16 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     int ng = clamp_knob(env_config().scan_groups, kGroups, 1, kGroups);
     while (ng & (ng - 1)) ng &= ng - 1;
 
-    // pair_bucket = -1 marks pairs whose class is out of range (never filled)
+    // (pair_bucket = -1 marks pairs whose class is out of range: never filled)
     if (do_plan) {
-        LMI_TRY(fill_u32(pair_bucket, 0xffffffffu, (size_t)P, s));
         hipLaunchKernelGGL(plan_count_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, counts);
         LMI_LAUNCH_CHECK("plan_count_kernel");
     }
     // (the seed reads the pair position of every (q, 0); pairs whose class is
     // out of range keep -1)
-    const bool seed = seed_r0 && w.use_v3 && !LOP && R > 1;
+    const bool seed = seed_plan;
     int32_t* pair_pos = seed ? (int32_t*)(ws + w.pair_pos) : nullptr;
     if (do_plan) {
-        if (seed) LMI_TRY(fill_u32(pair_pos, 0xffffffffu, (size_t)P, s));
         hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
                            idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
         LMI_LAUNCH_CHECK("plan_fill_kernel");
@@ -1871,7 +1905,6 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
 
     // tail split (scan v3): K = the queue's share of the grid
     uint32_t* split_mask = (uint32_t*)(ws + w.split_mask);
-    if (do_plan) LMI_TRY(fill_u32(split_mask, 0u, (size_t)P, s));
     // (not after the nearest-chunk-first plan: its queue has no seed count)
     const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
                         : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
@@ -1932,12 +1965,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         b.seed_margin = seed_margin;
         b.ng = ng;
         b.lag = std::max(0, std::min(3, env_config().scan_lag));
-#ifdef LMI_ABLATION
-        // diagnostic: keep the previous call's per-pair bounds (near-final
-        // seeds when the same batch is repeated) to measure seeding quality
-        if (!env_config().scan_keep_thr)
-#endif
-        if (do_plan) LMI_TRY(fill_u32(ws + w.thr_g, 0xffffffffu, (size_t)P * 2, s));
+        // (thr_g was reset by prep)
         if (!do_scan) rc = LMI_OK;
         else
         if (w.use_v3 && LOP) {
