@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
     const int32_t* __restrict__ classes, int32_t P, int32_t C, const int32_t* __restrict__ counts,
     const int32_t* __restrict__ chunk_first, int32_t QB, int32_t* __restrict__ pair_q,
     int32_t* __restrict__ pair_bucket, Tile* __restrict__ tiles, int32_t* __restrict__ meta,
-    int32_t* __restrict__ work, int32_t ng, int32_t* __restrict__ pair_pos) {
+    int32_t* __restrict__ work, int32_t ng, int32_t* __restrict__ pair_pos, int32_t qpad) {
     __shared__ int sh[kPlanThreads / 64];
     __shared__ int wcnt[kPlanThreads / 64];
     __shared__ int g0_all[kGroups], gr_all[kGroups], g0_lt[kGroups], gr_lt[kGroups];
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_fill_kernel(
     {
         int acc = 0;
         for (int x = 0; x < kGroups; ++x) {
-            goff[x] = acc;
+            goff[x] = acc + x * qpad;  // (each queue region followed by qpad free slots)
             acc += g0_all[x] + gr_all[x];
         }
         if (c == C - 1 && tid == 0) {
@@ -363,33 +363,33 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(Tile* __restrict__ til
 // chunk j writes slot s*X + j (X = max_chunks, the stride is S*X; part 0 keeps
 // chunk j's slot); bit j of mask[pp] tells the chunk merge to read slots
 // X + j .. (S-1)*X + j too (chunks j < 32 only).  Every part but the last has
-// a whole number of 32-row blocks, and at least two.
-__global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict__ tin,
-                                                         Tile* __restrict__ tout,
+// a whole number of 32-row blocks, and at least two.  In place: plan_fill left
+// K (S - 1) free slots after every queue, so only the last K tiles move.
+__global__ __launch_bounds__(256) void tail_split_kernel(Tile* __restrict__ tiles,
                                                          int32_t* __restrict__ meta,
                                                          const int64_t* __restrict__ bucket_off,
                                                          int64_t* __restrict__ ext_off, int32_t C,
                                                          int32_t chunk_rows, int32_t X, int32_t K,
                                                          int32_t S, uint32_t* __restrict__ mask) {
     __shared__ int wsp[4];
+    __shared__ int s_pp0[256], s_np[256], s_bit[256];  // the split tiles' pair blocks
     const int x = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (x == 0)
         for (int i = tid; i <= C; i += 256) ext_off[i] = bucket_off[i];
     const int o = meta[x], n = meta[kGroups + x];
     const int seeds = meta[2 * kGroups + 1 + x];
     const int k2 = max(0, min(K, n - seeds));  // the candidates: the queue's last k2 tiles
-    const int no = o + x * K * (S - 1);        // (every queue grows by at most K (S - 1))
-    for (int i = tid; i < n - k2; i += 256) tout[no + i] = tin[o + i];
     Tile t{};
     int64_t rs = 0, re = 0;
     bool sp = false;
     if (tid < k2) {
-        t = tin[o + n - k2 + tid];
+        t = tiles[o + n - k2 + tid];
         rs = bucket_off[t.c] + (int64_t)t.chunk * chunk_rows;
         re = min(rs + (int64_t)chunk_rows, bucket_off[t.c + 1]);
         sp = re - rs >= 2 * 32 * S && t.chunk < 32;
-        if (sp)
-            for (int i = 0; i < t.np; ++i) atomicOr(&mask[t.pp0 + i], 1u << t.chunk);
+        s_pp0[tid] = t.pp0;
+        s_np[tid] = sp ? t.np : 0;
+        s_bit[tid] = 1 << (t.chunk & 31);
     }
     const uint64_t m = __ballot(sp);
     if (lane == 0) wsp[w] = __popcll(m);
@@ -400,9 +400,9 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
         total += wsp[v];
     }
     if (tid < k2) {
-        const int at = no + (n - k2) + tid + before * (S - 1);
+        const int at = o + (n - k2) + tid + before * (S - 1);
         if (!sp) {
-            tout[at] = t;
+            tiles[at] = t;
         } else {
             const int pr = (int)((re - rs) / (32 * S)) * 32;  // rows of every part but the last
             const int v = C + 1 + 2 * S * (x * K + tid);
@@ -411,13 +411,16 @@ __global__ __launch_bounds__(256) void tail_split_kernel(const Tile* __restrict_
                 const int slot = p * X + t.chunk;
                 ext_off[v + 2 * p] = a0 - (int64_t)slot * chunk_rows;
                 ext_off[v + 2 * p + 1] = (p == S - 1) ? re : a0 + pr;
-                tout[at + p] = Tile{v + 2 * p, t.pp0, t.np, slot};
+                tiles[at + p] = Tile{v + 2 * p, t.pp0, t.np, slot};
             }
         }
     }
+    // the pairs of every split tile: bit chunk of their mask (the whole
+    // workgroup per tile, fire-and-forget atomics)
+    for (int i = 0; i < k2; ++i)
+        for (int e = tid; e < s_np[i]; e += 256) atomicOr(&mask[s_pp0[i] + e], (uint32_t)s_bit[i]);
     __syncthreads();  // (every thread read meta[x] above)
     if (tid == 0) {
-        meta[x] = no;
         meta[kGroups + x] = n + total * (S - 1);
         atomicAdd(&meta[2 * kGroups], total * (S - 1));
     }
@@ -1502,7 +1505,7 @@ struct WsLayout {
     size_t qbuf, invq, counts, pair_q, pair_bucket, tiles, tiles_tmp, ntiles, work, partial, thr_g, pref,
         pref_tmp, pref_tmp2, n_seed, total;
     int32_t max_tiles;
-    size_t tiles_split, ext_off, split_mask;  // tail split (scan v3)
+    size_t ext_off, split_mask;  // tail split (scan v3)
     size_t pair_pos;  // LMI_Q_SEED_ROUND0: grouped position of every pair id
     size_t seed_pos;  //   and of every grouped pair's (q, 0)
     int32_t qb;      // queries per tile
@@ -1558,14 +1561,14 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     // tiles <= sum_c nch_c * ceil(cnt_c/QB) <= sum_c nch_c * (cnt_c/QB + 1)
     const size_t mt = (P / QB + 1) * (size_t)std::max(idx->max_chunks, 1) + (size_t)idx->n_chunks;
     w.max_tiles = (int32_t)std::min<size_t>(mt, (size_t)INT32_MAX);
-    w.tiles = take((size_t)w.max_tiles * sizeof(Tile));
+    // (+ K (S - 1) free slots after every queue: the tail split's parts, in place)
+    const size_t S = (size_t)split_parts();
+    w.tiles = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK * (S - 1)) * sizeof(Tile));
     w.tiles_tmp = take((size_t)w.max_tiles * sizeof(Tile));
     w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));
     // (x S: the other parts of tail-split chunks, slot s * max_chunks + j)
-    const size_t S = (size_t)split_parts();
     w.partial = take(P * (size_t)(S * std::max(idx->max_chunks, 1)) * KL * sizeof(uint64_t));
-    w.tiles_split = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK * (S - 1)) * sizeof(Tile));
     w.ext_off = take(((size_t)idx->n_buckets + 1 + 2 * S * (size_t)kGroups * kSplitMaxK) * 8);
     w.split_mask = take(P * 4);
     w.thr_g = take(P * sizeof(uint64_t));
@@ -1868,9 +1871,17 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     // out of range keep -1)
     const bool seed = seed_plan;
     int32_t* pair_pos = seed ? (int32_t*)(ws + w.pair_pos) : nullptr;
+    const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
+    // tail split (scan v3): K = the queue's share of the grid; plan_fill leaves
+    // K (S - 1) free slots after every queue for its parts
+    const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
+                        : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
+                                                                            : (num_cus() + ng - 1) / ng);
+    const int qpad = split_k * (split_parts() - 1);
     if (do_plan) {
         hipLaunchKernelGGL(plan_fill_kernel, dim3(C), dim3(kPlanThreads), 0, s, classes, P, C, counts,
-                           idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos);
+                           idx->chunk_first, QB, pair_q, pair_bucket, tiles, meta, work, ng, pair_pos,
+                           qpad);
         LMI_LAUNCH_CHECK("plan_fill_kernel");
     }
     int32_t* seed_pos = seed ? (int32_t*)(ws + w.seed_pos) : nullptr;
@@ -1879,7 +1890,6 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                            P, R, seed_pos);
         LMI_LAUNCH_CHECK("seed_pos_kernel");
     }
-    const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
     if (do_plan && !nearest_first && env_config().scan_order != 0) {
         hipLaunchKernelGGL(tile_order_kernel, dim3(ng), dim3(1024), 0, s, tiles, (Tile*)(ws + w.tiles_tmp),
                            meta, idx->bucket_off, idx->chunk_rows, QB, counts,
@@ -1903,20 +1913,16 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     }
     if (nearest_first) ng = 1;  // one queue: seed tiles strictly first
 
-    // tail split (scan v3): K = the queue's share of the grid
+    // tail split (scan v3; not after the nearest-chunk-first plan: its queue
+    // has no seed count)
     uint32_t* split_mask = (uint32_t*)(ws + w.split_mask);
-    // (not after the nearest-chunk-first plan: its queue has no seed count)
-    const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
-                        : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
-                                                                            : (num_cus() + ng - 1) / ng);
     const int64_t* scan_off = idx->bucket_off;
     if (split_k > 0) {
         if (do_plan)
-            hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, (Tile*)(ws + w.tiles_split),
-                           meta, idx->bucket_off, (int64_t*)(ws + w.ext_off), C, idx->chunk_rows,
-                           std::max(idx->max_chunks, 1), split_k, split_parts(), split_mask);
+            hipLaunchKernelGGL(tail_split_kernel, dim3(kGroups), dim3(256), 0, s, tiles, meta,
+                               idx->bucket_off, (int64_t*)(ws + w.ext_off), C, idx->chunk_rows,
+                               std::max(idx->max_chunks, 1), split_k, split_parts(), split_mask);
         LMI_LAUNCH_CHECK("tail_split_kernel");
-        tiles = (Tile*)(ws + w.tiles_split);
         scan_off = (const int64_t*)(ws + w.ext_off);
     }
 
