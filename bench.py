@@ -290,7 +290,9 @@ STEP_TEXT = {
                          "; each batch passes every stage, the timed launches answer one batch each"),
     "graph": lambda a: ("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
                         "copy stream during the previous step's search (double-buffered), + search + D2H "
-                        "of the answer" if not a.no_pipeline else
+                        "of the answer" + ("; the next step is launched before this one's answer is "
+                                           "read (one launch ahead)" if a.one_ahead else "")
+                        if not a.no_pipeline else
                         "hip-graph replay (H2D of the host batch + search + D2H of the answer)"),
     "eager": lambda a: "eager launches (H2D of the host batch + search + D2H)",
 }
@@ -396,6 +398,9 @@ def main():
                          "merge/replay/D2H of b in one launch of three captured branches) instead of "
                          "the per-batch step graph with the upload pipelined (the default; measured "
                          "equal at G = 1 and faster at G = 8, DESIGN.md §5)")
+    ap.add_argument("--one-ahead", action="store_true",
+                    help="launch each step before reading the previous step's answer "
+                         "(GraphedSearch.launch / result; measured no faster, DESIGN.md §5)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="upload each batch inside its own step instead of during the previous "
                          "step's search (GraphedSearch(pipeline=True), the default)")
@@ -493,15 +498,30 @@ def main():
             del gs
             return timed_eager(dist)
         h2d = h2d_ms(gs.h_blk[gs.rank_in_group], gs.d_blk) + (gs.upload_bytes(),)
-        out = None
-        for _ in range(args.warmup):
-            out = gs.run()
+        one_ahead = gs.pipeline and args.one_ahead
+
+        def steps(n):
+            # pipelined: the next step is launched before this one's answer is
+            # read (GraphedSearch.launch / result), so the host's synchronise-
+            # to-launch gap overlaps the GPU work; n launches, n answers read
+            if not one_ahead:
+                o = None
+                for _ in range(n):
+                    o = gs.run()
+                return o
+            o, t = None, gs.launch()
+            for i in range(n):
+                t2 = gs.launch() if i + 1 < n else None
+                o = gs.result(t)
+                t = t2
+            return o
+
+        out = steps(args.warmup) if args.warmup else None
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = gs.run()
+        out = steps(args.steps)
         torch.cuda.synchronize()
         if world > 1:
             torch.distributed.barrier()

@@ -1157,13 +1157,17 @@ class GraphedSearch:
                 raise RuntimeError(f"graph warm-up failed on some rank: {err!r}")
         elif err is not None:
             raise err
-        self.h = torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
+        # one pinned answer buffer per graph: with launch() / result() a graph
+        # may run while the host reads the other's answer
+        self.hs = [torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
+                   for _ in range(2 if self.pipeline else 1)]
+        self.h = self.hs[0]
         self.graphs, self._keep = [], []
         for slot in range(2 if self.pipeline else 1):
             gr = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gr):
                 buf = step(slot)
-                self.h.copy_(buf, non_blocking=True)
+                self.hs[slot].copy_(buf, non_blocking=True)
             self.graphs.append(gr)
             self._keep.append(buf)
         self.graph = self.graphs[0]
@@ -1225,7 +1229,7 @@ class GraphedSearch:
             if not self.stage(q_nav, q_search):
                 return self._eager(q_nav, q_search)
         if self.pipeline:
-            self._run_pipelined(dev)
+            return self.result(self.launch())
         elif self.graph is not None:
             self.graph.replay()
         else:
@@ -1234,10 +1238,35 @@ class GraphedSearch:
             _wait_with_deadline(dev, self.timeout_s)
         else:
             torch.cuda.current_stream(dev).synchronize()
-        hd, ha, st, rst = answer_views(self.h, self.nq, self.w)
+        return self._answer(self.h)
+
+    def _answer(self, h):
+        hd, ha, st, rst = answer_views(h, self.nq, self.w)
         if st & _lib.LMI_STATUS_INTERNAL or rst:
             raise RuntimeError(f"search: internal status {st}/{rst}")
         return hd, ha
+
+    def launch(self) -> int:
+        """pipeline=True: enqueue one step on the staged batch without waiting
+        for it (the next batch's upload starts beside it); returns a ticket for
+        result().  Keeping one launch ahead of result() hides the host's
+        synchronise-to-launch gap between steps (at most two in flight: a
+        ticket's answer is valid until the launch after next)."""
+        if not self.pipeline:
+            raise ValueError("launch() needs GraphedSearch(pipeline=True)")
+        slot = self._slot
+        self._run_pipelined(self.searcher.index.device)
+        return slot
+
+    def result(self, ticket: int):
+        """Wait for the step of `ticket` (from launch()) -> (dists f64 [nq, w],
+        anns uint32 [nq, w]): numpy views of that step's pinned answer."""
+        ev = self._done_ev[ticket]
+        if self.G > 1:
+            _wait_event_with_deadline(ev, self.timeout_s)
+        else:
+            ev.synchronize()
+        return self._answer(self.hs[ticket])
 
     def _upload(self, slot):
         """The staged block into d_blks[slot] on the copy stream, once the
@@ -1547,6 +1576,19 @@ class StreamedSearch:
         self._scan(js); self._finish(js); sync()
         yield tuple(a.copy() for a in self._answer(js))
         self._t = None
+
+
+def _wait_event_with_deadline(ev, timeout_s: float) -> None:
+    """_wait_with_deadline on a recorded event."""
+    deadline = time.monotonic() + timeout_s
+    spins = 0
+    while not ev.query():
+        spins += 1
+        if spins > 1000:
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"search step not finished after {timeout_s:.0f} s: a peer rank "
+                                   "stopped inside the step's collectives; end this process")
+            time.sleep(1e-4)
 
 
 def _wait_with_deadline(dev, timeout_s: float) -> None:

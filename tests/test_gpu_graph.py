@@ -149,3 +149,32 @@ def test_graph_replays_survive_eager_work_between(setup, pipeline):
     d2, a2 = g.run(qn2, q2)
     np.testing.assert_array_equal(d2, e0)
     np.testing.assert_array_equal(a2, b0)
+
+
+def test_launch_one_ahead_answers_each_batch(setup):
+    """GraphedSearch(pipeline=True).launch / result: a step launched before the
+    previous one's answer is read; every answer equals the eager search of the
+    batch staged for it, across a restaged batch."""
+    w, s = setup
+    T = lambda a: torch.from_numpy(a).cuda()
+    perm = np.random.default_rng(7).permutation(w["q"].shape[0])
+    qn2, q2 = w["qn"][perm], w["q"][perm]
+    d0, a0 = s.search(T(w["qn"]), T(w["q"]), 4, k=10)
+    e0, b0 = s.search(T(qn2), T(q2), 4, k=10)
+    g = s.graph(w["qn"], w["q"], 4, k=10, pipeline=True)
+    t = g.launch()
+    for _ in range(5):
+        t2 = g.launch()
+        d, a = g.result(t)
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+        t = t2
+    d, a = g.result(t)
+    np.testing.assert_array_equal(a, a0)
+    assert g.stage(qn2, q2)
+    t = g.launch()
+    t2 = g.launch()
+    for tk in (t, t2):
+        d, a = g.result(tk)
+        np.testing.assert_array_equal(d, e0)
+        np.testing.assert_array_equal(a, b0)
