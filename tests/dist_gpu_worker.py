@@ -46,6 +46,14 @@ def main(out_path):
         g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_, capture=False)
         d, a = g.run()
         res[f"graph_{dist_}_d"], res[f"graph_{dist_}_a"] = d.copy(), a.copy()
+    # the batch stream's G > 1 path (every rank uploads and routes the whole
+    # batch; the list exchange in the finish branch), its branches launched
+    # eagerly over gloo: three distinct batches
+    perms = [np.random.default_rng(70 + i).permutation(w["q"].shape[0]) for i in range(3)]
+    for dist_ in ("f32", "f64"):
+        st = s.streamed(w["qn"], w["q"], 4, k=10, dist=dist_, capture=False)
+        for i, (d, a) in enumerate(st.stream([(w["qn"][p], w["q"][p]) for p in perms])):
+            res[f"stream_{dist_}_{i}_d"], res[f"stream_{dist_}_{i}_a"] = d, a
     if rank == 0:
         np.savez(out_path, **res)
     dist.barrier()

@@ -64,3 +64,10 @@ def test_two_process_product_path_equals_one_process(world, tmp_path):
         d, a = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_).run()
         np.testing.assert_array_equal(got[f"graph_{dist_}_d"], d)
         np.testing.assert_array_equal(got[f"graph_{dist_}_a"], a)
+    perms = [np.random.default_rng(70 + i).permutation(w["q"].shape[0]) for i in range(3)]
+    for dist_ in ("f32", "f64"):
+        for i, p in enumerate(perms):
+            d, a = s.search(torch.from_numpy(w["qn"][p]).cuda(), torch.from_numpy(w["q"][p]).cuda(),
+                            4, k=10, dist=dist_)
+            np.testing.assert_array_equal(got[f"stream_{dist_}_{i}_d"], d)
+            np.testing.assert_array_equal(got[f"stream_{dist_}_{i}_a"], a)
