@@ -284,10 +284,11 @@ def h2d_ms(src, dst, reps=10):
 
 
 STEP_TEXT = {
-    "stream": lambda a: ("batch stream (StreamedSearch): one launch of three captured branches per "
-                         "batch -- H2D + router + plan of batch b+2, the scan of b+1, chunk merge + "
-                         "replay + D2H of the answer of b" + (" (+ all-gather + K3)" if a.gpus > 1 else "") +
-                         "; each batch passes every stage, the timed launches answer one batch each"),
+    "stream": lambda a: ("batch stream (StreamedSearch): per launch, on four streams -- the H2D of "
+                         "batch b+2 (copy engine) then its router + plan, the scan of b+1, the chunk "
+                         "merge" + (" + all-gather + K3" if a.gpus > 1 else "") + " + replay + D2H of "
+                         "the answer of b (each a captured graph); every batch passes every stage, "
+                         "each timed launch answers one batch"),
     "graph": lambda a: ("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
                         "copy stream during the previous step's search (double-buffered), + search + D2H "
                         "of the answer" + ("; the next step is launched before this one's answer is "
@@ -393,11 +394,11 @@ def main():
     ap.add_argument("--parity-sample", type=int, default=64,
                     help="queries whose lists are checked against a float64 brute force")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--stream", action="store_true",
-                    help="time the batch stream (StreamedSearch: plan of batch b+2, scan of b+1 and "
-                         "merge/replay/D2H of b in one launch of three captured branches) instead of "
-                         "the per-batch step graph with the upload pipelined (the default; measured "
-                         "equal at G = 1 and faster at G = 8, DESIGN.md §5)")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="time the per-batch step graph (GraphedSearch, the upload pipelined on a "
+                         "copy stream) instead of the batch stream (StreamedSearch, the default: the "
+                         "H2D + plan of batch b+2, the scan of b+1 and the merge/replay/D2H of b per "
+                         "launch on four streams; DESIGN.md §5)")
     ap.add_argument("--one-ahead", action="store_true",
                     help="launch each step before reading the previous step's answer "
                          "(GraphedSearch.launch / result; measured no faster, DESIGN.md §5)")
@@ -439,7 +440,7 @@ def main():
     q_h = q.cpu().numpy()
     q16_exact = index.storage == "f16" and bool(np.array_equal(q_h.astype(np.float16).astype(np.float32), q_h))
     # the batch stream takes fp16-exact batches on an fp16 index (the phased scan)
-    use_stream = use_graph and args.stream and q16_exact
+    use_stream = use_graph and not args.no_stream and q16_exact
     qn_pin = torch.from_numpy(qn_h).pin_memory()
     q_pin = torch.from_numpy(q_h.astype(np.float16) if q16_exact else q_h).pin_memory()
     checks = {}

@@ -1401,10 +1401,14 @@ class StreamedSearch:
             scan_fn(ix, self.q32[j], self.cls[j], kl, qmode=_lib.LMI_Q_F16, out=(dl, pl, st),
                     ws=self.ws[j], seed_round0=seed, phases=ph)
 
+        def upload(j):
+            self.d_blk[j].copy_(self.h_stage[j], non_blocking=True)
+
         def plan(j):
+            # (the staged rows are in d_blk[j]: upload(j) ran before, on the
+            # copy stream in a launch)
             self.lists[j][2].zero_()
             blk = self.d_blk[j]
-            blk.copy_(self.h_stage[j], non_blocking=True)
             s.router.topr(blk[:nq * dn].view(torch.float32).view(nq, dn), R, out=self.cls[j])
             self.q32[j].copy_(blk[nq * dn:].view(torch.float16).view(nq, d))
             phase(j, _lib.LMI_Q_PHASE_PLAN)
@@ -1427,25 +1431,14 @@ class StreamedSearch:
                           pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]))
             self.h_ans[j].copy_(buf, non_blocking=True)
 
-        self._plan, self._scan, self._finish = plan, scan, finish
-        self._side = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-
-        def launch_body(g):
-            # S first (the persistent scan takes the CUs first; P and F fill in
-            # beside it and in its tail), then P and F on forked streams
-            main = torch.cuda.current_stream(dev)
-            b1, b2 = self._side
-            b1.wait_stream(main)
-            b2.wait_stream(main)
-            scan((g + 2) % NS)
-            with torch.cuda.stream(b1):
-                plan(g)
-            with torch.cuda.stream(b2):
-                finish((g + 1) % NS)
-            main.wait_stream(b1)
-            main.wait_stream(b2)
-
-        self._body = launch_body
+        self._upload, self._plan, self._scan, self._finish = upload, plan, scan, finish
+        # four streams: uploads (the copy engine), plan, scan (the caller's
+        # stream), finish; per-slot events order them across launches
+        self._cs = torch.cuda.Stream(dev)
+        self._ps = torch.cuda.Stream(dev)
+        self._fs = torch.cuda.Stream(dev)
+        ev = lambda: [torch.cuda.Event() for _ in range(NS)]
+        self._up, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev()
         self.graphs = None
         self._t = None  # launch counter once primed
         if not self.stage(nav, qs):
@@ -1460,6 +1453,7 @@ class StreamedSearch:
         try:
             with torch.cuda.stream(side):
                 for j in range(NS):
+                    upload(j)
                     plan(j)
                     scan(j)
                     finish(j)
@@ -1475,12 +1469,14 @@ class StreamedSearch:
         elif err is not None:
             raise err
         if capture:
-            self.graphs = []
-            for g in range(NS):
-                gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr):
-                    launch_body(g)
-                self.graphs.append(gr)
+            # one graph per (branch, slot): plan, scan and finish each a chain
+            self.graphs = {}
+            for name, fn in (("P", plan), ("S", scan), ("F", finish)):
+                for j in range(NS):
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr):
+                        fn(j)
+                    self.graphs[name, j] = gr
             torch.cuda.synchronize(dev)
 
     def stage(self, q_nav, q_search, slot: Optional[int] = None) -> bool:
@@ -1508,33 +1504,66 @@ class StreamedSearch:
 
     def prime(self):
         """Fill the pipeline with the staged rows of slots 1 and 2 (eagerly:
-        plan + scan of slot 1, plan of slot 2): the next launch answers slot 1."""
+        upload + plan + scan of slot 1, upload + plan of slot 2): the next
+        launch answers slot 1."""
         dev = self.searcher.index.device
+        self._upload(1)
         self._plan(1)
         self._scan(1)
+        self._upload(2)
         self._plan(2)
         torch.cuda.current_stream(dev).synchronize()
         self._t = 0
 
+    def _run(self, name, j):
+        if self.graphs is not None:
+            self.graphs[name, j].replay()
+        else:
+            {"P": self._plan, "S": self._scan, "F": self._finish}[name](j)
+
     def step(self):
         """One launch -> (dists f64 [nq, w], anns uint32 [nq, w]) of the batch
-        it finished (numpy views, valid for the next two launches).  Plans the
-        rows staged in slot t mod 3 (stage() before step() to stream a new
-        batch; without it the slot's previous rows are planned again)."""
+        it finished (numpy views, valid for the next two launches).  Uploads and
+        plans the rows staged in slot t mod 3 (stage() before step() to stream a
+        new batch; without it the slot's previous rows are planned again),
+        scans slot t+2 and finishes slot t+1 (mod 3), on four streams:
+
+            copy:   H2D of slot P                       (the copy engine)
+            plan:   wait H2D(P) -> router, plan (P)
+            scan:   wait plan(S, last launch) -> scan (S)
+            finish: wait scan(F, last launch) -> merge, replay, D2H (F)
+
+        The scan holds every CU while it runs; the plan and finish chains, both
+        latency-bound, then run side by side instead of one after the other."""
         if self._t is None:
             self.prime()
         dev = self.searcher.index.device
-        g = self._t % self.NS
-        if self.graphs is not None:
-            self.graphs[g].replay()
-        else:
-            self._body(g)
+        NS = self.NS
+        g = self._t % NS
+        jp, js, jf = g, (g + 2) % NS, (g + 1) % NS
+        main = torch.cuda.current_stream(dev)
+        # (d_blk[jp] was last read by the plan three launches ago, which the
+        # finish the host waited for in the last step depended on)
+        with torch.cuda.stream(self._cs):
+            self._upload(jp)
+        self._up[jp].record(self._cs)
+        main.wait_event(self._pdone[js])
+        self._run("S", js)
+        self._sdone[js].record(main)
+        self._ps.wait_event(self._up[jp])
+        with torch.cuda.stream(self._ps):
+            self._run("P", jp)
+        self._pdone[jp].record(self._ps)
+        self._fs.wait_event(self._sdone[jf])
+        with torch.cuda.stream(self._fs):
+            self._run("F", jf)
+        self._fdone[jf].record(self._fs)
         self._t += 1
         if self.G > 1 and self.graphs is not None:
-            _wait_with_deadline(dev, self.timeout_s)
+            _wait_event_with_deadline(self._fdone[jf], self.timeout_s)
         else:
-            torch.cuda.current_stream(dev).synchronize()
-        return self._answer((g + 1) % self.NS)
+            self._fdone[jf].synchronize()
+        return self._answer(jf)
 
     def _answer(self, j):
         hd, ha, st, rst = answer_views(self.h_ans[j], self.nq, self.w)
@@ -1559,7 +1588,7 @@ class StreamedSearch:
                 raise ValueError("the batch stream needs fp16-exact query batches")
         if len(first) < 2:
             for j in (1, 2)[:len(first)]:
-                self._plan(j); self._scan(j); self._finish(j); sync()
+                self._upload(j); self._plan(j); self._scan(j); self._finish(j); sync()
                 yield tuple(a.copy() for a in self._answer(j))
             return
         self.prime()
@@ -1569,6 +1598,7 @@ class StreamedSearch:
             yield tuple(a.copy() for a in self.step())
         # drain: slot (t+1)%3 holds the scanned last-but-one batch, slot
         # (t+2)%3 the planned last one (launch t-1 planned it)
+        torch.cuda.synchronize(dev)  # (every stream of the last launch)
         t = self._t
         jf, js = (t + 1) % self.NS, (t + 2) % self.NS
         self._finish(jf); sync()
