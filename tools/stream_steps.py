@@ -13,6 +13,7 @@ ap.add_argument("--worlds", default="1,8")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--eager", action="store_true", help="launch the three branches eagerly on three streams")
 ap.add_argument("--modes", default="stream", help="comma list of stream, stream-eager, graph-pipe, graph")
+ap.add_argument("--chunks", default="", help="comma list of chunk rows to try (default: the bench's by W)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -22,8 +23,9 @@ dist.init_process_group("nccl", rank=0, world_size=1)   # a one-process group: r
 x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
 router = DeviceRouter(layers)
 labels = router.argmax(xn); del xn
-for W in map(int, a.worlds.split(",")):
-    ck = 8192 if W == 1 else 4096 if W <= 4 else 2048
+for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
+              for ck in (list(map(int, a.chunks.split(","))) if a.chunks else
+                         [8192 if W == 1 else 4096 if W <= 4 else 2048])]:
     ix = DeviceIndex(x, labels, 122, chunk_rows=ck, rank=0, world=W)
     s = Searcher(ix, router)
     for mode in a.modes.split(","):
