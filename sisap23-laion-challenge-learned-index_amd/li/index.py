@@ -1341,7 +1341,7 @@ class StreamedSearch:
 
     def __init__(self, searcher: "Searcher", q_nav, q_search, R: int, k: int = 10, *,
                  k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True):
+                 capture: bool = True, lookahead: bool = True):
         s = searcher
         ix = s.index
         dev = ix.device
@@ -1441,6 +1441,8 @@ class StreamedSearch:
         self._up, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev()
         self.graphs = None
         self._t = None  # launch counter once primed
+        self.lookahead = bool(lookahead)
+        self._s_ahead = False  # the next launch's scan is already enqueued
         if not self.stage(nav, qs):
             raise ValueError("the batch stream needs fp16-exact query batches")
         for j in range(NS):
@@ -1514,6 +1516,7 @@ class StreamedSearch:
         self._plan(2)
         torch.cuda.current_stream(dev).synchronize()
         self._t = 0
+        self._s_ahead = False
 
     def _run(self, name, j):
         if self.graphs is not None:
@@ -1534,7 +1537,10 @@ class StreamedSearch:
             finish: wait scan(F, last launch) -> merge, replay, D2H (F)
 
         The scan holds every CU while it runs; the plan and finish chains, both
-        latency-bound, then run side by side instead of one after the other."""
+        latency-bound, then run side by side instead of one after the other.
+        With `lookahead` the next launch's scan (of the slot planned here) is
+        enqueued too, behind this plan: it starts when the plan is done, not
+        when the host has read this launch's answer."""
         if self._t is None:
             self.prime()
         dev = self.searcher.index.device
@@ -1547,9 +1553,10 @@ class StreamedSearch:
         with torch.cuda.stream(self._cs):
             self._upload(jp)
         self._up[jp].record(self._cs)
-        main.wait_event(self._pdone[js])
-        self._run("S", js)
-        self._sdone[js].record(main)
+        if not self._s_ahead:
+            main.wait_event(self._pdone[js])
+            self._run("S", js)
+            self._sdone[js].record(main)
         self._ps.wait_event(self._up[jp])
         with torch.cuda.stream(self._ps):
             self._run("P", jp)
@@ -1558,6 +1565,12 @@ class StreamedSearch:
         with torch.cuda.stream(self._fs):
             self._run("F", jf)
         self._fdone[jf].record(self._fs)
+        if self.lookahead:
+            # the next launch's scan: slot jp, once its plan is done
+            main.wait_event(self._pdone[jp])
+            self._run("S", jp)
+            self._sdone[jp].record(main)
+        self._s_ahead = self.lookahead
         self._t += 1
         if self.G > 1 and self.graphs is not None:
             _wait_event_with_deadline(self._fdone[jf], self.timeout_s)
@@ -1603,9 +1616,12 @@ class StreamedSearch:
         jf, js = (t + 1) % self.NS, (t + 2) % self.NS
         self._finish(jf); sync()
         yield tuple(a.copy() for a in self._answer(jf))
-        self._scan(js); self._finish(js); sync()
+        if not self._s_ahead:  # (with lookahead the last launch enqueued it)
+            self._scan(js)
+        self._finish(js); sync()
         yield tuple(a.copy() for a in self._answer(js))
         self._t = None
+        self._s_ahead = False
 
 
 def _wait_event_with_deadline(ev, timeout_s: float) -> None:

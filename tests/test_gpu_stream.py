@@ -98,3 +98,22 @@ def test_stream_rejects_inexact_batches(setup):
     assert not st.stage(w["qn"], w["q"] + np.float32(1e-5))
     with pytest.raises(ValueError):
         s.streamed(w["qn"], w["q"] + np.float32(1e-5), 4, k=10)
+
+
+@pytest.mark.parametrize("lookahead", [False, True])
+def test_stream_with_and_without_lookahead(setup, lookahead):
+    """The next launch's scan enqueued ahead (the default) or not: the same
+    answers, batch by batch, and over repeated steps."""
+    w, s = setup
+    bs = _batches(w, 5, seed=40)
+    ref = [s.search(T(a), T(b), 4, k=10) for a, b in bs]
+    st = s.streamed(w["qn"], w["q"], 4, k=10, lookahead=lookahead)
+    got = list(st.stream(bs))
+    for (d, a), (d0, a0) in zip(got, ref):
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+    d0, a0 = s.search(T(w["qn"]), T(w["q"]), 4, k=10)
+    st = s.streamed(w["qn"], w["q"], 4, k=10, lookahead=lookahead)
+    for _ in range(4):
+        d, a = st.step()
+        np.testing.assert_array_equal(a, a0)
