@@ -284,11 +284,11 @@ def h2d_ms(src, dst, reps=10):
 
 
 STEP_TEXT = {
-    "stream": lambda a: ("batch stream (StreamedSearch): per launch, on four streams -- the H2D of "
-                         "batch b+2 (copy engine) then its router + plan, the scan of b+1, the chunk "
-                         "merge" + (" + all-gather + K3" if a.gpus > 1 else "") + " + replay + D2H of "
-                         "the answer of b (each a captured graph); every batch passes every stage, "
-                         "each timed launch answers one batch"),
+    "stream": lambda a: ("batch stream (StreamedSearch): per launch, on five streams -- the H2D of "
+                         "batch b+3 (copy engine) then its router, the plan of b+2, the scan of b+1, "
+                         "the chunk merge" + (" + all-gather + K3" if a.gpus > 1 else "") + " + replay "
+                         "+ D2H of the answer of b (each a captured graph); every batch passes every "
+                         "stage, each timed launch answers one batch"),
     "graph": lambda a: ("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
                         "copy stream during the previous step's search (double-buffered), + search + D2H "
                         "of the answer" + ("; the next step is launched before this one's answer is "
@@ -627,9 +627,9 @@ def main():
 
     el, scan_ms, (dists, anns), h2d = timed(args.dist)
     ms_step = el / args.steps * 1e3
-    # submission to answer: a streamed batch is answered by the third launch
-    # that sees it (plan, scan, merge/replay), a graph-step batch by its own
-    lat_ms = ms_step * (3 if step_mode.get(args.dist) == "stream" else 1)
+    # submission to answer: a streamed batch is answered by the fourth launch
+    # that sees it (route, plan, scan, merge/replay), a graph-step batch by its own
+    lat_ms = ms_step * (4 if step_mode.get(args.dist) == "stream" else 1)
     value = args.nq / (el / args.steps)
     # the other arithmetic, timed the same way (float64: the reference's on
     # float16 data, e.g. the real clip768 'emb'; float32: on float32 data)

@@ -795,7 +795,7 @@ class Searcher:
         return t
 
     def streamed(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "StreamedSearch":
-        """The step as a three-stage pipeline of captured graphs over a stream
+        """The step as a four-stage pipeline of captured graphs over a stream
         of batches (StreamedSearch); answers equal search(...) per batch."""
         return StreamedSearch(self, q_nav, q_search, R, k, **kw)
 
@@ -1306,42 +1306,42 @@ class GraphedSearch:
 
 
 class StreamedSearch:
-    """A stream of query batches through the step as a three-stage pipeline of
-    captured HIP graphs ("Batch stream").  Every launch runs three
-    independent branches, each on its own slot of device buffers:
+    """A stream of query batches through the step as a four-stage pipeline
+    ("The batch stream"):
 
-        P  batch b+2: H2D of its staged host rows -> router (K1) -> plan
-           (lmi_bucket_topk, PLAN phase: query fragments and norms, the tile
-           plan, the seed map, the tail split, the bound reset)
-        S  batch b+1: the scan kernel (SCAN phase)
-        F  batch b:   chunk merge (MERGE phase; + the float64 refinement)
+        R  batch b+3: H2D of its staged host rows (copy engine) -> router (K1)
+        P  batch b+2: the queries widened, K2's PLAN phase (fragments and
+           norms, the tile plan, the seed map, the tail split, the bounds)
+        S  batch b+1: K2's SCAN phase
+        F  batch b:   K2's MERGE phase (+ the float64 refinement)
            [-> all-gather + K3 at G > 1] -> replay (K4) -> D2H of the answer
 
-    so one batch's scan runs while the batch before it is merged, replayed and
-    copied out and the batch after it is uploaded, routed and planned: the
-    latency-bound kernels fill the scan's tail instead of following it.  Every
-    batch passes through every stage (the same kernels as Searcher.search), so
-    each answer equals Searcher.search of its batch bit for bit; a launch
-    answers the batch submitted two launches earlier.
+    One launch (`step`) runs the four stages on five streams, each stage a
+    captured graph per slot, ordered across launches by per-slot events, and
+    returns the answer of the batch it finished.  The persistent scan holds
+    every CU while it runs, so the latency-bound R, P and F chains start in
+    its tail and run side by side; the next scan waits only for P.  Every
+    batch passes every stage (the same kernels as Searcher.search), so each
+    answer equals Searcher.search of its batch bit for bit; a launch answers
+    the batch submitted three launches earlier.
 
-    Three slots of per-batch device state (staged rows, classes, scan
-    workspace, lists, answer) rotate over the launches: launch t runs graph
-    t mod 3 with P on slot t mod 3, S on slot (t+2) mod 3 and F on slot
-    (t+1) mod 3.  A graph is launched only when its S and F slots hold a
-    planned / scanned batch (the fill and drain run the same branch functions
-    eagerly), so no kernel ever reads an unplanned workspace.
+    Four slots of per-batch device state (staged rows, classes, scan
+    workspace, lists, answer) rotate over the launches: launch t routes slot
+    t mod 4, plans t+3, scans t+2 and finishes t+1 (mod 4).  A stage runs only
+    on a slot whose earlier stages ran (the fill and drain run the same stage
+    functions eagerly), so no kernel reads an unplanned workspace.
 
-    G > 1: every rank uploads and routes the whole batch in P (no collective
-    there, and P is off the critical path); the one collective, the list
-    exchange, runs in F as in Searcher.search.  fp16 index and fp16-exact
-    query batches only (the phased scan is the fp16 scan); other batches go
-    through GraphedSearch / Searcher.search."""
+    G > 1: every rank uploads and routes the whole batch (no collective in R
+    or P, both off the critical path); the one collective, the list exchange,
+    runs in F as in Searcher.search.  fp16 index and fp16-exact query batches
+    only (the phased scan is the fp16 scan); other batches go through
+    GraphedSearch / Searcher.search."""
 
-    NS = 3
+    NS = 4
 
     def __init__(self, searcher: "Searcher", q_nav, q_search, R: int, k: int = 10, *,
                  k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True, lookahead: bool = True):
+                 capture: bool = True, lookahead: Optional[bool] = None):
         s = searcher
         ix = s.index
         dev = ix.device
@@ -1404,13 +1404,15 @@ class StreamedSearch:
         def upload(j):
             self.d_blk[j].copy_(self.h_stage[j], non_blocking=True)
 
-        def plan(j):
+        def route(j):
             # (the staged rows are in d_blk[j]: upload(j) ran before, on the
             # copy stream in a launch)
-            self.lists[j][2].zero_()
             blk = self.d_blk[j]
             s.router.topr(blk[:nq * dn].view(torch.float32).view(nq, dn), R, out=self.cls[j])
-            self.q32[j].copy_(blk[nq * dn:].view(torch.float16).view(nq, d))
+
+        def plan(j):
+            self.lists[j][2].zero_()
+            self.q32[j].copy_(self.d_blk[j][nq * dn:].view(torch.float16).view(nq, d))
             phase(j, _lib.LMI_Q_PHASE_PLAN)
 
         def scan(j):
@@ -1431,17 +1433,21 @@ class StreamedSearch:
                           pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]))
             self.h_ans[j].copy_(buf, non_blocking=True)
 
-        self._upload, self._plan, self._scan, self._finish = upload, plan, scan, finish
-        # four streams: uploads (the copy engine), plan, scan (the caller's
-        # stream), finish; per-slot events order them across launches
+        self._upload, self._route, self._plan, self._scan, self._finish = upload, route, plan, scan, finish
+        # five streams: uploads (the copy engine), route, plan, scan (the
+        # caller's stream), finish; per-slot events order them across launches
         self._cs = torch.cuda.Stream(dev)
+        self._rs = torch.cuda.Stream(dev)
         self._ps = torch.cuda.Stream(dev)
         self._fs = torch.cuda.Stream(dev)
         ev = lambda: [torch.cuda.Event() for _ in range(NS)]
-        self._up, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev()
+        self._up, self._rdone, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev(), ev()
         self.graphs = None
         self._t = None  # launch counter once primed
-        self.lookahead = bool(lookahead)
+        # the next scan enqueued ahead: measured faster on one GPU (6.99 vs
+        # 7.01-7.03 ms) and slower on a stripe of 8 (1.27 vs 1.22 ms, it takes
+        # the CUs from the route and finish chains), so by default on one GPU only
+        self.lookahead = (ix.world == 1) if lookahead is None else bool(lookahead)
         self._s_ahead = False  # the next launch's scan is already enqueued
         if not self.stage(nav, qs):
             raise ValueError("the batch stream needs fp16-exact query batches")
@@ -1456,6 +1462,7 @@ class StreamedSearch:
             with torch.cuda.stream(side):
                 for j in range(NS):
                     upload(j)
+                    route(j)
                     plan(j)
                     scan(j)
                     finish(j)
@@ -1471,9 +1478,9 @@ class StreamedSearch:
         elif err is not None:
             raise err
         if capture:
-            # one graph per (branch, slot): plan, scan and finish each a chain
+            # one graph per (stage, slot): route, plan, scan and finish each a chain
             self.graphs = {}
-            for name, fn in (("P", plan), ("S", scan), ("F", finish)):
+            for name, fn in (("R", route), ("P", plan), ("S", scan), ("F", finish)):
                 for j in range(NS):
                     gr = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(gr):
@@ -1505,15 +1512,14 @@ class StreamedSearch:
         return True
 
     def prime(self):
-        """Fill the pipeline with the staged rows of slots 1 and 2 (eagerly:
-        upload + plan + scan of slot 1, upload + plan of slot 2): the next
+        """Fill the pipeline with the staged rows of slots 1, 2 and 3 (eagerly:
+        slot 1 up to its scan, slot 2 up to its plan, slot 3 routed): the next
         launch answers slot 1."""
         dev = self.searcher.index.device
-        self._upload(1)
-        self._plan(1)
-        self._scan(1)
-        self._upload(2)
-        self._plan(2)
+        for j, upto in ((1, 3), (2, 2), (3, 1)):
+            self._upload(j)
+            for f in (self._route, self._plan, self._scan)[:upto]:
+                f(j)
         torch.cuda.current_stream(dev).synchronize()
         self._t = 0
         self._s_ahead = False
@@ -1522,42 +1528,48 @@ class StreamedSearch:
         if self.graphs is not None:
             self.graphs[name, j].replay()
         else:
-            {"P": self._plan, "S": self._scan, "F": self._finish}[name](j)
+            {"R": self._route, "P": self._plan, "S": self._scan, "F": self._finish}[name](j)
 
     def step(self):
         """One launch -> (dists f64 [nq, w], anns uint32 [nq, w]) of the batch
-        it finished (numpy views, valid for the next two launches).  Uploads and
-        plans the rows staged in slot t mod 3 (stage() before step() to stream a
-        new batch; without it the slot's previous rows are planned again),
-        scans slot t+2 and finishes slot t+1 (mod 3), on four streams:
+        it finished (numpy views, valid for the next three launches).  Slot
+        t mod 4 is uploaded and routed (stage() before step() streams a new
+        batch; without it the slot's previous rows are used again), slot
+        t + 3 planned, t + 2 scanned and t + 1 finished (mod 4), on five
+        streams ordered by per-slot events:
 
-            copy:   H2D of slot P                       (the copy engine)
-            plan:   wait H2D(P) -> router, plan (P)
-            scan:   wait plan(S, last launch) -> scan (S)
-            finish: wait scan(F, last launch) -> merge, replay, D2H (F)
+            copy:   H2D of slot R                        (the copy engine)
+            route:  wait H2D(R) -> router (R)
+            plan:   wait route(P, last launch) -> widen, K2 PLAN (P)
+            scan:   wait plan(S, last launch) -> K2 SCAN (S)
+            finish: wait scan(F, last launch) -> merge [all-gather + K3],
+                    replay, D2H (F)
 
-        The scan holds every CU while it runs; the plan and finish chains, both
-        latency-bound, then run side by side instead of one after the other.
-        With `lookahead` the next launch's scan (of the slot planned here) is
-        enqueued too, behind this plan: it starts when the plan is done, not
-        when the host has read this launch's answer."""
+        The scan holds every CU while it runs; the three latency-bound chains
+        then run side by side, and the next scan waits only for the plan.  With
+        `lookahead` the next launch's scan (of the slot planned here) is
+        enqueued too, behind this plan."""
         if self._t is None:
             self.prime()
         dev = self.searcher.index.device
         NS = self.NS
         g = self._t % NS
-        jp, js, jf = g, (g + 2) % NS, (g + 1) % NS
+        jr, jp, js, jf = g, (g + 3) % NS, (g + 2) % NS, (g + 1) % NS
         main = torch.cuda.current_stream(dev)
-        # (d_blk[jp] was last read by the plan three launches ago, which the
+        # (d_blk[jr] was last read by the plan three launches ago, which the
         # finish the host waited for in the last step depended on)
         with torch.cuda.stream(self._cs):
-            self._upload(jp)
-        self._up[jp].record(self._cs)
+            self._upload(jr)
+        self._up[jr].record(self._cs)
         if not self._s_ahead:
             main.wait_event(self._pdone[js])
             self._run("S", js)
             self._sdone[js].record(main)
-        self._ps.wait_event(self._up[jp])
+        self._rs.wait_event(self._up[jr])
+        with torch.cuda.stream(self._rs):
+            self._run("R", jr)
+        self._rdone[jr].record(self._rs)
+        self._ps.wait_event(self._rdone[jp])
         with torch.cuda.stream(self._ps):
             self._run("P", jp)
         self._pdone[jp].record(self._ps)
@@ -1586,43 +1598,46 @@ class StreamedSearch:
 
     def stream(self, batches):
         """Answer an iterable of (q_nav, q_search) batches in order, yielding
-        (dists, anns) copies per batch: two batches fill the pipeline, then one
-        launch per batch, then the last two finish eagerly."""
+        (dists, anns) copies per batch: three batches fill the pipeline, then
+        one launch per batch, then the last three finish eagerly."""
         dev = self.searcher.index.device
+        NS = self.NS
         sync = lambda: torch.cuda.current_stream(dev).synchronize()
+        ans = lambda j: tuple(a.copy() for a in self._answer(j))
         it = iter(batches)
         first = []
         for b in it:
             first.append(b)
-            if len(first) == 2:
+            if len(first) == NS - 1:
                 break
-        for j, b in zip((1, 2), first):
+        for j, b in zip(range(1, NS), first):
             if not self.stage(*b, slot=j):
                 raise ValueError("the batch stream needs fp16-exact query batches")
-        if len(first) < 2:
-            for j in (1, 2)[:len(first)]:
-                self._upload(j); self._plan(j); self._scan(j); self._finish(j); sync()
-                yield tuple(a.copy() for a in self._answer(j))
+        if len(first) < NS - 1:
+            for j in range(1, 1 + len(first)):
+                self._upload(j); self._route(j); self._plan(j); self._scan(j); self._finish(j); sync()
+                yield ans(j)
             return
         self.prime()
         for b in it:
-            if not self.stage(*b, slot=self._t % self.NS):
+            if not self.stage(*b, slot=self._t % NS):
                 raise ValueError("the batch stream needs fp16-exact query batches")
             yield tuple(a.copy() for a in self.step())
-        # drain: slot (t+1)%3 holds the scanned last-but-one batch, slot
-        # (t+2)%3 the planned last one (launch t-1 planned it)
+        # drain: slot t+1 is scanned, t+2 planned (its scan enqueued when
+        # lookahead), t+3 routed (mod 4), t the launch count
         torch.cuda.synchronize(dev)  # (every stream of the last launch)
         t = self._t
-        jf, js = (t + 1) % self.NS, (t + 2) % self.NS
-        self._finish(jf); sync()
-        yield tuple(a.copy() for a in self._answer(jf))
-        if not self._s_ahead:  # (with lookahead the last launch enqueued it)
-            self._scan(js)
-        self._finish(js); sync()
-        yield tuple(a.copy() for a in self._answer(js))
+        j1, j2, j3 = (t + 1) % NS, (t + 2) % NS, (t + 3) % NS
+        self._finish(j1); sync()
+        yield ans(j1)
+        if not self._s_ahead:
+            self._scan(j2)
+        self._finish(j2); sync()
+        yield ans(j2)
+        self._plan(j3); self._scan(j3); self._finish(j3); sync()
+        yield ans(j3)
         self._t = None
         self._s_ahead = False
-
 
 def _wait_event_with_deadline(ev, timeout_s: float) -> None:
     """_wait_with_deadline on a recorded event."""

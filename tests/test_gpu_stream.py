@@ -1,5 +1,5 @@
 """StreamedSearch (the step as a three-stage pipeline of captured graphs over a
-stream of batches: plan of batch b+2, scan of b+1, merge/replay/D2H of b in
+stream of batches: route of batch b+3, plan of b+2, scan of b+1, merge/replay/D2H of b in
 one launch) answers every batch exactly as Searcher.search does; the phase
 flags of lmi_bucket_topk (ABI 7) compose to the one-call result."""
 import numpy as np
@@ -64,7 +64,7 @@ def test_stream_of_batches_equals_search(setup, dist, R):
         np.testing.assert_array_equal(a, a0)
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 4])
 def test_short_streams(setup, n):
     w, s = setup
     bs = _batches(w, n, seed=10 + n)
