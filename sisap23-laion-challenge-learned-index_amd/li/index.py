@@ -1310,9 +1310,9 @@ class StreamedSearch:
     ("The batch stream"):
 
         R  batch b+3: H2D of its staged host rows (copy engine) -> router (K1)
-        P  batch b+2: the queries widened, K2's PLAN phase (fragments and
+        P  batch b+3: the queries widened, K2's PLAN phase (fragments and
            norms, the tile plan, the seed map, the tail split, the bounds)
-        S  batch b+1: K2's SCAN phase
+        S  batch b+1: K2's SCAN phase (of a batch planned two launches ago)
         F  batch b:   K2's MERGE phase (+ the float64 refinement)
            [-> all-gather + K3 at G > 1] -> replay (K4) -> D2H of the answer
 
@@ -1320,14 +1320,15 @@ class StreamedSearch:
     captured graph per slot, ordered across launches by per-slot events, and
     returns the answer of the batch it finished.  The persistent scan holds
     every CU while it runs, so the latency-bound R, P and F chains start in
-    its tail and run side by side; the next scan waits only for P.  Every
+    its tail and run side by side; the next scan, enqueued ahead, waits for a
+    plan done a launch earlier, so the scans run back to back.  Every
     batch passes every stage (the same kernels as Searcher.search), so each
     answer equals Searcher.search of its batch bit for bit; a launch answers
     the batch submitted three launches earlier.
 
     Four slots of per-batch device state (staged rows, classes, scan
-    workspace, lists, answer) rotate over the launches: launch t routes slot
-    t mod 4, plans t+3, scans t+2 and finishes t+1 (mod 4).  A stage runs only
+    workspace, lists, answer) rotate over the launches: launch t routes and
+    plans slot t mod 4, scans t+2 and finishes t+1 (mod 4).  A stage runs only
     on a slot whose earlier stages ran (the fill and drain run the same stage
     functions eagerly), so no kernel reads an unplanned workspace.
 
@@ -1444,9 +1445,11 @@ class StreamedSearch:
         self._up, self._rdone, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev(), ev()
         self.graphs = None
         self._t = None  # launch counter once primed
-        # the next scan enqueued ahead: measured faster on one GPU (6.99 vs
-        # 7.01-7.03 ms) and slower on a stripe of 8 (1.27 vs 1.22 ms, it takes
-        # the CUs from the route and finish chains), so by default on one GPU only
+        # the next scan enqueued ahead, behind this one (its plan ran a launch
+        # earlier), so the scans run back to back: faster on one GPU (7.11 vs
+        # 7.19-7.23 ms per launch), slower on a stripe of 8 (1.30 vs 1.27-1.28:
+        # the next scan takes the CUs the route / plan / finish chains wait
+        # for), so by default on one GPU only
         self.lookahead = (ix.world == 1) if lookahead is None else bool(lookahead)
         self._s_ahead = False  # the next launch's scan is already enqueued
         if not self.stage(nav, qs):
@@ -1513,10 +1516,10 @@ class StreamedSearch:
 
     def prime(self):
         """Fill the pipeline with the staged rows of slots 1, 2 and 3 (eagerly:
-        slot 1 up to its scan, slot 2 up to its plan, slot 3 routed): the next
+        slot 1 up to its scan, slots 2 and 3 up to their plans): the next
         launch answers slot 1."""
         dev = self.searcher.index.device
-        for j, upto in ((1, 3), (2, 2), (3, 1)):
+        for j, upto in ((1, 3), (2, 2), (3, 2)):
             self._upload(j)
             for f in (self._route, self._plan, self._scan)[:upto]:
                 f(j)
@@ -1534,27 +1537,27 @@ class StreamedSearch:
         """One launch -> (dists f64 [nq, w], anns uint32 [nq, w]) of the batch
         it finished (numpy views, valid for the next three launches).  Slot
         t mod 4 is uploaded and routed (stage() before step() streams a new
-        batch; without it the slot's previous rows are used again), slot
-        t + 3 planned, t + 2 scanned and t + 1 finished (mod 4), on five
-        streams ordered by per-slot events:
+        batch; without it the slot's previous rows are used again) and
+        planned, slot t + 2 scanned and t + 1 finished (mod 4), on five streams
+        ordered by per-slot events:
 
-            copy:   H2D of slot R                        (the copy engine)
-            route:  wait H2D(R) -> router (R)
-            plan:   wait route(P, last launch) -> widen, K2 PLAN (P)
-            scan:   wait plan(S, last launch) -> K2 SCAN (S)
-            finish: wait scan(F, last launch) -> merge [all-gather + K3],
-                    replay, D2H (F)
+            copy:   H2D of slot t                      (the copy engine)
+            route:  wait H2D -> router (slot t)
+            plan:   wait route -> widen, K2 PLAN (slot t)
+            scan:   wait plan(two launches ago) -> K2 SCAN (slot t+2)
+            finish: wait scan(last launch) -> merge [all-gather + K3],
+                    replay, D2H (slot t+1)
 
-        The scan holds every CU while it runs; the three latency-bound chains
-        then run side by side, and the next scan waits only for the plan.  With
-        `lookahead` the next launch's scan (of the slot planned here) is
-        enqueued too, behind this plan."""
+        The scan holds every CU while it runs; the latency-bound chains start
+        in its tail.  With `lookahead` (the default on one GPU) the next
+        launch's scan, of a slot planned a launch earlier, is enqueued too, so
+        the scans run back to back and the other stages fill their tails."""
         if self._t is None:
             self.prime()
         dev = self.searcher.index.device
         NS = self.NS
         g = self._t % NS
-        jr, jp, js, jf = g, (g + 3) % NS, (g + 2) % NS, (g + 1) % NS
+        jr, js, jf = g, (g + 2) % NS, (g + 1) % NS
         main = torch.cuda.current_stream(dev)
         # (d_blk[jr] was last read by the plan three launches ago, which the
         # finish the host waited for in the last step depended on)
@@ -1569,19 +1572,21 @@ class StreamedSearch:
         with torch.cuda.stream(self._rs):
             self._run("R", jr)
         self._rdone[jr].record(self._rs)
-        self._ps.wait_event(self._rdone[jp])
+        self._ps.wait_event(self._rdone[jr])
         with torch.cuda.stream(self._ps):
-            self._run("P", jp)
-        self._pdone[jp].record(self._ps)
+            self._run("P", jr)
+        self._pdone[jr].record(self._ps)
         self._fs.wait_event(self._sdone[jf])
         with torch.cuda.stream(self._fs):
             self._run("F", jf)
         self._fdone[jf].record(self._fs)
         if self.lookahead:
-            # the next launch's scan: slot jp, once its plan is done
-            main.wait_event(self._pdone[jp])
-            self._run("S", jp)
-            self._sdone[jp].record(main)
+            # the next launch's scan: slot t+3, planned in the last launch (in
+            # the tail of its scan), so it follows this scan at once
+            jn = (g + 3) % NS
+            main.wait_event(self._pdone[jn])
+            self._run("S", jn)
+            self._sdone[jn].record(main)
         self._s_ahead = self.lookahead
         self._t += 1
         if self.G > 1 and self.graphs is not None:
@@ -1623,8 +1628,8 @@ class StreamedSearch:
             if not self.stage(*b, slot=self._t % NS):
                 raise ValueError("the batch stream needs fp16-exact query batches")
             yield tuple(a.copy() for a in self.step())
-        # drain: slot t+1 is scanned, t+2 planned (its scan enqueued when
-        # lookahead), t+3 routed (mod 4), t the launch count
+        # drain: slot t+1 is scanned, t+2 and t+3 planned (mod 4; t+2's scan
+        # enqueued when lookahead), t the launch count
         torch.cuda.synchronize(dev)  # (every stream of the last launch)
         t = self._t
         j1, j2, j3 = (t + 1) % NS, (t + 2) % NS, (t + 3) % NS
@@ -1634,7 +1639,7 @@ class StreamedSearch:
             self._scan(j2)
         self._finish(j2); sync()
         yield ans(j2)
-        self._plan(j3); self._scan(j3); self._finish(j3); sync()
+        self._scan(j3); self._finish(j3); sync()
         yield ans(j3)
         self._t = None
         self._s_ahead = False
