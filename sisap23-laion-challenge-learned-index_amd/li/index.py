@@ -1342,7 +1342,7 @@ class StreamedSearch:
 
     def __init__(self, searcher: "Searcher", q_nav, q_search, R: int, k: int = 10, *,
                  k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True, lookahead: Optional[bool] = None):
+                 capture: bool = True, lookahead=None):
         s = searcher
         ix = s.index
         dev = ix.device
@@ -1445,12 +1445,15 @@ class StreamedSearch:
         self._up, self._rdone, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev(), ev()
         self.graphs = None
         self._t = None  # launch counter once primed
-        # the next scan enqueued ahead, behind this one (its plan ran a launch
-        # earlier), so the scans run back to back: faster on one GPU (7.11 vs
-        # 7.19-7.23 ms per launch), slower on a stripe of 8 (1.30 vs 1.27-1.28:
-        # the next scan takes the CUs the route / plan / finish chains wait
-        # for), so by default on one GPU only
-        self.lookahead = (ix.world == 1) if lookahead is None else bool(lookahead)
+        # the next launch's scan enqueued ahead (its plan ran a launch
+        # earlier), waiting on the device for this launch's finish
+        # (lookahead="finish", the default): no host round trip before it, and
+        # it does not take the CUs the route / plan / finish chains wait for.
+        # Same box (profiles/r03_stream_lookahead3_ab.txt): one GPU 7.03-7.04 ms
+        # per launch against 7.08-7.09 with the scan right behind the last one
+        # (True) and 7.15-7.16 without lookahead (False); a stripe of 8
+        # 1.25-1.26 / 1.23-1.24 / 1.26-1.27 (True was the slowest on another box)
+        self.lookahead = "finish" if lookahead is None else lookahead
         self._s_ahead = False  # the next launch's scan is already enqueued
         if not self.stage(nav, qs):
             raise ValueError("the batch stream needs fp16-exact query batches")
@@ -1549,9 +1552,10 @@ class StreamedSearch:
                     replay, D2H (slot t+1)
 
         The scan holds every CU while it runs; the latency-bound chains start
-        in its tail.  With `lookahead` (the default on one GPU) the next
-        launch's scan, of a slot planned a launch earlier, is enqueued too, so
-        the scans run back to back and the other stages fill their tails."""
+        in its tail.  With `lookahead` the next launch's scan, of a slot
+        planned a launch earlier, is enqueued too: right behind this scan
+        (True), or (the default, "finish") behind this launch's finish on the
+        device, without a host round trip."""
         if self._t is None:
             self.prime()
         dev = self.searcher.index.device
@@ -1585,9 +1589,11 @@ class StreamedSearch:
             # the tail of its scan), so it follows this scan at once
             jn = (g + 3) % NS
             main.wait_event(self._pdone[jn])
+            if self.lookahead == "finish":
+                main.wait_event(self._fdone[jf])
             self._run("S", jn)
             self._sdone[jn].record(main)
-        self._s_ahead = self.lookahead
+        self._s_ahead = bool(self.lookahead)
         self._t += 1
         if self.G > 1 and self.graphs is not None:
             _wait_event_with_deadline(self._fdone[jf], self.timeout_s)

@@ -12,7 +12,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--worlds", default="1,8")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--eager", action="store_true", help="launch the three branches eagerly on three streams")
-ap.add_argument("--modes", default="stream", help="comma list of stream (default lookahead), stream-nola (none), stream-eager, graph-pipe, graph")
+ap.add_argument("--modes", default="stream", help="comma list of stream (default lookahead), stream-nola (none), stream-la (ahead), stream-fin (after the finish), stream-eager, graph-pipe, graph")
 ap.add_argument("--chunks", default="", help="comma list of chunk rows to try (default: the bench's by W)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
@@ -31,7 +31,8 @@ for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
     for mode in a.modes.split(","):
         if mode.startswith("stream"):
             st = s.streamed(qn, q, 4, k=10, capture=not (a.eager or mode == "stream-eager"),
-                            lookahead=False if mode == "stream-nola" else None)
+                            lookahead={"stream-nola": False, "stream-la": True,
+                                       "stream-fin": "finish"}.get(mode))
             fn = st.step
         else:
             st = s.graph(qn, q, 4, k=10, pipeline=mode == "graph-pipe")
