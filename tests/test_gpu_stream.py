@@ -100,7 +100,7 @@ def test_stream_rejects_inexact_batches(setup):
         s.streamed(w["qn"], w["q"] + np.float32(1e-5), 4, k=10)
 
 
-@pytest.mark.parametrize("lookahead", [False, True])
+@pytest.mark.parametrize("lookahead", [False, True, "finish"])
 def test_stream_with_and_without_lookahead(setup, lookahead):
     """The next launch's scan enqueued ahead (the default) or not: the same
     answers, batch by batch, and over repeated steps."""
