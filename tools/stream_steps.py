@@ -13,6 +13,7 @@ ap.add_argument("--worlds", default="1,8")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--eager", action="store_true", help="launch the three branches eagerly on three streams")
 ap.add_argument("--modes", default="stream", help="comma list of stream (default lookahead), stream-nola (none), stream-la (ahead), stream-fin (after the finish), stream-eager, graph-pipe, graph")
+ap.add_argument("--dist", default="f32", choices=["f32", "f64"])
 ap.add_argument("--chunks", default="", help="comma list of chunk rows to try (default: the bench's by W)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
@@ -30,12 +31,12 @@ for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
     s = Searcher(ix, router)
     for mode in a.modes.split(","):
         if mode.startswith("stream"):
-            st = s.streamed(qn, q, 4, k=10, capture=not (a.eager or mode == "stream-eager"),
+            st = s.streamed(qn, q, 4, k=10, dist=a.dist, capture=not (a.eager or mode == "stream-eager"),
                             lookahead={"stream-nola": False, "stream-la": True,
                                        "stream-fin": "finish"}.get(mode))
             fn = st.step
         else:
-            st = s.graph(qn, q, 4, k=10, pipeline=mode == "graph-pipe")
+            st = s.graph(qn, q, 4, k=10, dist=a.dist, pipeline=mode == "graph-pipe")
             fn = st.run
         for _ in range(3):
             fn()
@@ -43,7 +44,7 @@ for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
         for _ in range(a.steps):
             fn()
         torch.cuda.synchronize()
-        print(f"world {W} chunk {ck}: {mode} {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step "
+        print(f"world {W} chunk {ck} {a.dist}: {mode} {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step "
               f"(scan WGs {os.environ.get('LMI_SCAN_WGS', 'all CUs')})", flush=True)
         del st, fn
     del s, ix; torch.cuda.empty_cache()
