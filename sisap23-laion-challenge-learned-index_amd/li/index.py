@@ -1591,6 +1591,8 @@ class StreamedSearch:
             main.wait_event(self._pdone[jn])
             if self.lookahead == "finish":
                 main.wait_event(self._fdone[jf])
+            elif self.lookahead == "plan":  # (a study: gate on this launch's plan)
+                main.wait_event(self._pdone[jr])
             self._run("S", jn)
             self._sdone[jn].record(main)
         self._s_ahead = bool(self.lookahead)

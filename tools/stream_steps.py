@@ -33,7 +33,7 @@ for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
         if mode.startswith("stream"):
             st = s.streamed(qn, q, 4, k=10, dist=a.dist, capture=not (a.eager or mode == "stream-eager"),
                             lookahead={"stream-nola": False, "stream-la": True,
-                                       "stream-fin": "finish"}.get(mode))
+                                       "stream-fin": "finish", "stream-plan": "plan"}.get(mode))
             fn = st.step
         else:
             st = s.graph(qn, q, 4, k=10, dist=a.dist, pipeline=mode == "graph-pipe")
