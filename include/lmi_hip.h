@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 7
+#define LMI_ABI_VERSION 8
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -344,6 +344,19 @@ int32_t lmi_timing_read(float* ms_out, int32_t max_n);
  * reference re-gathers every bucket from the DataFrame on every call
  * (LearnedIndex.py:152-153, :168). */
 uint64_t lmi_host_hash64(const void* data, uint64_t n_bytes, int32_t threads);
+
+/* ---- staging a host query batch (ABI 8) ------------------------------------ */
+/* The reference's queries are host arrays (search.py:49, :85-87); the batch
+ * stream (li.stream.StreamedSearch.stage) writes each new batch into pinned
+ * staging memory with these, on `threads` OpenMP threads (<= 0: all).
+ * lmi_host_stage_f16: n float32 values -> fp16 (IEEE binary16, round to
+ * nearest even) in dst; returns 1 when every value round-trips exactly
+ * (numpy's array_equal(src.astype(f16).astype(f32), src): the fp16 MFMA
+ * scan's precondition), 0 when some value does not (dst then holds rounded
+ * values that no fp16-exact path may use), -LMI_E_INVALID on null pointers.
+ * lmi_host_copy: a memcpy of n_bytes cut over the threads. */
+int32_t lmi_host_stage_f16(const float* src, uint64_t n, uint16_t* dst, int32_t threads);
+int lmi_host_copy(void* dst, const void* src, uint64_t n_bytes, int32_t threads);
 
 /* ---- misc --------------------------------------------------------------- */
 const char* lmi_last_error(void);

@@ -34,17 +34,13 @@ EnvConfig read_env() {
     e.scan_v2 = env_b("LMI_SCAN_V2");
     e.scan_abl = env_i("LMI_SCAN_ABL", 0);
     e.scan_groups = env_i("LMI_SCAN_GROUPS", 0);
-    e.scan_order = env_i("LMI_SCAN_ORDER", 0);
     e.scan_lag = env_i("LMI_SCAN_LAG", 0);
     e.scan_split = env_i("LMI_SCAN_SPLIT", 0);
     e.scan_split_parts = env_i("LMI_SCAN_SPLIT_PARTS", 2);
     e.scan_wgs = env_i("LMI_SCAN_WGS", 0);
     e.scan_no_pref = env_b("LMI_SCAN_NO_PREF");
-    e.scan_keep_thr = env_b("LMI_SCAN_KEEP_THR");
     e.router_fma = env_b("LMI_ROUTER_FMA");
     e.router_qg = env_i("LMI_ROUTER_QG", 0);
-    e.replay_abl = env_i("LMI_REPLAY_ABL", 0);
-    e.replay_flow = env_b("LMI_REPLAY_FLOW");
     return e;
 }
 

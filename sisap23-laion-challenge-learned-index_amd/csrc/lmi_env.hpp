@@ -11,9 +11,8 @@ namespace lmi {
 struct EnvConfig {
     bool scan_v1;        // LMI_SCAN_V1: force the general scan kernel
     bool scan_v2;        // LMI_SCAN_V2: force the 4-wave ring
-    int scan_abl;        // LMI_SCAN_ABL (diagnostic builds)
+    int scan_abl;        // LMI_SCAN_ABL (the `make ablation` library only)
     int scan_groups;     // LMI_SCAN_GROUPS: tile queues (power of two <= 8), 0 = default
-    int scan_order;      // LMI_SCAN_ORDER: 0 plan order (default), 1 heavy-first per tile, 2 per chunk
     int scan_lag;        // LMI_SCAN_LAG
     int scan_split;      // LMI_SCAN_SPLIT: split the last K tiles of every queue (0: K = the
                          //   queue's share of the grid, the default; -1: off)
@@ -21,11 +20,8 @@ struct EnvConfig {
     int scan_wgs;        // LMI_SCAN_WGS: persistent scan workgroups (0 = one per CU; tests
                          //   use a few to make tiles run after others have published bounds)
     bool scan_no_pref;   // LMI_SCAN_NO_PREF
-    bool scan_keep_thr;  // LMI_SCAN_KEEP_THR (diagnostic builds)
     bool router_fma;     // LMI_ROUTER_FMA: FMA-chain router instead of MFMA
     int router_qg;       // LMI_ROUTER_QG: 1/2/4 query groups per workgroup, 0 = auto
-    int replay_abl;      // LMI_REPLAY_ABL (diagnostic builds)
-    bool replay_flow;    // LMI_REPLAY_FLOW: all rounds as one dataflow launch (slower, a study)
 };
 const EnvConfig& env_config();
 

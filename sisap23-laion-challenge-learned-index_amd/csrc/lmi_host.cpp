@@ -1,5 +1,5 @@
 // Host utilities of the drop-in (no GPU work): a multi-threaded content hash
-// of a host buffer.
+// of a host buffer, and the staging of a host query batch into pinned memory.
 //
 // li.LearnedIndex keeps the bucket-sorted corpus in HBM between calls, where
 // the reference re-gathers every bucket from the DataFrame on every call
@@ -15,9 +15,11 @@
 // order, so the value does not depend on the thread count.  Not
 // cryptographic: it detects changed data, not adversarial collisions.
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
+#include <immintrin.h>
 #include <omp.h>
 
 #include "../../include/lmi_hip.h"
@@ -74,4 +76,127 @@ extern "C" uint64_t lmi_host_hash64(const void* data, uint64_t n_bytes, int32_t 
     uint64_t h = n_bytes * P5;
     for (uint64_t b = 0; b < nb; ++b) h = round1(h, hb[b]);
     return avalanche(h);
+}
+
+// ---- staging a host batch (ABI 8) ------------------------------------------
+// The reference's query batch is a host array (search.py:49, :85-87); the
+// batch stream uploads it from pinned staging memory (li.stream).  Writing a
+// new 10k x 768 batch there is 15-31 MB of host memory traffic per step, so it
+// runs on all host cores.  float32 rows are converted to fp16 in the same pass
+// that checks they round-trip (the fp16 MFMA scan's exactness precondition,
+// numpy's `array_equal(q.astype(f16).astype(f32), q)`).
+namespace {
+
+constexpr uint64_t kStageBlock = 1ull << 16;  // elements per OpenMP work item
+
+// float32 -> fp16 bits, round to nearest even (IEEE 754 binary16), the scalar
+// form for hosts without F16C
+uint16_t f32_to_f16_bits(float f) {
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u;
+    const uint32_t ax = x & 0x7FFFFFFFu;
+    if (ax >= 0x7F800000u)  // inf / nan (nan keeps a quiet payload bit)
+        return (uint16_t)(sign | 0x7C00u | (ax > 0x7F800000u ? 0x200u | ((ax >> 13) & 0x3FFu) : 0u));
+    if (ax >= 0x477FF000u) return (uint16_t)(sign | 0x7C00u);  // rounds to >= 65520: inf
+    if (ax < 0x38800000u) {  // below the smallest normal half: a subnormal (or 0)
+        if (ax < 0x33000000u) return (uint16_t)sign;           // < 2^-25: rounds to 0
+        const uint32_t e = ax >> 23;                          // 102..112
+        const uint32_t m = (ax & 0x7FFFFFu) | 0x800000u;
+        const uint32_t shift = 126 - e;                       // 14..24
+        uint32_t h = m >> shift;
+        const uint32_t rem = m & ((1u << shift) - 1), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (h & 1u))) ++h;
+        return (uint16_t)(sign | h);
+    }
+    uint32_t h = ((ax - 0x38000000u) >> 13);                  // rebias 127 -> 15
+    const uint32_t rem = ax & 0x1FFFu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;   // may carry into the exponent
+    return (uint16_t)(sign | h);
+}
+
+float f16_bits_to_f32(uint16_t h) {
+    const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1Fu, m = h & 0x3FFu, x;
+    if (e == 0x1F) {
+        x = sign | 0x7F800000u | (m << 13);
+    } else if (e == 0) {
+        if (m == 0) {
+            x = sign;
+        } else {  // subnormal: normalise
+            e = 113;
+            while (!(m & 0x400u)) { m <<= 1; --e; }
+            x = sign | (e << 23) | ((m & 0x3FFu) << 13);
+        }
+    } else {
+        x = sign | ((e + 112) << 23) | (m << 13);
+    }
+    float f;
+    std::memcpy(&f, &x, 4);
+    return f;
+}
+
+bool stage_scalar(const float* s, uint64_t n, uint16_t* d) {
+    bool exact = true;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint16_t h = f32_to_f16_bits(s[i]);
+        d[i] = h;
+        exact &= f16_bits_to_f32(h) == s[i];
+    }
+    return exact;
+}
+
+__attribute__((target("avx2,f16c"))) bool stage_f16c(const float* s, uint64_t n, uint16_t* d) {
+    __m256 bad = _mm256_setzero_ps();
+    uint64_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        const __m256 v = _mm256_loadu_ps(s + i);
+        const __m128i h = _mm256_cvtps_ph(v, _MM_FROUND_TO_NEAREST_INT | _MM_FROUND_NO_EXC);
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(d + i), h);
+        // not equal (or unordered) after the round trip: not fp16-exact
+        bad = _mm256_or_ps(bad, _mm256_cmp_ps(v, _mm256_cvtph_ps(h), _CMP_NEQ_UQ));
+    }
+    bool exact = _mm256_testz_ps(bad, bad) != 0;
+    if (i < n) exact &= stage_scalar(s + i, n - i, d + i);
+    return exact;
+}
+
+bool use_f16c() {
+    static const bool ok = __builtin_cpu_supports("f16c") && __builtin_cpu_supports("avx2");
+    const char* e = std::getenv("LMI_HOST_SCALAR");  // test hook: the scalar conversion
+    return ok && !(e && e[0] == '1');
+}
+
+}  // namespace
+
+extern "C" int32_t lmi_host_stage_f16(const float* src, uint64_t n, uint16_t* dst, int32_t threads) {
+    if (n == 0) return 1;
+    if (src == nullptr || dst == nullptr) return -LMI_E_INVALID;
+    const bool vec = use_f16c();
+    const uint64_t nb = (n + kStageBlock - 1) / kStageBlock;
+    const int nt = threads > 0 ? threads : omp_get_max_threads();
+    int inexact = 0;
+#pragma omp parallel for schedule(static) num_threads(nt) reduction(| : inexact)
+    for (int64_t b = 0; b < (int64_t)nb; ++b) {
+        const uint64_t a = (uint64_t)b * kStageBlock;
+        const uint64_t len = n - a < kStageBlock ? n - a : kStageBlock;
+        const bool ok = vec ? stage_f16c(src + a, len, dst + a) : stage_scalar(src + a, len, dst + a);
+        inexact |= ok ? 0 : 1;
+    }
+    return inexact ? 0 : 1;
+}
+
+extern "C" int lmi_host_copy(void* dst, const void* src, uint64_t n_bytes, int32_t threads) {
+    if (n_bytes == 0) return LMI_OK;
+    if (src == nullptr || dst == nullptr) return LMI_E_INVALID;
+    constexpr uint64_t kCopyBlock = 1ull << 20;
+    const uint64_t nb = (n_bytes + kCopyBlock - 1) / kCopyBlock;
+    const int nt = threads > 0 ? threads : omp_get_max_threads();
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int64_t b = 0; b < (int64_t)nb; ++b) {
+        const uint64_t a = (uint64_t)b * kCopyBlock;
+        const uint64_t len = n_bytes - a < kCopyBlock ? n_bytes - a : kCopyBlock;
+        std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, len);
+    }
+    return LMI_OK;
 }

@@ -84,7 +84,6 @@ struct RoundArgs {
     int32_t* uraw;           // [nq * kl] scratch (positions of relevant entries),
                              // category c at [g0 * kl, g1 * kl)
     int32_t* status;
-    int32_t abl;  // diagnostic builds: 1/2/3 stop after grouping / U / selection
 };
 
 // a list distance as the reference holds it: float32 widened, or float64
@@ -244,9 +243,6 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
     // [g0, g1) with g0 = #{q : classes[q, r] < c} (disjoint across categories)
     const int g0 = a.gb[2 * c], g1 = a.gb[2 * c + 1];  // (replay_groups_kernel)
     if (g1 <= g0) return;
-#ifdef LMI_ABLATION
-    if (a.abl == 1) return;
-#endif
     const int32_t* G = a.groups;
     const int kr = a.kr;
     const int kl_use = min(kr, a.kl);
@@ -298,9 +294,6 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
         if (nb_tot == 0) return;  // LearnedIndex.py:157-159
         umin = block_min_g(umin, sh);
         umax = -block_min_g(-umax, sh);
-#ifdef LMI_ABLATION
-        if (a.abl == 2) return;
-#endif
         const int want = kr + kl_use;
         const int lane = tid & 63, wv = tid >> 6;
         if (umax - umin < kBmBits) {
@@ -430,9 +423,6 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
         }  // (register selection)
         __syncthreads();
         const int ns = nsw[kTG / 64];
-#ifdef LMI_ABLATION
-        if (a.abl == 3) return;
-#endif
         __syncthreads();
         if (ns >= kr) {
             // normal case: B_q then the smallest members of U not in B_q;
@@ -598,182 +588,6 @@ __global__ __launch_bounds__(kTG) void replay_group_kernel(RoundArgs a) {
     replay_group_body(a, blockIdx.x);
 }
 
-// ---------------------------------------------------------------------------
-// The whole replay as ONE persistent launch after the groups are laid out
-// (replay_flow_kernel): work items (round r, category c) are dequeued in
-// round-major order; an item waits until every query of its group has merged
-// round r-1 (a per-item counter the merges increment), runs the group
-// (replay_group_body), merges its queries' rows (the stable merge of
-// replay_merge_kernel, one wave per query) and signals the items of round
-// r+1 that hold those queries.  An item only waits for items dequeued before
-// it, which are held by running workgroups, so the grid always drains.
-// Would replace 2R + 1 launches (R groups, R merges, the thresholds / output)
-// and the gaps between them; the results are the same arrays
-// (tests/test_gpu_replay.py), but it measured 4x slower (LMI_REPLAY_FLOW only,
-// see lmi_replay_device).
-// ---------------------------------------------------------------------------
-struct FlowArgs {
-    RoundArgs base;           // classes, nq, R, kl, kr, C, lists, bucket sizes, status
-    const int32_t* groups;    // [R][nq] (replay_groups_kernel)
-    const int32_t* gb;        // [R][C + 1][2]
-    int32_t use_threshold;
-    const double* thr_round0; // nullable (round 0 thresholded: search_single's threshold)
-    double* thr;              // [nq]
-    double* drd[2];           // round rows by round parity [nq][kr]
-    int32_t* drp[2];
-    double* Fd[2];            // merged rows by round parity [nq][fs]
-    int32_t* Fp[2];
-    int32_t* uraw;            // [R][nq * kl]
-    int32_t* done;            // [R][C + 1] merges of round r-1 done per item (zeroed)
-    int32_t* work;            // dequeue counter (zeroed)
-    int32_t fs, k_final, w_out;
-    const int64_t* pos_to_id;
-    int64_t n_total;
-    double* dists;            // [nq][w_out]
-    uint32_t* anns;
-};
-
-__global__ __launch_bounds__(kTG) void replay_flow_kernel(FlowArgs f) {
-    __shared__ int s_item;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int C = f.base.C, R = f.base.R, kr = f.base.kr, nq = f.base.nq;
-    const int kl_use = min(kr, f.base.kl);
-    for (;;) {
-        if (tid == 0) s_item = atomicAdd(f.work, 1);
-        __syncthreads();
-        const int item = s_item;
-        __syncthreads();  // (s_item is rewritten next iteration)
-        if (item >= (C + 1) * R) break;
-        const int r = item / (C + 1), c = item - r * (C + 1);
-        const int32_t* G = f.groups + (size_t)r * nq;
-        const int g0 = f.gb[2 * (size_t)item], g1 = f.gb[2 * (size_t)item + 1];
-        if (g1 <= g0) continue;  // an empty group: no query to merge
-        double* drd = f.drd[r & 1];
-        int32_t* drp = f.drp[r & 1];
-        if (r == 0) {
-            // round 0's rows reset (later rounds': by the previous merge) and
-            // its thresholds (LearnedIndex.py:143-163 with threshold_dist)
-            for (int gi = g0 + tid; gi < g1; gi += kTG) {
-                const int q = G[gi];
-                for (int j = 0; j < kr; ++j) {
-                    drd[(size_t)q * kr + j] = kFill;
-                    drp[(size_t)q * kr + j] = -1;
-                }
-                if (f.thr_round0) f.thr[q] = f.thr_round0[q];
-            }
-            __syncthreads();
-        } else {
-            if (tid == 0) {
-                // bounded (seconds): a group count that never completes would be
-                // a layout bug; flag it (status 8) and drain rather than hang
-                // (relaxed polls, one acquire fence after: an acquire load per
-                //  poll invalidates the XCD's L2 every time, which measured the
-                //  replay 5x slower than its per-round launches)
-                for (uint32_t spins = 0;
-                     __hip_atomic_load(&f.done[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < g1 - g0;
-                     ++spins) {
-                    if (spins >= (1u << 22)) {
-                        atomicOr(f.base.status, 8);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            }
-            __syncthreads();
-        }
-        RoundArgs a = f.base;
-        a.r = r;
-        a.groups = G;
-        a.gb = f.gb + (size_t)r * (C + 1) * 2;
-        a.thresholded = ((r > 0 && f.use_threshold) || (r == 0 && f.thr_round0)) ? 1 : 0;
-        a.thr = f.thr;
-        a.dr_d = drd;
-        a.dr_p = drp;
-        a.uraw = f.uraw + (size_t)r * nq * f.base.kl;
-        replay_group_body(a, c);
-        __syncthreads();
-        // the stable merge of each query's F with its round row
-        // (LearnedIndex.py:82-97), one wave per query
-        const int wF = r == 0 ? 0 : (r == 1 ? kr : f.k_final);
-        const int wn = r == 0 ? kr : min(f.k_final, wF + kr);
-        const int n = wF + kr;
-        const bool last = r + 1 == R;
-        const double* Fd = f.Fd[r & 1];
-        const int32_t* Fp = f.Fp[r & 1];
-        double* Fd_out = f.Fd[(r + 1) & 1];
-        int32_t* Fp_out = f.Fp[(r + 1) & 1];
-        for (int gi = g0 + wv; gi < g1; gi += kTG / 64) {
-            const int q = G[gi];
-            const double* fd = Fd + (size_t)q * f.fs;
-            const double* dd = drd + (size_t)q * kr;
-            double thr_next = -__builtin_inf();
-            for (int j = lane; j < n; j += 64) {
-                double dj;
-                int32_t pj;
-                int rank;
-                if (r == 0) {
-                    dj = dd[j];
-                    pj = drp[(size_t)q * kr + j];
-                    rank = j;  // round 0's row as it is (its max is the threshold)
-                    thr_next = fmax(thr_next, dj);
-                } else {
-                    dj = j < wF ? fd[j] : dd[j - wF];
-                    pj = j < wF ? Fp[(size_t)q * f.fs + j] : drp[(size_t)q * kr + j - wF];
-                    rank = 0;
-                    for (int i = 0; i < wF; ++i) {
-                        const double di = fd[i];
-                        rank += (di < dj || (di == dj && i < j)) ? 1 : 0;
-                    }
-                    for (int i = 0; i < kr; ++i) {
-                        const double di = dd[i];
-                        rank += (di < dj || (di == dj && wF + i < j)) ? 1 : 0;
-                    }
-                    if (rank == wn - 1) thr_next = dj;  // the merged row is ascending
-                }
-                if (rank < wn) {
-                    Fd_out[(size_t)q * f.fs + rank] = dj;
-                    Fp_out[(size_t)q * f.fs + rank] = pj;
-                    if (last && rank < f.w_out) {
-                        int64_t id = 0;
-                        if (pj >= 0) {
-                            if (pj < f.n_total) id = f.pos_to_id[pj];
-                            else atomicOr(f.base.status, 4);
-                        }
-                        f.dists[(size_t)q * f.w_out + rank] = dj;
-                        f.anns[(size_t)q * f.w_out + rank] = (uint32_t)id;
-                    }
-                }
-            }
-            if (!last) {
-                // the next round's prologue: its row reset and threshold
-                for (int j = lane; j < kr; j += 64) {
-                    f.drd[(r + 1) & 1][(size_t)q * kr + j] = kFill;
-                    f.drp[(r + 1) & 1][(size_t)q * kr + j] = -1;
-                }
-                if (r == 0) {
-                    for (int off = 32; off > 0; off >>= 1) thr_next = fmax(thr_next, __shfl_xor(thr_next, off));
-                } else {
-                    for (int off = 32; off > 0; off >>= 1) thr_next = fmax(thr_next, __shfl_xor(thr_next, off));
-                }
-                if (lane == 0) f.thr[q] = thr_next;
-            }
-        }
-        __threadfence();
-        __syncthreads();
-        if (!last) {
-            // signal round r+1: each of the group's queries is one merge done
-            // for the item that holds it next round
-            for (int gi = g0 + tid; gi < g1; gi += kTG) {
-                const int q = G[gi];
-                const int c1 = cat_of(f.base.classes[(size_t)q * R + r + 1], C);
-                atomicAdd(&f.done[(size_t)(r + 1) * (C + 1) + c1], 1);
-            }
-        }
-        (void)kl_use;
-    }
-}
-
 __global__ __launch_bounds__(kT) void replay_thr_kernel(int32_t nq, int32_t kr, int32_t fs,
                                                         int32_t wF, int32_t mode,
                                                         const double* __restrict__ Fd,
@@ -876,18 +690,8 @@ __global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, i
     anns[t] = (uint32_t)id;  // numpy int64 -> uint32 assignment
 }
 
-int num_cus_replay() {
-    static int n = [] {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) v = 256;
-        return v > 0 ? v : 256;
-    }();
-    return n;
-}
-
 struct ReplayWs {
-    size_t groups, gb, Fd[2], Fp[2], drd[2], drp[2], thr, uraw, done, total;
+    size_t groups, gb, Fd[2], Fp[2], drd[2], drp[2], thr, uraw, total;
 };
 
 ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
@@ -910,8 +714,7 @@ ReplayWs replay_ws(int nq, int R, int kl, int kr, int w, int C) {
         s.drp[b] = take((size_t)nq * kr * 4);
     }
     s.thr = take((size_t)nq * 8);
-    s.uraw = take((size_t)R * nq * kl * 4);  // per round (the flow kernel overlaps rounds)
-    s.done = take((size_t)R * (C + 1) * 4 + 4);  // + the flow kernel's dequeue counter
+    s.uraw = take((size_t)nq * kl * 4);  // one round's (the rounds run one after another)
     s.total = off;
     return s;
 }
@@ -1002,57 +805,6 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
     // every round's groups in one launch ((C + 1) x R workgroups)
     hipLaunchKernelGGL(replay_groups_kernel, dim3(C + 1, R), dim3(kTG), 0, st, classes, nq, R, C, groups, gb);
     LMI_LAUNCH_CHECK("replay_groups_kernel");
-    if (env_config().replay_flow) {
-        // LMI_REPLAY_FLOW (a study, not the default): all rounds in one
-        // persistent dataflow launch, items waiting on the previous round's
-        // merges.  Measured 4x slower than the per-round launches below (489
-        // vs 117 us on the bench's lists): every agent-scope release / acquire
-        // writes back / invalidates the XCD's L2 on gfx950, and a group's
-        // merges run one wave per query instead of one thread per element.
-        int32_t* done = (int32_t*)(ws + s.done);
-        LMI_TRY(fill_u32(done, 0u, (size_t)R * (C + 1) + 1, st));
-        FlowArgs f{};
-        f.base.classes = classes;
-        f.base.nq = nq;
-        f.base.R = R;
-        f.base.kl = k_list;
-        f.base.kr = k_round;
-        f.base.C = C;
-        f.base.lists_d = lists_d;
-        f.base.lists_f64 = lists_f64;
-        f.base.lists_p = lists_pos;
-        f.base.bucket_size = bucket_size;
-        f.base.status = status;
-#ifdef LMI_ABLATION
-        f.base.abl = env_config().replay_abl;
-#endif
-        f.groups = groups;
-        f.gb = gb;
-        f.use_threshold = use_threshold;
-        f.thr_round0 = thr_round0;
-        f.thr = (double*)(ws + s.thr);
-        for (int b = 0; b < 2; ++b) {
-            f.drd[b] = (double*)(ws + s.drd[b]);
-            f.drp[b] = (int32_t*)(ws + s.drp[b]);
-            f.Fd[b] = (double*)(ws + s.Fd[b]);
-            f.Fp[b] = (int32_t*)(ws + s.Fp[b]);
-        }
-        f.uraw = (int32_t*)(ws + s.uraw);
-        f.done = done;
-        f.work = done + (size_t)R * (C + 1);
-        f.fs = fs;
-        f.k_final = k_final;
-        f.w_out = w;
-        f.pos_to_id = pos_to_id;
-        f.n_total = n_total;
-        f.dists = dists_out;
-        f.anns = anns_out;
-        const int items = (C + 1) * R;
-        hipLaunchKernelGGL(replay_flow_kernel, dim3((unsigned)std::min(items, num_cus_replay())),
-                           dim3(kTG), 0, st, f);
-        LMI_LAUNCH_CHECK("replay_flow_kernel");
-        return LMI_OK;
-    }
     int cur = 0;  // F lives in buffer cur; the merge writes the other one
     int wF = 0;
     for (int r = 0; r < R; ++r) {
@@ -1087,9 +839,6 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         a.dr_p = drp;
         a.uraw = (int32_t*)(ws + s.uraw);
         a.status = status;
-#ifdef LMI_ABLATION
-        a.abl = env_config().replay_abl;
-#endif
         hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, a);
         LMI_LAUNCH_CHECK("replay_group_kernel");
         const bool last = r + 1 == R;

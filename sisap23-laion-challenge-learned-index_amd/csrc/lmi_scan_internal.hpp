@@ -125,6 +125,7 @@ struct Scan2Args {
     const unsigned long long* lo_g;  // LO: [nq*R] lower-bound key (d, gpos) per pair id
     const int32_t* pair_pos;    // LMI_Q_SEED_ROUND0: [P] grouped position of the pair's (q, 0), -1 if none; else null
     float seed_margin;          //   (distance added to the seed: 2 eps in the float64 mode)
+    unsigned long long* dbg;    // diagnostic counters of the ABL != 0 variants (lmi_scan_abl.hip); null
 };
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],

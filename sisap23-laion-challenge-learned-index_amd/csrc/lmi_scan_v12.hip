@@ -354,7 +354,7 @@ __device__ __forceinline__ void insert_survivors(const float (&dv)[16], float bo
     }
 }
 
-// ABL (diagnostic builds only, -DLMI_ABLATION): 1 = no top-k insertion,
+// ABL (round-1 diagnostic variants, no longer instantiated): 1 = no top-k insertion,
 // 2 = no MFMA / LDS reads (DMA + barriers only), 3 = no DMA (compute on
 // whatever the ring holds); scan v3 also: 4 = no DMA, no insertion, 5 = no
 // DMA, no epilogue, 6 = 5 without the per-stage barrier.  Results are wrong
@@ -617,12 +617,6 @@ int launch_scan2_v(const Scan2Args& b, hipStream_t s) {
 
 template <int KL>
 int launch_scan2(const Scan2Args& b, hipStream_t s) {
-#ifdef LMI_ABLATION
-    const int abl = env_config().scan_abl;
-    if (abl == 1) return launch_scan2_v<KL, 1>(b, s);
-    if (abl == 2) return launch_scan2_v<KL, 2>(b, s);
-    if (abl == 3) return launch_scan2_v<KL, 3>(b, s);
-#endif
     return launch_scan2_v<KL, 0>(b, s);
 }
 

@@ -140,6 +140,17 @@ class LearnedIndex(Logger):
     def _identity(self, data_navigation, data_search, labels):
         return (identity_key(data_search), identity_key(labels), identity_key(data_navigation.index))
 
+    def _is_attached(self, data_navigation, data_search, labels) -> bool:
+        """The attached objects themselves (held by strong references, so no
+        freed object's id() or buffer can be taken for them), with their value
+        arrays still where they were at attach time."""
+        t = self._trusted
+        if t is None or self._index is None or t[1] != self._cache_key:
+            return False
+        refs = t[2]
+        return (refs[0] is data_search and refs[1] is labels and refs[2] is data_navigation.index
+                and t[0] == self._identity(data_navigation, data_search, labels))
+
     def attach(self, data_navigation, data_search, pred_categories):
         """Build the HBM index of data_search (rows in data_navigation's id
         order, bucket labels `pred_categories`) now, outside any timed call,
@@ -151,8 +162,10 @@ class LearnedIndex(Logger):
         self._trusted = None
         self._cat_written = None
         self._device_index(data_navigation, data_search, pred_categories)
+        # strong references to the trusted objects: while they are held, their
+        # id()s and buffers cannot be reused by new objects
         self._trusted = (self._identity(data_navigation, data_search, pred_categories),
-                         self._cache_key)
+                         self._cache_key, (data_search, pred_categories, data_navigation.index))
         self._attached_labels = pred_categories if isinstance(pred_categories, np.ndarray) else None
         return self._index
 
@@ -164,9 +177,7 @@ class LearnedIndex(Logger):
     def _device_index(self, data_navigation, data_search, labels):
         """DeviceIndex of data_search rows in data_navigation order."""
         from .index import DeviceIndex
-        if self._trusted is not None and self._index is not None and \
-                self._trusted[1] == self._cache_key and \
-                self._trusted[0] == self._identity(data_navigation, data_search, labels):
+        if self._is_attached(data_navigation, data_search, labels):
             return self._index
         labels = np.asarray(labels).astype(np.int64)
         ds = _search_frame(data_search)

@@ -75,6 +75,8 @@ EXPORTS = (
     "lmi_abi_version",
     "lmi_config_reload",
     "lmi_host_hash64",
+    "lmi_host_stage_f16",
+    "lmi_host_copy",
 )
 
 
@@ -97,7 +99,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class IndexDesc(C.Structure):
@@ -159,6 +161,8 @@ _SIGNATURES = {
     "lmi_abi_version": (C.c_int32, []),
     "lmi_config_reload": (C.c_int, []),
     "lmi_host_hash64": (C.c_uint64, [_P, C.c_uint64, _I32]),
+    "lmi_host_stage_f16": (C.c_int32, [_P, C.c_uint64, _P, _I32]),
+    "lmi_host_copy": (C.c_int, [_P, _P, C.c_uint64, _I32]),
 }
 
 _lock = threading.Lock()

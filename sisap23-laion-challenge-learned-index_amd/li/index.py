@@ -797,12 +797,14 @@ class Searcher:
     def streamed(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "StreamedSearch":
         """The step as a four-stage pipeline of captured graphs over a stream
         of batches (StreamedSearch); answers equal search(...) per batch."""
+        from .stream import StreamedSearch
         return StreamedSearch(self, q_nav, q_search, R, k, **kw)
 
     def graph(self, q_nav, q_search, R: int, k: int = 10, **kw) -> "GraphedSearch":
         """The step captured as a HIP graph (GraphedSearch), from the batch in
         host memory to the answer in host memory: same results as
         search(..., semantics="reference", replay_on="device")."""
+        from .graphed import GraphedSearch
         return GraphedSearch(self, q_nav, q_search, R, k, **kw)
 
     def search(self, q_nav, q_search, R: int, k: int = 10, *, k_round: int = 10,
@@ -967,729 +969,3 @@ class Searcher:
                      use_threshold=use_threshold)
         lap("replay", t0) if sync else None
         return out
-
-
-def _host_array(x) -> np.ndarray:
-    """A query batch (numpy, or a torch tensor on any device) as a host array."""
-    if isinstance(x, torch.Tensor):
-        return x.detach().cpu().numpy()
-    return np.asarray(x)
-
-
-class GraphedSearch:
-    """One search step captured once as a HIP graph and replayed per batch,
-    from queries in HOST memory to the answer in host memory, as the
-    reference's timer sees it (search.py:116-141; its queries are host arrays,
-    search.py:49, :85-87):
-
-        H2D of the staged batch (pinned host rows)
-        -> router (K1) -> scan (K2) [-> all-gather + K3] -> replay (K4)
-        -> D2H of the answer and of both status words
-
-    The ~25 launches and the copies go to the GPU as one graph launch, with no
-    host work between them.
-
-    Staging (`stage`, outside the step, like the reference's h5 loads before
-    its timer): the batch is written into a pinned host buffer laid out per
-    rank block as [pca96 f32 (per x 96) | clip768 (per x d) | classes (per x
-    R, G > 1 only)].  The clip768 rows are staged as fp16 when the index is
-    fp16 and every query value is fp16-representable (checked on the host at
-    staging; float16 input is exact by construction): half the bytes over
-    PCIe, widened to float32 on the device.  A batch that is not fp16-exact
-    under an fp16 capture is answered by the eager path instead.
-
-    G > 1 ranks: rank g uploads only its block (1/G of the batch), routes its
-    queries into the block's classes, and ONE all-gather over xGMI hands every
-    rank the whole batch and all classes; then the striped scan and the list
-    exchange as in Searcher.search.
-
-    The graph owns its scan workspace (index._ws may be replaced by a later
-    eager call with a bigger batch).  `run()` returns numpy views
-    of the graph's pinned output buffer, valid until the next run."""
-
-    def __init__(self, searcher: "Searcher", q_nav, q_search, R: int,
-                 k: int = 10, *, k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True, pipeline: bool = False):
-        s = searcher
-        ix = s.index
-        dev = ix.device
-        lib = _lib.load()
-        self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
-        self.use_threshold, self.dist = use_threshold, dist
-        G = ix.world
-        grouped = G > 1 and torch.distributed.is_initialized()
-        if k_round > _lib.LMI_MAX_K or (capture and grouped and
-                                       torch.distributed.get_backend(s.group) != "nccl"):
-            raise ValueError("graph capture needs k_round <= 16 and RCCL collectives "
-                             "(capture=False runs the same step eagerly, e.g. over gloo)")
-        nav = _host_array(q_nav)
-        qs = _host_array(q_search)
-        nq, d, dn = int(qs.shape[0]), ix.d, int(nav.shape[1])
-        if qs.shape != (nq, d) or nav.shape[0] != nq:
-            raise ValueError("query shapes do not match the index")
-        self.nq, self.d, self.dn = nq, d, dn
-        # the batch's precision class is decided on the host, once per capture
-        self.f16_up = ix.storage == "f16" and d % 2 == 0 and (
-            qs.dtype == np.float16 or _np_fp16_exact(qs))
-        self.qmode = _lib.LMI_Q_F16 if self.f16_up else _lib.LMI_Q_F32
-        f64 = dist == "f64"
-        # the batch is shared over the ranks of the process group (the index's
-        # world is the stripe count; they differ only in a one-process
-        # rehearsal of one stripe, tools/shard_step.py)
-        Gi = G if grouped else 1
-        G = torch.distributed.get_world_size(s.group) if Gi > 1 else 1
-        g = torch.distributed.get_rank(s.group) if Gi > 1 else 0
-        self.per = per = -(-nq // G)
-        self.wq = wq = d // 2 if self.f16_up else d          # int32 words per staged row
-        self.bw = bw = per * dn + per * wq + (per * R if G > 1 else 0)
-        pin = torch.cuda.is_available()
-        self.bw_all = bw
-        self.h_blk = torch.zeros((G, bw), dtype=torch.int32, pin_memory=pin)
-        if not self.stage(nav, qs):
-            raise ValueError("staging failed")
-        need = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
-            C.byref(ix.desc), nq, R, k_round, self.qmode)
-        self.ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
-        # pipeline: two device copies of the staged block, each with its own
-        # captured graph; run() uploads the next one on a copy stream while
-        # the current graph runs (the upload leaves the graph)
-        self.pipeline = bool(pipeline) and capture
-        self.d_blks = [torch.empty((bw,), dtype=torch.int32, device=dev)
-                       for _ in range(2 if self.pipeline else 1)]
-        self.d_blk = self.d_blks[0]
-        self.d_all = torch.empty((G, bw), dtype=torch.int32, device=dev) if G > 1 else None
-        self.q32 = torch.empty((G * per, d), dtype=torch.float32, device=dev) \
-            if (self.f16_up or G > 1) else None
-        self.cls = torch.empty((G * per, R), dtype=torch.int32, device=dev) if G > 1 else None
-        bsz, p2id = s._device_tables()
-        self.w = k_round if R == 1 else k
-        self.rank_in_group = g
-        self.G = G
-        # collectives inside a replayed graph are GPU work the process group's
-        # watchdog does not track: run() bounds its own wait instead
-        self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
-        copy_stream = torch.cuda.Stream(dev)
-
-        def step(slot=0):
-            ans = answer_buffer(nq, self.w, dev)
-            main = torch.cuda.current_stream(dev)
-            d_blk = self.d_blks[slot]
-            if G == 1:
-                if not self.pipeline:
-                    # pca96 rows first; the clip768 rows come in on a second
-                    # stream while the router runs
-                    d_blk[:per * dn].copy_(self.h_blk[0, :per * dn], non_blocking=True)
-                    copy_stream.wait_stream(main)
-                    with torch.cuda.stream(copy_stream):
-                        d_blk[per * dn:].copy_(self.h_blk[0, per * dn:], non_blocking=True)
-                classes = s.router.topr(d_blk[:per * dn].view(torch.float32).view(per, dn), R)[0]
-                if not self.pipeline:
-                    main.wait_stream(copy_stream)
-                sv = d_blk[per * dn:per * dn + per * wq]
-                if self.f16_up:
-                    q = self.q32
-                    q.copy_(sv.view(torch.float16).view(per, d))
-                else:
-                    q = sv.view(torch.float32).view(per, d)
-            else:
-                # this rank's block: upload, route its queries into the block,
-                # one all-gather of every block (queries + classes)
-                from .dist import _all_gather
-                if not self.pipeline:
-                    d_blk.copy_(self.h_blk[g], non_blocking=True)
-                s.router.topr(d_blk[:per * dn].view(torch.float32).view(per, dn), R,
-                              out=d_blk[per * (dn + wq):])
-                _all_gather(self.d_all.view(-1), d_blk, s.group)
-                sv = self.d_all[:, per * dn:per * (dn + wq)]
-                if self.f16_up:
-                    self.q32.view(G, per, d).copy_(sv.view(torch.float16).view(G, per, d))
-                else:
-                    self.q32.view(G, per, d).copy_(sv.view(torch.float32).view(G, per, d))
-                self.cls.view(G, per, R).copy_(self.d_all[:, per * (dn + wq):].view(G, per, R))
-                q = self.q32[:nq]
-                classes = self.cls[:nq]
-            d_, pos, _ = s._scan(q, classes, k_round, self.qmode, f64, status_out=ans[3][0:1],
-                                 ws=self.ws, seed_round0=use_threshold and k <= k_round and _SEED_ROUND0)
-            replay_device(classes, d_, pos, k_round=k_round, k_final=k, bucket_size=bsz,
-                          pos_to_id=p2id, use_threshold=use_threshold,
-                          out=(ans[1], ans[2], ans[3][1:2]))
-            return ans[0]
-
-        # warm up on a side stream (allocations, kernel attributes, RCCL
-        # communicators), then capture.  G > 1: the ranks agree that every
-        # rank's warm-up succeeded before any rank captures (a rank that
-        # raised before entering a collective would otherwise leave the others
-        # waiting in the next one; a rank that fails inside a collective is
-        # ended by the process group's timeout, li.dist.init_from_env)
-        self._step = None
-        if not capture:
-            # the same step, launched eagerly per run (the multi-process gloo
-            # rehearsal of the sharded upload on one GPU: tests/test_gpu_dist.py)
-            buf = step()
-            torch.cuda.synchronize(dev)
-            self.h = torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
-            self.graph = None
-            self._step = step
-            return
-        self._cs = copy_stream
-        if self.pipeline:
-            self._up_ev = [torch.cuda.Event() for _ in range(2)]
-            self._done_ev = [torch.cuda.Event() for _ in range(2)]
-            for slot in range(2):
-                self.d_blks[slot].copy_(self.h_blk[g], non_blocking=True)
-            torch.cuda.synchronize(dev)
-        slots = (0, 1) if self.pipeline else (0, 0)
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        err = None
-        try:
-            with torch.cuda.stream(side):
-                for slot in slots:
-                    buf = step(slot)
-            torch.cuda.current_stream(dev).wait_stream(side)
-            torch.cuda.synchronize(dev)
-        except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
-            err = e
-        if Gi > 1:
-            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
-            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
-            if int(ok.item()) == 0:
-                raise RuntimeError(f"graph warm-up failed on some rank: {err!r}")
-        elif err is not None:
-            raise err
-        # one pinned answer buffer per graph: with launch() / result() a graph
-        # may run while the host reads the other's answer
-        self.hs = [torch.empty(tuple(buf.shape), dtype=torch.int32, pin_memory=True)
-                   for _ in range(2 if self.pipeline else 1)]
-        self.h = self.hs[0]
-        self.graphs, self._keep = [], []
-        for slot in range(2 if self.pipeline else 1):
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                buf = step(slot)
-                self.hs[slot].copy_(buf, non_blocking=True)
-            self.graphs.append(gr)
-            self._keep.append(buf)
-        self.graph = self.graphs[0]
-        self._slot = 0
-        self._fresh = [True, True]   # d_blks[slot] holds the staged batch
-        torch.cuda.synchronize(dev)
-
-    def stage(self, q_nav, q_search) -> bool:
-        """Write a batch (host or device arrays of the captured shape) into the
-        pinned staging buffer.  False if it cannot be staged in the captured
-        precision (clip768 values not fp16-representable under an fp16
-        capture): run() then answers it on the eager path."""
-        nav = _host_array(q_nav).astype(np.float32, copy=False)
-        qs = _host_array(q_search)
-        nq, d, dn, per, wq = self.nq, self.d, self.dn, self.per, self.wq
-        if nav.shape != (nq, dn) or qs.shape != (nq, d):
-            raise ValueError("a staged batch must have the captured shape")
-        if self.f16_up:
-            if qs.dtype == np.float16:
-                q16 = qs
-            else:
-                q32 = qs.astype(np.float32, copy=False)
-                q16 = q32.astype(np.float16)
-                if not np.array_equal(q16.astype(np.float32), q32):
-                    return False
-            src, sdt = q16, np.float16
-        else:
-            src, sdt = qs.astype(np.float32, copy=False), np.float32
-        if getattr(self, "pipeline", False):
-            # an upload from the pinned buffer may be in flight (run());
-            # both device copies are stale from now on
-            self._cs.synchronize()
-            self._fresh = [False, False]
-        blk = self.h_blk.numpy()
-        for g in range(blk.shape[0]):
-            lo, hi = min(nq, g * per), min(nq, (g + 1) * per)
-            nv = blk[g, :per * dn].view(np.float32).reshape(per, dn)
-            nv[:hi - lo] = nav[lo:hi]
-            nv[hi - lo:] = 0
-            sv = blk[g, per * dn:per * (dn + wq)].view(sdt).reshape(per, d)
-            sv[:hi - lo] = src[lo:hi]
-            sv[hi - lo:] = 0
-        self._staged = (nav, qs)
-        return True
-
-    def upload_bytes(self) -> int:
-        """Bytes this rank moves host -> device per step."""
-        per, dn, wq = self.per, self.dn, self.wq
-        return 4 * per * (dn + wq)
-
-    def run(self, q_nav=None, q_search=None):
-        """Replay the step (after staging a new batch, if given) -> (dists f64
-        [nq, w], anns uint32 [nq, w])."""
-        s = self.searcher
-        dev = s.index.device
-        if q_nav is not None or q_search is not None:
-            if q_nav is None or q_search is None:
-                raise ValueError("stage both q_nav and q_search")
-            if not self.stage(q_nav, q_search):
-                return self._eager(q_nav, q_search)
-        if self.pipeline:
-            return self.result(self.launch())
-        elif self.graph is not None:
-            self.graph.replay()
-        else:
-            self.h.copy_(self._step(), non_blocking=True)
-        if self.G > 1 and self.graph is not None:
-            _wait_with_deadline(dev, self.timeout_s)
-        else:
-            torch.cuda.current_stream(dev).synchronize()
-        return self._answer(self.h)
-
-    def _answer(self, h):
-        hd, ha, st, rst = answer_views(h, self.nq, self.w)
-        if st & _lib.LMI_STATUS_INTERNAL or rst:
-            raise RuntimeError(f"search: internal status {st}/{rst}")
-        return hd, ha
-
-    def launch(self) -> int:
-        """pipeline=True: enqueue one step on the staged batch without waiting
-        for it (the next batch's upload starts beside it); returns a ticket for
-        result().  Keeping one launch ahead of result() hides the host's
-        synchronise-to-launch gap between steps (at most two in flight: a
-        ticket's answer is valid until the launch after next)."""
-        if not self.pipeline:
-            raise ValueError("launch() needs GraphedSearch(pipeline=True)")
-        slot = self._slot
-        self._run_pipelined(self.searcher.index.device)
-        return slot
-
-    def result(self, ticket: int):
-        """Wait for the step of `ticket` (from launch()) -> (dists f64 [nq, w],
-        anns uint32 [nq, w]): numpy views of that step's pinned answer."""
-        ev = self._done_ev[ticket]
-        if self.G > 1:
-            _wait_event_with_deadline(ev, self.timeout_s)
-        else:
-            ev.synchronize()
-        return self._answer(self.hs[ticket])
-
-    def _upload(self, slot):
-        """The staged block into d_blks[slot] on the copy stream, once the
-        graph that last read that copy has finished."""
-        cs = self._cs
-        cs.wait_event(self._done_ev[slot])
-        with torch.cuda.stream(cs):
-            self.d_blks[slot].copy_(self.h_blk[self.rank_in_group], non_blocking=True)
-        self._up_ev[slot].record(cs)
-        self._fresh[slot] = True
-
-    def _run_pipelined(self, dev):
-        """Replay the current slot's graph; meanwhile upload the staged batch
-        into the other slot for the next run (a stream of batches: the copy
-        engine moves batch i + 1 while batch i is searched)."""
-        main = torch.cuda.current_stream(dev)
-        slot = self._slot
-        if not self._fresh[slot]:
-            self._upload(slot)
-        main.wait_event(self._up_ev[slot])
-        self.graphs[slot].replay()
-        self._done_ev[slot].record(main)
-        self._fresh[slot] = False
-        nxt = 1 - slot
-        if not self._fresh[nxt]:
-            self._upload(nxt)
-        self._slot = nxt
-
-    def _eager(self, q_nav, q_search):
-        dev = self.searcher.index.device
-        self.searcher._qcheck = None
-        return self.searcher.search(_as_torch(_host_array(q_nav), dev, torch.float32),
-                                    _as_torch(_host_array(q_search), dev, torch.float32),
-                                    self.R, k=self.k, k_round=self.k_round,
-                                    use_threshold=self.use_threshold, dist=self.dist)
-
-
-
-class StreamedSearch:
-    """A stream of query batches through the step as a four-stage pipeline
-    ("The batch stream"):
-
-        R  batch b+3: H2D of its staged host rows (copy engine) -> router (K1)
-        P  batch b+3: the queries widened, K2's PLAN phase (fragments and
-           norms, the tile plan, the seed map, the tail split, the bounds)
-        S  batch b+1: K2's SCAN phase (of a batch planned two launches ago)
-        F  batch b:   K2's MERGE phase (+ the float64 refinement)
-           [-> all-gather + K3 at G > 1] -> replay (K4) -> D2H of the answer
-
-    One launch (`step`) runs the four stages on five streams, each stage a
-    captured graph per slot, ordered across launches by per-slot events, and
-    returns the answer of the batch it finished.  The persistent scan holds
-    every CU while it runs, so the latency-bound R, P and F chains start in
-    its tail and run side by side; the next scan, enqueued ahead, waits for a
-    plan done a launch earlier, so the scans run back to back.  Every
-    batch passes every stage (the same kernels as Searcher.search), so each
-    answer equals Searcher.search of its batch bit for bit; a launch answers
-    the batch submitted three launches earlier.
-
-    Four slots of per-batch device state (staged rows, classes, scan
-    workspace, lists, answer) rotate over the launches: launch t routes and
-    plans slot t mod 4, scans t+2 and finishes t+1 (mod 4).  A stage runs only
-    on a slot whose earlier stages ran (the fill and drain run the same stage
-    functions eagerly), so no kernel reads an unplanned workspace.
-
-    G > 1: every rank uploads and routes the whole batch (no collective in R
-    or P, both off the critical path); the one collective, the list exchange,
-    runs in F as in Searcher.search.  fp16 index and fp16-exact query batches
-    only (the phased scan is the fp16 scan); other batches go through
-    GraphedSearch / Searcher.search."""
-
-    NS = 4
-
-    def __init__(self, searcher: "Searcher", q_nav, q_search, R: int, k: int = 10, *,
-                 k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True, lookahead=None):
-        s = searcher
-        ix = s.index
-        dev = ix.device
-        lib = _lib.load()
-        self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
-        self.use_threshold, self.dist = use_threshold, dist
-        G = ix.world
-        # the list exchange spans the process group's ranks (a stripe of a
-        # G-way index in a process without a group: the rank's own lists)
-        self.G = torch.distributed.get_world_size(s.group) if (
-            G > 1 and torch.distributed.is_initialized()) else 1
-        if k_round > _lib.LMI_MAX_K:
-            raise ValueError("the phased scan needs k_round <= 16")
-        if capture and self.G > 1 and torch.distributed.get_backend(s.group) != "nccl":
-            raise ValueError("graph capture needs RCCL collectives (capture=False runs the "
-                             "branches eagerly, e.g. over gloo)")
-        nav, qs = _host_array(q_nav), _host_array(q_search)
-        nq, d, dn = int(qs.shape[0]), ix.d, int(nav.shape[1])
-        if qs.shape != (nq, d) or nav.shape[0] != nq:
-            raise ValueError("query shapes do not match the index")
-        if not (ix.storage == "f16" and d % 2 == 0):
-            raise ValueError("the batch stream needs an fp16 index with an even d")
-        self.nq, self.d, self.dn = nq, d, dn
-        f64 = dist == "f64"
-        self.w = k_round if R == 1 else k
-        kl = k_round
-        NS = self.NS
-        self.bw = nq * dn + nq * (d // 2)
-        pin = torch.cuda.is_available()
-        self.h_stage = [torch.zeros((self.bw,), dtype=torch.int32, pin_memory=pin) for _ in range(NS)]
-        self.d_blk = [torch.empty((self.bw,), dtype=torch.int32, device=dev) for _ in range(NS)]
-        self.q32 = [torch.empty((nq, d), dtype=torch.float32, device=dev) for _ in range(NS)]
-        self.cls = [torch.empty((nq, R), dtype=torch.int32, device=dev) for _ in range(NS)]
-        wsb = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
-            C.byref(ix.desc), nq, R, kl, _lib.LMI_Q_F16)
-        self.ws = [torch.empty(max(int(wsb), 256), dtype=torch.uint8, device=dev) for _ in range(NS)]
-        self.ans = [answer_buffer(nq, self.w, dev) for _ in range(NS)]
-        self.h_ans = [torch.empty((3 * nq * self.w + 2,), dtype=torch.int32, pin_memory=pin)
-                      for _ in range(NS)]
-        ldt = torch.float64 if f64 else torch.float32
-        if self.G > 1:
-            from .dist import packed_lists
-            self.pk = [packed_lists(nq * R, kl, f64, dev) for _ in range(NS)]
-            self.lists = [(b[1].view(nq, R, kl), b[2].view(nq, R, kl), b[3]) for b in self.pk]
-        else:
-            self.pk = None
-            self.lists = [(torch.empty((nq, R, kl), dtype=ldt, device=dev),
-                           torch.empty((nq, R, kl), dtype=torch.int32, device=dev),
-                           self.ans[j][3][0:1]) for j in range(NS)]
-        bsz, p2id = s._device_tables()
-        seed = use_threshold and k <= k_round and _SEED_ROUND0
-        scan_fn = bucket_topk_f64 if f64 else bucket_topk
-        self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
-
-        def phase(j, ph):
-            dl, pl, st = self.lists[j]
-            scan_fn(ix, self.q32[j], self.cls[j], kl, qmode=_lib.LMI_Q_F16, out=(dl, pl, st),
-                    ws=self.ws[j], seed_round0=seed, phases=ph)
-
-        def upload(j):
-            self.d_blk[j].copy_(self.h_stage[j], non_blocking=True)
-
-        def route(j):
-            # (the staged rows are in d_blk[j]: upload(j) ran before, on the
-            # copy stream in a launch)
-            blk = self.d_blk[j]
-            s.router.topr(blk[:nq * dn].view(torch.float32).view(nq, dn), R, out=self.cls[j])
-
-        def plan(j):
-            self.lists[j][2].zero_()
-            self.q32[j].copy_(self.d_blk[j][nq * dn:].view(torch.float16).view(nq, d))
-            phase(j, _lib.LMI_Q_PHASE_PLAN)
-
-        def scan(j):
-            phase(j, _lib.LMI_Q_PHASE_SCAN)
-
-        def finish(j):
-            phase(j, _lib.LMI_Q_PHASE_MERGE)
-            buf, ad, aa, ast = self.ans[j]
-            ast[1:2].zero_()
-            if self.G > 1:
-                from .dist import gather_merge_packed
-                dd, pp, _ = gather_merge_packed(self.pk[j][0], nq * R, kl, f64, s.group,
-                                                status_out=ast[0:1])
-                dd, pp = dd.view(nq, R, kl), pp.view(nq, R, kl)
-            else:
-                dd, pp = self.lists[j][0], self.lists[j][1]
-            replay_device(self.cls[j], dd, pp, k_round=k_round, k_final=k, bucket_size=bsz,
-                          pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]))
-            self.h_ans[j].copy_(buf, non_blocking=True)
-
-        self._upload, self._route, self._plan, self._scan, self._finish = upload, route, plan, scan, finish
-        # five streams: uploads (the copy engine), route, plan, scan (the
-        # caller's stream), finish; per-slot events order them across launches
-        self._cs = torch.cuda.Stream(dev)
-        self._rs = torch.cuda.Stream(dev)
-        self._ps = torch.cuda.Stream(dev)
-        self._fs = torch.cuda.Stream(dev)
-        ev = lambda: [torch.cuda.Event() for _ in range(NS)]
-        self._up, self._rdone, self._pdone, self._sdone, self._fdone = ev(), ev(), ev(), ev(), ev()
-        self.graphs = None
-        self._t = None  # launch counter once primed
-        # the next launch's scan enqueued ahead (its plan ran a launch
-        # earlier), waiting on the device for this launch's finish
-        # (lookahead="finish", the default): no host round trip before it, and
-        # it does not take the CUs the route / plan / finish chains wait for.
-        # Same box (profiles/r03_stream_lookahead3_ab.txt): one GPU 7.03-7.04 ms
-        # per launch against 7.08-7.09 with the scan right behind the last one
-        # (True) and 7.15-7.16 without lookahead (False); a stripe of 8
-        # 1.25-1.26 / 1.23-1.24 / 1.26-1.27 (True was the slowest on another box)
-        self.lookahead = "finish" if lookahead is None else lookahead
-        self._s_ahead = False  # the next launch's scan is already enqueued
-        if not self.stage(nav, qs):
-            raise ValueError("the batch stream needs fp16-exact query batches")
-        for j in range(NS):
-            self.h_stage[j].copy_(self.h_stage[0])
-        # warm-up: one eager pass of every branch on every slot (allocations,
-        # kernel attributes, communicators), in pipeline order, on a side stream
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        err = None
-        try:
-            with torch.cuda.stream(side):
-                for j in range(NS):
-                    upload(j)
-                    route(j)
-                    plan(j)
-                    scan(j)
-                    finish(j)
-            torch.cuda.current_stream(dev).wait_stream(side)
-            torch.cuda.synchronize(dev)
-        except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
-            err = e
-        if self.G > 1:
-            ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
-            torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
-            if int(ok.item()) == 0:
-                raise RuntimeError(f"stream warm-up failed on some rank: {err!r}")
-        elif err is not None:
-            raise err
-        if capture:
-            # one graph per (stage, slot): route, plan, scan and finish each a chain
-            self.graphs = {}
-            for name, fn in (("R", route), ("P", plan), ("S", scan), ("F", finish)):
-                for j in range(NS):
-                    gr = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gr):
-                        fn(j)
-                    self.graphs[name, j] = gr
-            torch.cuda.synchronize(dev)
-
-    def stage(self, q_nav, q_search, slot: Optional[int] = None) -> bool:
-        """Write a batch into the pinned staging rows of `slot` (default: the
-        slot the next launch plans).  False if a clip768 value is not
-        fp16-representable (the stream cannot take that batch)."""
-        nav = _host_array(q_nav).astype(np.float32, copy=False)
-        qs = _host_array(q_search)
-        nq, d, dn = self.nq, self.d, self.dn
-        if nav.shape != (nq, dn) or qs.shape != (nq, d):
-            raise ValueError("a staged batch must have the stream's shape")
-        if qs.dtype == np.float16:
-            q16 = qs
-        else:
-            q32 = qs.astype(np.float32, copy=False)
-            q16 = q32.astype(np.float16)
-            if not np.array_equal(q16.astype(np.float32), q32):
-                return False
-        if slot is None:
-            slot = (self._t or 0) % self.NS
-        blk = self.h_stage[slot].numpy()
-        blk[:nq * dn].view(np.float32).reshape(nq, dn)[:] = nav
-        blk[nq * dn:].view(np.float16).reshape(nq, d)[:] = q16
-        return True
-
-    def prime(self):
-        """Fill the pipeline with the staged rows of slots 1, 2 and 3 (eagerly:
-        slot 1 up to its scan, slots 2 and 3 up to their plans): the next
-        launch answers slot 1."""
-        dev = self.searcher.index.device
-        for j, upto in ((1, 3), (2, 2), (3, 2)):
-            self._upload(j)
-            for f in (self._route, self._plan, self._scan)[:upto]:
-                f(j)
-        torch.cuda.current_stream(dev).synchronize()
-        self._t = 0
-        self._s_ahead = False
-
-    def _run(self, name, j):
-        if self.graphs is not None:
-            self.graphs[name, j].replay()
-        else:
-            {"R": self._route, "P": self._plan, "S": self._scan, "F": self._finish}[name](j)
-
-    def step(self):
-        """One launch -> (dists f64 [nq, w], anns uint32 [nq, w]) of the batch
-        it finished (numpy views, valid for the next three launches).  Slot
-        t mod 4 is uploaded and routed (stage() before step() streams a new
-        batch; without it the slot's previous rows are used again) and
-        planned, slot t + 2 scanned and t + 1 finished (mod 4), on five streams
-        ordered by per-slot events:
-
-            copy:   H2D of slot t                      (the copy engine)
-            route:  wait H2D -> router (slot t)
-            plan:   wait route -> widen, K2 PLAN (slot t)
-            scan:   wait plan(two launches ago) -> K2 SCAN (slot t+2)
-            finish: wait scan(last launch) -> merge [all-gather + K3],
-                    replay, D2H (slot t+1)
-
-        The scan holds every CU while it runs; the latency-bound chains start
-        in its tail.  With `lookahead` the next launch's scan, of a slot
-        planned a launch earlier, is enqueued too: right behind this scan
-        (True), or (the default, "finish") behind this launch's finish on the
-        device, without a host round trip."""
-        if self._t is None:
-            self.prime()
-        dev = self.searcher.index.device
-        NS = self.NS
-        g = self._t % NS
-        jr, js, jf = g, (g + 2) % NS, (g + 1) % NS
-        main = torch.cuda.current_stream(dev)
-        # (d_blk[jr] was last read by the plan three launches ago, which the
-        # finish the host waited for in the last step depended on)
-        with torch.cuda.stream(self._cs):
-            self._upload(jr)
-        self._up[jr].record(self._cs)
-        if not self._s_ahead:
-            main.wait_event(self._pdone[js])
-            self._run("S", js)
-            self._sdone[js].record(main)
-        self._rs.wait_event(self._up[jr])
-        with torch.cuda.stream(self._rs):
-            self._run("R", jr)
-        self._rdone[jr].record(self._rs)
-        self._ps.wait_event(self._rdone[jr])
-        with torch.cuda.stream(self._ps):
-            self._run("P", jr)
-        self._pdone[jr].record(self._ps)
-        self._fs.wait_event(self._sdone[jf])
-        with torch.cuda.stream(self._fs):
-            self._run("F", jf)
-        self._fdone[jf].record(self._fs)
-        if self.lookahead:
-            # the next launch's scan: slot t+3, planned in the last launch (in
-            # the tail of its scan), so it follows this scan at once
-            jn = (g + 3) % NS
-            main.wait_event(self._pdone[jn])
-            if self.lookahead == "finish":
-                main.wait_event(self._fdone[jf])
-            elif self.lookahead == "plan":  # (a study: gate on this launch's plan)
-                main.wait_event(self._pdone[jr])
-            self._run("S", jn)
-            self._sdone[jn].record(main)
-        self._s_ahead = bool(self.lookahead)
-        self._t += 1
-        if self.G > 1 and self.graphs is not None:
-            _wait_event_with_deadline(self._fdone[jf], self.timeout_s)
-        else:
-            self._fdone[jf].synchronize()
-        return self._answer(jf)
-
-    def _answer(self, j):
-        hd, ha, st, rst = answer_views(self.h_ans[j], self.nq, self.w)
-        if st & (_lib.LMI_STATUS_INTERNAL | _lib.LMI_STATUS_QUERY_NOT_F16) or rst:
-            raise RuntimeError(f"stream: status {st}/{rst}")
-        return hd, ha
-
-    def stream(self, batches):
-        """Answer an iterable of (q_nav, q_search) batches in order, yielding
-        (dists, anns) copies per batch: three batches fill the pipeline, then
-        one launch per batch, then the last three finish eagerly."""
-        dev = self.searcher.index.device
-        NS = self.NS
-        sync = lambda: torch.cuda.current_stream(dev).synchronize()
-        ans = lambda j: tuple(a.copy() for a in self._answer(j))
-        it = iter(batches)
-        first = []
-        for b in it:
-            first.append(b)
-            if len(first) == NS - 1:
-                break
-        for j, b in zip(range(1, NS), first):
-            if not self.stage(*b, slot=j):
-                raise ValueError("the batch stream needs fp16-exact query batches")
-        if len(first) < NS - 1:
-            for j in range(1, 1 + len(first)):
-                self._upload(j); self._route(j); self._plan(j); self._scan(j); self._finish(j); sync()
-                yield ans(j)
-            return
-        self.prime()
-        for b in it:
-            if not self.stage(*b, slot=self._t % NS):
-                raise ValueError("the batch stream needs fp16-exact query batches")
-            yield tuple(a.copy() for a in self.step())
-        # drain: slot t+1 is scanned, t+2 and t+3 planned (mod 4; t+2's scan
-        # enqueued when lookahead), t the launch count
-        torch.cuda.synchronize(dev)  # (every stream of the last launch)
-        t = self._t
-        j1, j2, j3 = (t + 1) % NS, (t + 2) % NS, (t + 3) % NS
-        self._finish(j1); sync()
-        yield ans(j1)
-        if not self._s_ahead:
-            self._scan(j2)
-        self._finish(j2); sync()
-        yield ans(j2)
-        self._scan(j3); self._finish(j3); sync()
-        yield ans(j3)
-        self._t = None
-        self._s_ahead = False
-
-def _wait_event_with_deadline(ev, timeout_s: float) -> None:
-    """_wait_with_deadline on a recorded event."""
-    deadline = time.monotonic() + timeout_s
-    spins = 0
-    while not ev.query():
-        spins += 1
-        if spins > 1000:
-            if time.monotonic() > deadline:
-                raise RuntimeError(f"search step not finished after {timeout_s:.0f} s: a peer rank "
-                                   "stopped inside the step's collectives; end this process")
-            time.sleep(1e-4)
-
-
-def _wait_with_deadline(dev, timeout_s: float) -> None:
-    """Wait for the current stream's work, raising after `timeout_s`: a graph
-    replay whose all-gather waits for a rank that died never completes, and
-    RCCL kernels captured in a graph are outside the process group's watchdog
-    (li.dist.init_from_env).  The caller should end the process: the stalled
-    kernels stay queued on the device until its context is torn down."""
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(dev))
-    deadline = time.monotonic() + timeout_s
-    spins = 0
-    while not ev.query():
-        spins += 1
-        if spins > 1000:
-            if time.monotonic() > deadline:
-                raise RuntimeError(f"search step not finished after {timeout_s:.0f} s: a peer rank "
-                                   "stopped inside the step's collectives; end this process")
-            time.sleep(1e-4)
-
-
-def _np_fp16_exact(x: np.ndarray) -> bool:
-    """True when every value of a host array round-trips through fp16."""
-    x = np.asarray(x)
-    if x.dtype == np.float16:
-        return True
-    x32 = x.astype(np.float32, copy=False)
-    if x.dtype != np.float32 and not np.array_equal(x32.astype(x.dtype), x):
-        return False
-    return bool(np.array_equal(x32.astype(np.float16).astype(np.float32), x32))

@@ -216,3 +216,40 @@ def build_random_workload(n: int, nq: int, n_buckets: int, arch: str, device, *,
         labels[a:b] = router.argmax(torch_nav(blk, P)).to(torch.int32)
         del blk
     return src, q, qn, layers, labels
+
+
+# ---------------------------------------------------------------------------
+# a stream of distinct query batches for the same workload
+# ---------------------------------------------------------------------------
+@torch.no_grad()
+def query_batches(n_batches: int, nq: int, device, *, kind: str = "mixture", d: int = 768,
+                  centres: int = 400, seed: int = 2023):
+    """n_batches distinct (q f32 [nq, d] fp16-exact, qn f32 [nq, 96]) batches
+    on `device`, from the same distribution as the workload's queries: batch 0
+    IS the workload's batch (build_lmi_workload's, or build_random_workload's
+    with kind="random"); batch i > 0 draws from its own seed.  The mixture's
+    centres and the pca96 projection are regenerated from their seeds (the
+    first draws of the same generators), so nothing else of the workload is
+    needed."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(96)
+    P = (torch.randn((d, 96), generator=g) / math.sqrt(d)).to(device)
+    out = []
+    if kind == "mixture":
+        gc = torch.Generator(device=device)
+        gc.manual_seed(seed)
+        cen = torch.randn((centres, d), generator=gc, device=device)
+        for i in range(n_batches):
+            q, _ = torch_mixture(nq, d, centres, seed=seed + 2219 + 7919 * i, device=device,
+                                 centres=cen, out_dtype=torch.float32)
+            out.append((q, torch_nav(q, P)))
+    elif kind == "random":
+        for i in range(n_batches):
+            gq = torch.Generator(device=device)
+            gq.manual_seed(seed + 2219 + 7919 * i)
+            q = torch.randn((nq, d), generator=gq, device=device)
+            q = (q / q.norm(dim=1, keepdim=True)).half().float()
+            out.append((q, torch_nav(q, P)))
+    else:
+        raise ValueError("kind must be 'mixture' or 'random'")
+    return out

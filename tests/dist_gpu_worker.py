@@ -13,6 +13,9 @@ sys.path[:0] = [os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"),
                 os.path.join(ROOT, "oracle"), HERE]
 
 
+N_BATCHES = 7
+
+
 def main(out_path):
     import numpy as np
     import torch
@@ -46,14 +49,33 @@ def main(out_path):
         g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_, capture=False)
         d, a = g.run()
         res[f"graph_{dist_}_d"], res[f"graph_{dist_}_a"] = d.copy(), a.copy()
-    # the batch stream's G > 1 path (every rank uploads and routes the whole
-    # batch; the list exchange in the finish branch), its branches launched
-    # eagerly over gloo: three distinct batches
-    perms = [np.random.default_rng(70 + i).permutation(w["q"].shape[0]) for i in range(3)]
+    # repeated graph steps on new staged batches (the sharded upload + one
+    # all-gather of queries and classes per step)
+    perms = [np.random.default_rng(70 + i).permutation(w["q"].shape[0]) for i in range(N_BATCHES)]
+    batches = [(w["qn"][p], w["q"][p]) for p in perms]
+    for dist_ in ("f32", "f64"):
+        g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_, capture=False)
+        for i, b in enumerate(batches[:3]):
+            d, a = g.run(*b)
+            res[f"graphrun_{dist_}_{i}_d"], res[f"graphrun_{dist_}_{i}_a"] = d.copy(), a.copy()
+    # the batch stream's G > 1 path (each rank stages and uploads its block of
+    # the batch and routes it; one all-gather per launch carries the lists of
+    # one batch with the blocks of the next), its stages launched eagerly over
+    # gloo: N_BATCHES distinct batches, so StreamedSearch.step() itself runs
+    # (N_BATCHES - 3 launches after the fill) before the drain
     for dist_ in ("f32", "f64"):
         st = s.streamed(w["qn"], w["q"], 4, k=10, dist=dist_, capture=False)
-        for i, (d, a) in enumerate(st.stream([(w["qn"][p], w["q"][p]) for p in perms])):
+        for i, (d, a) in enumerate(st.stream(batches)):
             res[f"stream_{dist_}_{i}_d"], res[f"stream_{dist_}_{i}_a"] = d, a
+        res[f"stream_{dist_}_launches"] = np.array([st.launches])
+    # the bench's use: stage() + step() per launch, a new batch each time,
+    # one batch not fp16-exact (answered by Searcher.search on every rank)
+    st = s.streamed(w["qn"], w["q"], 4, k=10, capture=False)
+    odd = (batches[1][0], batches[1][1] + np.float32(1e-5))
+    seq = [batches[i % 4] for i in range(7)]
+    seq[5] = odd
+    for i, (d, a) in enumerate(st.stream(seq)):
+        res[f"stream_odd_{i}_d"], res[f"stream_odd_{i}_a"] = d, a
     if rank == 0:
         np.savez(out_path, **res)
     dist.barrier()

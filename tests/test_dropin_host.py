@@ -47,3 +47,32 @@ def test_attached_rewrite_skipped_only_when_unchanged():
     assert np.array_equal(d["category"].to_numpy(), other)
     li.detach()
     assert li._cat_written is None
+
+
+def test_attached_index_served_only_for_the_attached_objects():
+    """The trust of attach(): the cached HBM index is served
+    without a content hash only for the very objects attached -- held by
+    strong references, so a new frame cannot inherit a freed one's id() or
+    buffer address -- and only while their value arrays are where they were."""
+    li = LearnedIndex()
+    nav, ds = _frame(), _frame()
+    lab = np.arange(1000) % 7
+    li._index, li._cache_key = object(), ("key",)
+    li._trusted = (li._identity(nav, ds, lab), li._cache_key, (ds, lab, nav.index))
+    assert li._is_attached(nav, ds, lab)
+    assert not li._is_attached(nav, ds.copy(), lab)          # equal values, another object
+    assert not li._is_attached(nav, ds, lab.copy())
+    nav2 = nav.copy()
+    assert not li._is_attached(nav2, ds, lab)                # another index object
+    li._cache_key = ("other",)                               # the cache was rebuilt
+    assert not li._is_attached(nav, ds, lab)
+    li._cache_key = ("key",)
+    ds[4] = 1.0                                              # a new column: new value arrays
+    assert not li._is_attached(nav, ds, lab)
+    # the trust holds the objects alive: dropping the caller's names frees nothing
+    import weakref
+    r = weakref.ref(lab)
+    del lab
+    assert r() is not None
+    li.detach()
+    assert li._trusted is None

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 import torch
 
+import dist_gpu_worker
 import workloads
 from li.index import DeviceIndex, DeviceRouter, Searcher
 
@@ -64,10 +65,23 @@ def test_two_process_product_path_equals_one_process(world, tmp_path):
         d, a = s.graph(w["qn"], w["q"], 4, k=10, dist=dist_).run()
         np.testing.assert_array_equal(got[f"graph_{dist_}_d"], d)
         np.testing.assert_array_equal(got[f"graph_{dist_}_a"], a)
-    perms = [np.random.default_rng(70 + i).permutation(w["q"].shape[0]) for i in range(3)]
+    perms = [np.random.default_rng(70 + i).permutation(w["q"].shape[0])
+             for i in range(dist_gpu_worker.N_BATCHES)]
+    batches = [(w["qn"][p], w["q"][p]) for p in perms]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     for dist_ in ("f32", "f64"):
-        for i, p in enumerate(perms):
-            d, a = s.search(torch.from_numpy(w["qn"][p]).cuda(), torch.from_numpy(w["q"][p]).cuda(),
-                            4, k=10, dist=dist_)
+        ref = [s.search(T(a), T(b), 4, k=10, dist=dist_) for a, b in batches]
+        for i in range(3):
+            np.testing.assert_array_equal(got[f"graphrun_{dist_}_{i}_d"], ref[i][0])
+            np.testing.assert_array_equal(got[f"graphrun_{dist_}_{i}_a"], ref[i][1])
+        for i, (d, a) in enumerate(ref):
             np.testing.assert_array_equal(got[f"stream_{dist_}_{i}_d"], d)
             np.testing.assert_array_equal(got[f"stream_{dist_}_{i}_a"], a)
+        # step() itself ran: one launch per batch after the three that fill
+        assert int(got[f"stream_{dist_}_launches"][0]) == dist_gpu_worker.N_BATCHES - 3
+    seq = [batches[i % 4] for i in range(7)]
+    seq[5] = (batches[1][0], batches[1][1] + np.float32(1e-5))
+    for i, (a_, b_) in enumerate(seq):
+        d, a = s.search(T(a_), T(b_), 4, k=10)
+        np.testing.assert_array_equal(got[f"stream_odd_{i}_d"], d)
+        np.testing.assert_array_equal(got[f"stream_odd_{i}_a"], a)

@@ -14,20 +14,6 @@ from li.index import replay, replay_device
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["rounds", "flow"], autouse=True)
-def replay_path(request, monkeypatch):
-    """Every test on both device paths: the per-round launches (the default)
-    and all rounds as one dataflow launch (LMI_REPLAY_FLOW=1, a study)."""
-    from li import _lib
-    monkeypatch.delenv("LMI_REPLAY_FLOW", raising=False)
-    if request.param == "flow":
-        monkeypatch.setenv("LMI_REPLAY_FLOW", "1")
-    _lib.load().lmi_config_reload()
-    yield request.param
-    monkeypatch.undo()
-    _lib.load().lmi_config_reload()
-
-
 def _random_lists(seed, nq, R, C, kl, tiny=(), empty=(), probe_empty=False):
     rng = np.random.default_rng(seed)
     size = rng.integers(40, 400, C).astype(np.int64)

@@ -1,7 +1,8 @@
-"""StreamedSearch (the step as a three-stage pipeline of captured graphs over a
-stream of batches: route of batch b+3, plan of b+2, scan of b+1, merge/replay/D2H of b in
-one launch) answers every batch exactly as Searcher.search does; the phase
-flags of lmi_bucket_topk (ABI 7) compose to the one-call result."""
+"""StreamedSearch (li.stream: the step as a four-stage pipeline of captured graphs
+over a stream of batches -- route and plan of batch t, scan of t-2,
+merge/replay/D2H of t-3 in one launch) answers every batch exactly as
+Searcher.search does; the phase flags of lmi_bucket_topk (ABI 7) compose to
+the one-call result."""
 import numpy as np
 import pytest
 import torch
@@ -100,7 +101,7 @@ def test_stream_rejects_inexact_batches(setup):
         s.streamed(w["qn"], w["q"] + np.float32(1e-5), 4, k=10)
 
 
-@pytest.mark.parametrize("lookahead", [False, True, "finish"])
+@pytest.mark.parametrize("lookahead", [False, True])
 def test_stream_with_and_without_lookahead(setup, lookahead):
     """The next launch's scan enqueued ahead (the default) or not: the same
     answers, batch by batch, and over repeated steps."""
@@ -116,4 +117,49 @@ def test_stream_with_and_without_lookahead(setup, lookahead):
     st = s.streamed(w["qn"], w["q"], 4, k=10, lookahead=lookahead)
     for _ in range(4):
         d, a = st.step()
+        np.testing.assert_array_equal(a, a0)
+
+
+@pytest.mark.parametrize("where", [0, 2, 5])
+def test_inexact_batch_in_a_stream_is_answered_eagerly(setup, where):
+    """A batch whose clip768 values fp16 cannot hold, in the middle of a stream
+    (or in the pipeline fill): staged with its flag, the launch that finishes it
+    raises QueryNotF16, and stream() answers it by Searcher.search (exact fp32
+    MFMA); every other batch still comes from the stream, all equal to search."""
+    w, s = setup
+    bs = _batches(w, 7, seed=90 + where)
+    bs[where] = (bs[where][0], bs[where][1] + np.float32(1e-5))
+    ref = [s.search(T(a), T(b), 4, k=10) for a, b in bs]
+    got = list(s.streamed(w["qn"], w["q"], 4, k=10).stream(bs))
+    assert len(got) == len(bs)
+    for (d, a), (d0, a0) in zip(got, ref):
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+
+
+def test_step_raises_on_an_inexact_staged_batch(setup):
+    from li.stream import QueryNotF16
+    w, s = setup
+    st = s.streamed(w["qn"], w["q"], 4, k=10)
+    d0, a0 = s.search(T(w["qn"]), T(w["q"]), 4, k=10)
+    st.step()
+    assert not st.stage(w["qn"], w["q"] + np.float32(1e-5))   # the slot of launch 1
+    for _ in range(3):                                         # launches 1-3 finish slots 2, 3, 0
+        d, a = st.step()
+        np.testing.assert_array_equal(a, a0)
+    with pytest.raises(QueryNotF16):
+        st.step()                                              # launch 4 finishes it
+    d, a = st.step()                                           # the stream goes on
+    np.testing.assert_array_equal(a, a0)
+
+
+def test_stream_of_float16_host_batches(setup):
+    """Batches held as float16 host arrays (the real clip768 'emb' dtype) are
+    staged by a copy; answers equal search on the same values."""
+    w, s = setup
+    bs = [(a, b.astype(np.float16)) for a, b in _batches(w, 6, seed=123)]
+    ref = [s.search(T(a), T(b.astype(np.float32)), 4, k=10) for a, b in bs]
+    got = list(s.streamed(w["qn"], w["q"], 4, k=10).stream(bs))
+    for (d, a), (d0, a0) in zip(got, ref):
+        np.testing.assert_array_equal(d, d0)
         np.testing.assert_array_equal(a, a0)

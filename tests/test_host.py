@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 8
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
@@ -198,3 +198,57 @@ def test_search_path_initialises_workspace_with_kernels():
                  "lmi_replay_gpu.hip", "lmi_router.hip", "lmi_abi.cpp"):
         src = open(os.path.join(csrc, name)).read()
         assert not re.search(r"\bhipMemset\w*\s*\(", src), name
+
+
+@pytest.mark.parametrize("scalar", [False, True])
+def test_host_stage_f16_matches_numpy(scalar, monkeypatch):
+    """lmi_host_stage_f16 (the batch stream's staging of a float32 host batch):
+    numpy's float16 rounding bit for bit, and its exactness flag equals numpy's
+    array_equal(q.astype(f16).astype(f32), q) -- on normals, subnormals, the
+    rounding ties, overflow to inf, signed zeros and NaN, with the F16C path
+    and the scalar one (LMI_HOST_SCALAR=1)."""
+    import numpy as np
+    from li import _lib
+    if scalar:
+        monkeypatch.setenv("LMI_HOST_SCALAR", "1")
+    lib = _lib.load()
+    rng = np.random.default_rng(11)
+    h = rng.integers(0, 1 << 16, 300_001, dtype=np.uint16).view(np.float16)
+    exact = h.astype(np.float32)
+    exact = exact[~np.isnan(exact)]
+    # every half value, ties between neighbours, values between, and extremes
+    a = np.concatenate([exact, exact * np.float32(1 + 2 ** -11), exact * np.float32(1 + 2 ** -12),
+                        exact * np.float32(1 + 3 * 2 ** -13),
+                        rng.standard_normal(100_000).astype(np.float32) * np.float32(2.0) **
+                        rng.integers(-30, 20, 100_000).astype(np.float32),
+                        np.array([65504, 65519.99, 65520, -65520, 1e30, -0.0, 0.0, 2 ** -25,
+                                  2 ** -25 * 1.0001, 2 ** -24, 3 * 2 ** -25, np.inf, -np.inf],
+                                 np.float32)])
+    with np.errstate(over="ignore"):
+        ref = a.astype(np.float16)
+    out = np.empty(a.size, np.uint16)
+    for t in (1, 3, 0):
+        out[:] = 0
+        assert lib.lmi_host_stage_f16(a.ctypes.data, a.size, out.ctypes.data, t) == 0
+        np.testing.assert_array_equal(out, ref.view(np.uint16))
+    ok = exact.astype(np.float32)
+    out = np.empty(ok.size, np.uint16)
+    assert lib.lmi_host_stage_f16(ok.ctypes.data, ok.size, out.ctypes.data, 0) == 1
+    np.testing.assert_array_equal(out, ok.astype(np.float16).view(np.uint16))
+    nan = np.array([1.0, np.nan], np.float32)
+    o2 = np.empty(2, np.uint16)
+    assert lib.lmi_host_stage_f16(nan.ctypes.data, 2, o2.ctypes.data, 1) == 0
+    assert np.isnan(o2.view(np.float16)[1])
+    assert lib.lmi_host_stage_f16(None, 4, o2.ctypes.data, 1) == -_lib.LMI_E_INVALID
+    assert lib.lmi_host_stage_f16(None, 0, None, 1) == 1
+
+
+def test_host_copy():
+    import numpy as np
+    from li import _lib
+    lib = _lib.load()
+    a = np.random.default_rng(2).integers(0, 256, (5 << 20) + 77, dtype=np.uint8)
+    b = np.zeros_like(a)
+    assert lib.lmi_host_copy(b.ctypes.data, a.ctypes.data, a.nbytes, 0) == 0
+    np.testing.assert_array_equal(a, b)
+    assert lib.lmi_host_copy(None, a.ctypes.data, 5, 1) == _lib.LMI_E_INVALID

@@ -58,15 +58,7 @@ else:
     classes, d, pos, size, ids = _random_lists(3, nq=10000, R=4, C=122, kl=10)
     args = [torch.from_numpy(x).to(dev) for x in (classes, d, pos)]
     bsz, p2id = torch.from_numpy(size).to(dev), torch.from_numpy(ids).to(dev)
-runs = [(abl, m) for m in ("rounds", "flow") for abl in os.environ.get("ABLS", "0").split(",")]
-for abl, mode in runs:
-    # rounds: the per-round launches (default); flow: all rounds in one
-    # dataflow launch (LMI_REPLAY_FLOW, a study)
-    os.environ["LMI_REPLAY_ABL"] = abl
-    os.environ.pop("LMI_REPLAY_FLOW", None)
-    if mode == "flow":
-        os.environ["LMI_REPLAY_FLOW"] = "1"
-    _lib.load().lmi_config_reload()
+for _ in (0,):
     fn = lambda: replay_device(*args, k_round=10, k_final=10, bucket_size=bsz, pos_to_id=p2id,
                                use_threshold=True)
     for _ in range(3):
@@ -78,4 +70,4 @@ for abl, mode in runs:
         fn()
     e1.record()
     torch.cuda.synchronize()
-    print(f"replay {mode} abl={abl}: {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us", flush=True)
+    print(f"replay (per-round launches): {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us", flush=True)

@@ -12,7 +12,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--worlds", default="1,8")
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--eager", action="store_true", help="launch the three branches eagerly on three streams")
-ap.add_argument("--modes", default="stream", help="comma list of stream (default lookahead), stream-nola (none), stream-la (ahead), stream-fin (after the finish), stream-eager, graph-pipe, graph")
+ap.add_argument("--modes", default="stream", help="comma list of stream (default: lookahead behind the finish), stream-nola (no lookahead), stream-eager, graph-pipe, graph")
 ap.add_argument("--dist", default="f32", choices=["f32", "f64"])
 ap.add_argument("--chunks", default="", help="comma list of chunk rows to try (default: the bench's by W)")
 a = ap.parse_args()
@@ -32,8 +32,7 @@ for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
     for mode in a.modes.split(","):
         if mode.startswith("stream"):
             st = s.streamed(qn, q, 4, k=10, dist=a.dist, capture=not (a.eager or mode == "stream-eager"),
-                            lookahead={"stream-nola": False, "stream-la": True,
-                                       "stream-fin": "finish", "stream-plan": "plan"}.get(mode))
+                            lookahead=mode != "stream-nola")
             fn = st.step
         else:
             st = s.graph(qn, q, 4, k=10, dist=a.dist, pipeline=mode == "graph-pipe")
