@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4, session b: the float64 mode's scan lists, 12-entry (product) vs 15
+# round 4, session b: the float64 mode's scan lists, 11-entry (product) vs 15
 # (liblmi_hip_kl15.so), per launch of the batch stream at W = 1 and rank 0 of
 # W = 8, f32 beside; then a kernel trace of the W = 8 float64 stream.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp; mkdir -p gpurun_out/r4b
