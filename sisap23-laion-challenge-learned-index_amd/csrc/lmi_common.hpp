@@ -56,11 +56,7 @@ void set_error(const char* fmt, ...);
 // "empty" (sorts after every finite and infinite distance).
 // scan list length of the float64 mode (k <= 10): 10 + guard entries for the
 // refinement band (lmi_refine.hip); a per-lane list walk in scan v3
-#ifndef LMI_F64KL
-#define LMI_F64KL 11  // (`make f64kl15`: round 3's 15-entry cooperative lists, for A/B runs)
-#endif
-constexpr int kF64KL = LMI_F64KL;
-static_assert(kF64KL == 11 || kF64KL == 12 || kF64KL == 15, "kF64KL");
+constexpr int kF64KL = 11;
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __host__ __device__ inline uint32_t f2ord(float f) {
