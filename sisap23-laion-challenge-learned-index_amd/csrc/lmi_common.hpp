@@ -54,9 +54,6 @@ void set_error(const char* fmt, ...);
 // (distance, position) order (LearnedIndex.py:170 argsort of a row whose
 // columns are in g.index order; :91 stable merge), and the all-ones key is
 // "empty" (sorts after every finite and infinite distance).
-// scan list length of the float64 mode (k <= 10): 10 + guard entries for the
-// refinement band (lmi_refine.hip); a per-lane list walk in scan v3
-constexpr int kF64KL = 11;
 constexpr uint64_t kEmptyKey = ~0ull;
 
 __host__ __device__ inline uint32_t f2ord(float f) {

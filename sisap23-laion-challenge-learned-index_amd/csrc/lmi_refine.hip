@@ -335,18 +335,14 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
 
 struct RefineWs {
     size_t scan, ld, lrow, lpos, failed, nfailed, total;
-    int kl;       // scan list length refined (kF64KL for k <= 10; else >= k + 5)
+    int kl;       // scan list length refined (>= k + 5, or 15 for k <= 10)
     int passes;   // 0: one scan of kl entries, else lower-bound passes
 };
 
 RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     RefineWs w{};
-    if (k <= 10) {
-        // 10 + guard entries (kF64KL): a per-lane list walk in scan v3 (15
-        // entries need its cooperative update: +0.5 ms at 10M); a band of
-        // kF64KL or more entries within 2 eps of the k-th goes to the exact
-        // fallback
-        w.kl = kF64KL;
+    if (k + 5 <= 15) {
+        w.kl = 15;
         w.passes = 0;
     } else {
         int kp;

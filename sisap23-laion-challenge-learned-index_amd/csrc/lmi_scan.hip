@@ -703,16 +703,13 @@ bool v3_capable(const lmi_index_desc* idx, int qmode) {
 // mode's 10 + 5 guard entries), else 16
 int pick_kl(const lmi_index_desc* idx, int qmode, int k) {
     if (k <= 10) return 10;
-    // kF64KL: the float64 mode's 10 + guard entries (lmi_refine.hip), still a
-    // per-lane list walk; 15: the k > 16 passes and the other k <= 15 (cooperative)
-    if (k <= kF64KL && v3_capable(idx, qmode)) return kF64KL;
     if (k <= 15 && v3_capable(idx, qmode)) return 15;
     return 16;
 }
 
 bool v3_eligible(const lmi_index_desc* idx, int qmode, int k) {
     const int kl = pick_kl(idx, qmode, k);
-    return v3_capable(idx, qmode) && (kl == 10 || kl == kF64KL || kl == 15);
+    return v3_capable(idx, qmode) && (kl == 10 || kl == 15);
 }
 
 WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, bool lo = false) {
@@ -1108,9 +1105,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
             rc = launch_scan3_v<15, 0, true>(b, s);
         }
         else if (w.use_v3)
-            rc = (KL == 10)       ? launch_scan3<10>(b, s)
-                 : (KL == kF64KL) ? launch_scan3<kF64KL>(b, s)
-                                  : launch_scan3<15>(b, s);
+            rc = (KL == 10) ? launch_scan3<10>(b, s) : launch_scan3<15>(b, s);
         else
             rc = (KL == 10) ? launch_scan2<10>(b, s) : launch_scan2<16>(b, s);
     } else if (LOP) {
@@ -1142,8 +1137,6 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                        out_d, out_pos, out_row, idx->n_rows, status, split_mask, w.split_s)
     if (KL == 10) {
         if (out_row) LMI_CM(10, true); else LMI_CM(10, false);
-    } else if (KL == kF64KL) {
-        if (out_row) LMI_CM(kF64KL, true); else LMI_CM(kF64KL, false);
     } else if (KL == 15) {
         if (out_row) LMI_CM(15, true); else LMI_CM(15, false);
     } else {

@@ -68,9 +68,8 @@ constexpr int NSLOT = 2 * NST;         // two blocks: one read, the next in flig
 constexpr int NW = 8;
 constexpr int QB = NW * 32;
 constexpr int NQF = D / 16;
-// lists of KL = 10 (k <= 10), 12 (the float64 mode's 10 + 2 guard entries) or
-// 15 (k of 13-15 and the k > 16 passes; the most the 160-KiB LDS holds beside
-// the ring)
+// lists of KL = 10 (k <= 10) or 15 (the float64 mode's 10 + 5 guard entries,
+// the most the 160-KiB LDS holds beside the ring)
 // lists: KL = 10 lane-interleaved ([entry][lane]); KL = 15 (cooperative
 // insertion) one lane's entries contiguous, lanes list_stride entries apart
 // (an odd number of 8-byte bank pairs: both the per-lane accesses of 32 lanes
@@ -79,7 +78,7 @@ template <int KL>
 constexpr int list_stride() { return KL == 10 ? 11 : KL; }
 template <int KL>
 constexpr size_t lds_bytes() { return (size_t)NSLOT * STAGE + (size_t)NW * 64 * list_stride<KL>() * 8 + 64; }
-static_assert(lds_bytes<15>() <= 160 * 1024 && lds_bytes<kF64KL>() <= 160 * 1024, "LDS budget");
+static_assert(lds_bytes<15>() <= 160 * 1024, "LDS budget");
 }  // namespace v3
 
 
@@ -138,18 +137,11 @@ __device__ __forceinline__ void list_store(uint32_t addr, const uint64_t (&L)[KL
         (lds_put_u64_at<OFF + I * ES>(addr, L[I]), ...);
     }(std::make_integer_sequence<int, KL>{});
 }
-// every entry := v (one register pair)
-template <int KL, int OFF = 0, int ES = 512>
-__device__ __forceinline__ void list_fill(uint32_t addr, uint64_t v) {
-    [&]<int... I>(std::integer_sequence<int, I...>) {
-        (lds_put_u64_at<OFF + I * ES>(addr, v), ...);
-    }(std::make_integer_sequence<int, KL>{});
-}
 // entry i at addr + OFF + i * ES (ES = 512: the lane-interleaved layout of
 // round 1, 8: one lane's entries contiguous)
 template <int KL, int OFF = 0, int ES = 512>
 __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
-    static_assert(KL == 10 || KL == 11 || KL == 12 || KL == 15, "one asm block of 10, 11, 12 or 15 reads");
+    static_assert(KL == 10 || KL == 15, "one asm block of 10 or 15 reads");
     // all reads in flight, one wait (a wait per read would serialise the LDS
     // round trips); one asm statement so no use can slip before the wait
     if constexpr (KL == 10) {
@@ -165,45 +157,13 @@ __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
             "ds_read_b64 %8, %10 offset:%19\n\t"
             "ds_read_b64 %9, %10 offset:%20\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]), "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9])
-            : "v"(addr), "i"(OFF), "i"(OFF + 1 * ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES), "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES), "i"(OFF + 8 * ES), "i"(OFF + 9 * ES)
+            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
+              "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9])
+            : "v"(addr), "i"(OFF), "i"(OFF + ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES),
+              "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES),
+              "i"(OFF + 8 * ES), "i"(OFF + 9 * ES)
             : "memory");
-    } else if constexpr (KL == 11) {
-        asm volatile(
-            "ds_read_b64 %0, %11 offset:%12\n\t"
-            "ds_read_b64 %1, %11 offset:%13\n\t"
-            "ds_read_b64 %2, %11 offset:%14\n\t"
-            "ds_read_b64 %3, %11 offset:%15\n\t"
-            "ds_read_b64 %4, %11 offset:%16\n\t"
-            "ds_read_b64 %5, %11 offset:%17\n\t"
-            "ds_read_b64 %6, %11 offset:%18\n\t"
-            "ds_read_b64 %7, %11 offset:%19\n\t"
-            "ds_read_b64 %8, %11 offset:%20\n\t"
-            "ds_read_b64 %9, %11 offset:%21\n\t"
-            "ds_read_b64 %10, %11 offset:%22\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]), "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9]), "=&v"(L[10])
-            : "v"(addr), "i"(OFF), "i"(OFF + 1 * ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES), "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES), "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES)
-            : "memory");
-    } else if constexpr (KL == 12) {
-        asm volatile(
-            "ds_read_b64 %0, %12 offset:%13\n\t"
-            "ds_read_b64 %1, %12 offset:%14\n\t"
-            "ds_read_b64 %2, %12 offset:%15\n\t"
-            "ds_read_b64 %3, %12 offset:%16\n\t"
-            "ds_read_b64 %4, %12 offset:%17\n\t"
-            "ds_read_b64 %5, %12 offset:%18\n\t"
-            "ds_read_b64 %6, %12 offset:%19\n\t"
-            "ds_read_b64 %7, %12 offset:%20\n\t"
-            "ds_read_b64 %8, %12 offset:%21\n\t"
-            "ds_read_b64 %9, %12 offset:%22\n\t"
-            "ds_read_b64 %10, %12 offset:%23\n\t"
-            "ds_read_b64 %11, %12 offset:%24\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]), "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9]), "=&v"(L[10]), "=&v"(L[11])
-            : "v"(addr), "i"(OFF), "i"(OFF + 1 * ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES), "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES), "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES), "i"(OFF + 11 * ES)
-            : "memory");
-    } else if constexpr (KL == 15) {
+    } else {
         asm volatile(
             "ds_read_b64 %0, %15 offset:%16\n\t"
             "ds_read_b64 %1, %15 offset:%17\n\t"
@@ -221,91 +181,17 @@ __device__ __forceinline__ void list_load(uint32_t addr, uint64_t (&L)[KL]) {
             "ds_read_b64 %13, %15 offset:%29\n\t"
             "ds_read_b64 %14, %15 offset:%30\n\t"
             "s_waitcnt lgkmcnt(0)"
-            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]), "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9]), "=&v"(L[10]), "=&v"(L[11]), "=&v"(L[12]), "=&v"(L[13]), "=&v"(L[14])
-            : "v"(addr), "i"(OFF), "i"(OFF + 1 * ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES), "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES), "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES), "i"(OFF + 11 * ES), "i"(OFF + 12 * ES), "i"(OFF + 13 * ES), "i"(OFF + 14 * ES)
+            : "=&v"(L[0]), "=&v"(L[1]), "=&v"(L[2]), "=&v"(L[3]), "=&v"(L[4]), "=&v"(L[5]),
+              "=&v"(L[6]), "=&v"(L[7]), "=&v"(L[8]), "=&v"(L[9]), "=&v"(L[10]), "=&v"(L[11]),
+              "=&v"(L[12]), "=&v"(L[13]), "=&v"(L[14])
+            : "v"(addr), "i"(OFF), "i"(OFF + ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES),
+              "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES),
+              "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES), "i"(OFF + 11 * ES),
+              "i"(OFF + 12 * ES), "i"(OFF + 13 * ES), "i"(OFF + 14 * ES)
             : "memory");
     }
 }
 
-// 32-bit words of a lane's list (the distance words at +4, the row words at
-// +0 of each entry), all reads in flight under one wait: the split list
-// operations below hold one word per entry at a time (half the registers of
-// a 64-bit copy: KL = 12 beside the 192 query registers without spills).
-template <int KL, int OFF, int ES>
-__device__ __forceinline__ void list_load32(uint32_t addr, uint32_t (&W)[KL]) {
-    static_assert(KL == 11 || KL == 12, "the split list operations serve KL = 11, 12");
-    if constexpr (KL == 11) {
-        asm volatile(
-            "ds_read_b32 %0, %11 offset:%12\n\t"
-            "ds_read_b32 %1, %11 offset:%13\n\t"
-            "ds_read_b32 %2, %11 offset:%14\n\t"
-            "ds_read_b32 %3, %11 offset:%15\n\t"
-            "ds_read_b32 %4, %11 offset:%16\n\t"
-            "ds_read_b32 %5, %11 offset:%17\n\t"
-            "ds_read_b32 %6, %11 offset:%18\n\t"
-            "ds_read_b32 %7, %11 offset:%19\n\t"
-            "ds_read_b32 %8, %11 offset:%20\n\t"
-            "ds_read_b32 %9, %11 offset:%21\n\t"
-            "ds_read_b32 %10, %11 offset:%22\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(W[0]), "=&v"(W[1]), "=&v"(W[2]), "=&v"(W[3]), "=&v"(W[4]), "=&v"(W[5]), "=&v"(W[6]), "=&v"(W[7]), "=&v"(W[8]), "=&v"(W[9]), "=&v"(W[10])
-            : "v"(addr), "i"(OFF), "i"(OFF + 1 * ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES), "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES), "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES)
-            : "memory");
-    } else if constexpr (KL == 12) {
-        asm volatile(
-            "ds_read_b32 %0, %12 offset:%13\n\t"
-            "ds_read_b32 %1, %12 offset:%14\n\t"
-            "ds_read_b32 %2, %12 offset:%15\n\t"
-            "ds_read_b32 %3, %12 offset:%16\n\t"
-            "ds_read_b32 %4, %12 offset:%17\n\t"
-            "ds_read_b32 %5, %12 offset:%18\n\t"
-            "ds_read_b32 %6, %12 offset:%19\n\t"
-            "ds_read_b32 %7, %12 offset:%20\n\t"
-            "ds_read_b32 %8, %12 offset:%21\n\t"
-            "ds_read_b32 %9, %12 offset:%22\n\t"
-            "ds_read_b32 %10, %12 offset:%23\n\t"
-            "ds_read_b32 %11, %12 offset:%24\n\t"
-            "s_waitcnt lgkmcnt(0)"
-            : "=&v"(W[0]), "=&v"(W[1]), "=&v"(W[2]), "=&v"(W[3]), "=&v"(W[4]), "=&v"(W[5]), "=&v"(W[6]), "=&v"(W[7]), "=&v"(W[8]), "=&v"(W[9]), "=&v"(W[10]), "=&v"(W[11])
-            : "v"(addr), "i"(OFF), "i"(OFF + 1 * ES), "i"(OFF + 2 * ES), "i"(OFF + 3 * ES), "i"(OFF + 4 * ES), "i"(OFF + 5 * ES), "i"(OFF + 6 * ES), "i"(OFF + 7 * ES), "i"(OFF + 8 * ES), "i"(OFF + 9 * ES), "i"(OFF + 10 * ES), "i"(OFF + 11 * ES)
-            : "memory");
-    }
-}
-template <int OFF>
-__device__ __forceinline__ void lds_put_u32_at(uint32_t addr, uint32_t v) {
-    asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(addr), "v"(v), "i"(OFF) : "memory");
-}
-template <int KL, int OFF, int ES>
-__device__ __forceinline__ void list_store32(uint32_t addr, const uint32_t (&W)[KL]) {
-    [&]<int... I>(std::integer_sequence<int, I...>) {
-        (lds_put_u32_at<OFF + I * ES>(addr, W[I]), ...);
-    }(std::make_integer_sequence<int, KL>{});
-}
-// Insert key x into a lane's sorted list in LDS (ascending distance words,
-// equal distances in arrival order; the caller guarantees dist(x) <
-// dist(entry KL-1)), one word per entry at a time: the distance words
-// decide the shift (bit i of `lt` = x goes before entry i), the row words
-// follow the same shift.  Returns the new KL-th distance word.
-template <int KL, int ES>
-__device__ __forceinline__ uint32_t list_insert_split(uint32_t la, uint64_t x) {
-    const uint32_t xh = (uint32_t)(x >> 32), xl = (uint32_t)x;
-    uint32_t W[KL];
-    list_load32<KL, 4, ES>(la, W);
-    uint32_t lt = 0;
-#pragma unroll
-    for (int i = 0; i < KL; ++i) lt |= (xh < W[i] ? 1u : 0u) << i;
-#pragma unroll
-    for (int i = KL - 1; i > 0; --i) W[i] = (lt >> (i - 1)) & 1u ? W[i - 1] : ((lt >> i) & 1u ? xh : W[i]);
-    W[0] = lt & 1u ? xh : W[0];
-    const uint32_t kth = W[KL - 1];
-    list_store32<KL, 4, ES>(la, W);
-    list_load32<KL, 0, ES>(la, W);
-#pragma unroll
-    for (int i = KL - 1; i > 0; --i) W[i] = (lt >> (i - 1)) & 1u ? W[i - 1] : ((lt >> i) & 1u ? xl : W[i]);
-    W[0] = lt & 1u ? xl : W[0];
-    list_store32<KL, 0, ES>(la, W);
-    return kth;
-}
 // In-place odd-even transposition sort of a short list (ascending keys).
 template <int KL>
 __device__ __forceinline__ void list_sort(uint64_t (&L)[KL]) {
@@ -435,11 +321,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     // spills them into the MFMA stream), so the lists are updated
     // cooperatively, 16 lanes per list, an entry per lane, four lists per
     // wave instruction.  ABL 65: cooperative at KL = 10 too (slower there).
-    constexpr bool kCoop = KL > 12 || ABL == 65;
-    // KL = kF64KL (the float64 mode): the walk holds one 32-bit word per entry
-    // at a time (a 64-bit copy spilled query fragments into the MFMA stream,
-    // tests/test_codeobj.py)
-    constexpr bool kSplit = (KL == 11 || KL == 12) && !kCoop;
+    constexpr bool kCoop = KL > 10 || ABL == 65;
     constexpr int LS = kCoop ? list_stride<KL>() : KL;  // entries per lane column
     constexpr int ES = kCoop ? 8 : 512;                  // bytes between a list's entries
     constexpr uint32_t LSTR = kCoop ? LS * 8 : 8;        // bytes between lanes' lists
@@ -544,10 +426,6 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
 #pragma unroll
         for (int j = 0; j < NST; ++j) dma_stage(j * STAGE, 0, j);
 
-        // (kSplit) this lane's list empty, one register pair for all entries,
-        // before the query fragments take their registers (the previous
-        // tile's merge read the lists before the dequeue barrier)
-        if constexpr (kSplit) list_fill<KL, 0, ES>(opaque_u(lbase), kEmptyKey);
         half8 qf[NQF];
         // the lane's bound: only objects with ord(d) <= thr can enter the
         // pair's top-KL (the distance part of a key: the bound may come from
@@ -594,7 +472,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             }
             my_invq = live ? a.invq[q] : 0.0f;
         }
-        if constexpr (!kSplit) {
+        {
             uint64_t E[KL];
             list_clear<KL>(E);
             list_store<KL, 0, ES>(opaque_u(lbase), E);
@@ -737,16 +615,6 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                         const uint64_t key = make_key(d, rb + (uint32_t)i);
                         if (LO && d == lo_d && eb * 32 + 4 * hh + i < lo_row) {
                             // at or before the pair's lower bound: not this pass's
-                        } else if constexpr (kSplit) {
-                            // (no append mode: the list starts EMPTY, so the
-                            // first KL candidates are inserted too) the
-                            // distance word of entry KL-1 decides; one word
-                            // per entry in registers at a time
-                            uint32_t last;
-                            asm volatile("ds_read_b32 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)"
-                                         : "=v"(last) : "v"(la), "i"(4 + (KL - 1) * 512) : "memory");
-                            if ((uint32_t)(key >> 32) < last) last = list_insert_split<KL, 512>(la, key);
-                            thr = std::min(thr, last);
                         } else if (cnt < KL) {
                             // append mode: the first KL candidates are stored
                             // unsorted; a full buffer is sorted once (stable)
@@ -875,7 +743,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         }
         if (defer && nblk > 0) epilogue(nblk - 1);
         // lanes still in append mode hold an unsorted (EMPTY-padded) buffer
-        if (!kCoop && !kSplit && __any(cnt < KL)) {
+        if (!kCoop && __any(cnt < KL)) {
             if (cnt < KL) {
                 uint64_t L[KL];
                 list_load<KL>(lbase, L);

@@ -47,8 +47,7 @@ extern "C" int lmi_abl_launch_scan3(int kl, int abl, const void* args, void* str
     lmi::Scan2Args b = *static_cast<const lmi::Scan2Args*>(args);
     b.dbg = dbg_ptr();
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    return kl == 10 ? launch_abl<10>(abl, b, s) : kl == lmi::kF64KL ? launch_abl<lmi::kF64KL>(abl, b, s)
-                                                            : launch_abl<15>(abl, b, s);
+    return kl == 10 ? launch_abl<10>(abl, b, s) : launch_abl<15>(abl, b, s);
 }
 
 extern "C" int lmi_debug_counters(unsigned long long* out16) {
