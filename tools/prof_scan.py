@@ -69,6 +69,10 @@ for abl, var in runs:
             life_us = cnt[9] / cnt[12] * 0.01
             print(f"   clock {ghz:.3f} GHz, workgroup life {life_us:.0f} us avg over {cnt[12] // a.reps} WGs/launch",
                   flush=True)
+        if abl == "7":
+            names = ["wave-events", "candidates", "appends", "sorted-inserts", "fills", "wave-blocks"]
+            print("   per launch: " + ", ".join(f"{nm}={cnt[i] / a.reps:.4g}" for i, nm in enumerate(names)),
+                  flush=True)
         # one more launch alone: the spread of workgroup starts and ends
         # (100-MHz s_memrealtime ticks -> us), i.e. the persistent grid's tail
         lib.lmi_debug_counters(cnt)
@@ -80,10 +84,6 @@ for abl, var in runs:
             t0 = c1[10]
             print(f"   one launch: span {(c1[11] - t0) * 0.01:.1f} us, last start {(c1[13] - t0) * 0.01:.1f} us, "
                   f"first end {(c1[14] - t0) * 0.01:.1f} us, mean life {c1[9] / c1[12] * 0.01:.1f} us", flush=True)
-        if abl == "7":
-            names = ["wave-events", "candidates", "appends", "sorted-inserts", "fills", "wave-blocks"]
-            print("   per launch: " + ", ".join(f"{nm}={cnt[i] / a.reps:.4g}" for i, nm in enumerate(names)),
-                  flush=True)
     if ref is not None:
         d, p_ = bucket_topk(ix, q, classes, 10)[:2]
         same = bool(torch.equal(d, ref[0]) and torch.equal(p_, ref[1]))
