@@ -361,10 +361,14 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     for (int w = 0; w < NW; ++w)
         if (w != wave && wtab[w] == simd) partner = w;
     partner = __builtin_amdgcn_readfirstlane(partner);
-    uint64_t clk0 = 0, rt0 = 0;
+    // (diagnostic builds: the entry clocks wait in LDS, not in registers --
+    // two live 64-bit values spilled a query fragment into the MFMA stream)
+    uint64_t* clk_lds = reinterpret_cast<uint64_t*>(wtab + NW + 2);
     if constexpr (ABL != 0) {
-        clk0 = __builtin_amdgcn_s_memtime();
-        rt0 = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) {
+            clk_lds[0] = __builtin_amdgcn_s_memtime();
+            clk_lds[1] = __builtin_amdgcn_s_memrealtime();
+        }
     }
     const uint32_t wbase = (uint32_t)(uintptr_t)(lists + wave * 64 * LS);  // this wave's lists
     const uint32_t lbase = wbase + (uint32_t)lane * LSTR;                   // this lane's
@@ -773,6 +777,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         if (tid == 0) {
             const uint64_t clk1 = __builtin_amdgcn_s_memtime();
             const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const uint64_t clk0 = clk_lds[0], rt0 = clk_lds[1];
             atomicAdd(&a.dbg[8], (unsigned long long)(clk1 - clk0));
             atomicAdd(&a.dbg[9], (unsigned long long)(rt1 - rt0));
             atomicMin(&a.dbg[10], (unsigned long long)rt0);

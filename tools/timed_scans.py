@@ -44,7 +44,8 @@ def main(root, out_path=None, kernel="scan3_kernel"):
             r.update(mean_ms=round(statistics.mean(ms), 4), median_ms=round(statistics.median(ms), 4),
                      min_ms=round(min(ms), 4), max_ms=round(max(ms), 4),
                      durations_ms=[round(x, 4) for x in ms],
-                     kernel_names=sorted({x[2].split("(")[0] for x in d}))
+                     kernel_names=sorted({x[2].replace("(anonymous namespace)::", "").split("(")[0]
+                                          .replace("void ", "") for x in d}))
         res["ranges"].append(r)
     s = json.dumps(res, indent=1)
     print(s)
