@@ -39,6 +39,8 @@ EnvConfig read_env() {
     e.scan_split_parts = env_i("LMI_SCAN_SPLIT_PARTS", 2);
     e.scan_wgs = env_i("LMI_SCAN_WGS", 0);
     e.scan_no_pref = env_b("LMI_SCAN_NO_PREF");
+    e.wide_passes = env_b("LMI_WIDE_PASSES");
+    e.wide_no_fixup = env_b("LMI_WIDE_NO_FIXUP");
     e.router_fma = env_b("LMI_ROUTER_FMA");
     e.router_qg = env_i("LMI_ROUTER_QG", 0);
     return e;

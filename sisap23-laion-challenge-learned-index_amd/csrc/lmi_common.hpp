@@ -139,12 +139,27 @@ inline int take_phases(int32_t& qmode) {
 // pair in the outputs (default k); prefill: write (+inf, -1) over all R*ldo
 // entries first (the first pass).  seed_r0: LMI_Q_SEED_ROUND0 (pairs r >= 1
 // start from the bound of pair (q, 0), + seed_margin in distance).
+// The scans of the wide path (k > 16, bucket_topk_wide): mode 1 writes every
+// (pair, chunk part) list as that part's own top-15 (no global bound); mode 2
+// collects every row within the pair's bound bound_ord[pair id] (a distance
+// ordinal; 0 = none) into cand[grouped pair * cap + i] (ccount: slots taken).
+struct WideScan {
+    int mode;
+    const uint32_t* bound_ord;
+    uint64_t* cand;
+    uint32_t* ccount;
+    int32_t cap;
+    uint32_t* bins;  // mode 1: [P][nbins], all ones at the start (Scan2Args::bins)
+    int32_t nbins;
+    int32_t take;    // mode 1: rows sampled from the start of every chunk
+};
 int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                      const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                      int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                      size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g = nullptr,
                      int32_t ldo = 0, bool prefill = true, bool seed_r0 = false,
-                     float seed_margin = 0.0f, int phases = kPhaseAll);
+                     float seed_margin = 0.0f, int phases = kPhaseAll,
+                     const WideScan* wide = nullptr);
 size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
                             int32_t qmode, bool lo = false);
 // k > LMI_MAX_K: passes_of() passes of kp-entry lists; bucket_topk_passes fills
@@ -155,6 +170,17 @@ int bucket_topk_passes(const lmi_index_desc* idx, const float* q, int32_t nq, in
                        const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                        int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
                        void* workspace, size_t ws_bytes, hipStream_t s);
+// k > LMI_MAX_K, the same lists as bucket_topk_passes from two scans (scan v3):
+// chunk lists -> per-pair bound (the kw-th smallest of the pair's chunk-list
+// distances, kw = passes * kp) -> collect the rows within it -> sort; pairs
+// without a bound (too few chunk-list entries) or whose candidates overflow
+// go through bucket_topk_passes restricted to them.  Off scan v3 (or under
+// LMI_WIDE_PASSES) it is bucket_topk_passes.
+size_t wide_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int ldo);
+int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                     const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
+                     int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
+                     void* workspace, size_t ws_bytes, hipStream_t s);
 // n_words 32-bit words of `value` from p (4-byte aligned) on stream s, by a
 // kernel (lmi_merge.hip): workspace initialisation stays a kernel node when a
 // caller captures the launch sequence in a HIP graph (no memset nodes).

@@ -20,6 +20,10 @@ struct EnvConfig {
     int scan_wgs;        // LMI_SCAN_WGS: persistent scan workgroups (0 = one per CU; tests
                          //   use a few to make tiles run after others have published bounds)
     bool scan_no_pref;   // LMI_SCAN_NO_PREF
+    bool wide_passes;    // LMI_WIDE_PASSES: k > 16 by lower-bound passes alone (the bound +
+                         //   collect scans off; A/B and tests)
+    bool wide_no_fixup;  // LMI_WIDE_NO_FIXUP (diagnostic, lists wrong): skip the fix-up passes, so
+                         //   the pairs that needed them keep (+inf, -1) -- counts them
     bool router_fma;     // LMI_ROUTER_FMA: FMA-chain router instead of MFMA
     int router_qg;       // LMI_ROUTER_QG: 1/2/4 query groups per workgroup, 0 = auto
 };

@@ -361,7 +361,7 @@ RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     w.lpos = take(P * w.kl * 4);
     w.failed = take(P * 4);
     w.nfailed = take(256);
-    w.scan = take(w.passes ? passes_ws_bytes(idx, nq, R, k + 5, qmode)
+    w.scan = take(w.passes ? wide_ws_bytes(idx, nq, R, k + 5, qmode, w.kl)
                            : scan_workspace_bytes(idx, nq, R, w.kl, qmode));
     w.total = off;
     return w;
@@ -473,7 +473,7 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     }
     if (phases & kPhasePlan) LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
     int rc = w.passes
-        ? bucket_topk_passes(idx, q, nq, ldq, classes, R, k + 5, qmode, (float*)(ws + w.ld),
+        ? bucket_topk_wide(idx, q, nq, ldq, classes, R, k + 5, qmode, (float*)(ws + w.ld),
                              (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), kl, status,
                              ws + w.scan, w.total - w.scan, s)
         : bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),

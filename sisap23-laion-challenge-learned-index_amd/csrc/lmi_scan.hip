@@ -660,6 +660,223 @@ __global__ __launch_bounds__(256) void next_lo_kernel(const float* __restrict__ 
     lo[p] = g < 0 ? ~0ull : (((unsigned long long)f2ord(d[o]) << 32) | (uint32_t)g);
 }
 
+// ---------------------------------------------------------------------------
+// k > 16: bound + collect (bucket_topk_wide)
+// ---------------------------------------------------------------------------
+// slot of the j-th list of a pair in the partial lists: chunks first, then
+// parts 1..S-1 of every split chunk (bit of sm) in ascending order (the order
+// chunk_merge_kernel reads them in; X = max_chunks / S)
+__device__ inline int wide_slot(int j, int nch_c, uint32_t sm, int S, int X) {
+    if (j < nch_c) return j;
+    const int jj = j - nch_c;
+    int nth = jj / (S - 1);
+    const int part = 1 + jj % (S - 1);
+    for (; nth > 0; --nth) sm &= sm - 1u;
+    return part * X + __builtin_ctz(sm);
+}
+
+// the bound pass's chunk table: chunk_first of chunk_rows-row chunks over
+// the index's buckets (one workgroup: a thread per contiguous run of buckets,
+// then a prefix over the threads)
+__global__ __launch_bounds__(256) void sub_chunk_first_kernel(const int64_t* __restrict__ bucket_off,
+                                                              int32_t C, int32_t chunk_rows,
+                                                              int32_t* __restrict__ chunk_first) {
+    __shared__ int32_t part[256];
+    const int t = threadIdx.x;
+    const int per = (C + 255) / 256;
+    const int c0 = min(C, t * per), c1 = min(C, c0 + per);
+    int32_t acc = 0;
+    for (int c = c0; c < c1; ++c) acc += (int32_t)((bucket_off[c + 1] - bucket_off[c] + chunk_rows - 1) / chunk_rows);
+    part[t] = acc;
+    __syncthreads();
+    if (t == 0) {
+        int32_t run = 0;
+        for (int i = 0; i < 256; ++i) {
+            const int32_t v = part[i];
+            part[i] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    acc = part[t];
+    for (int c = c0; c < c1; ++c) {
+        chunk_first[c] = acc;
+        acc += (int32_t)((bucket_off[c + 1] - bucket_off[c] + chunk_rows - 1) / chunk_rows);
+    }
+    if (c0 < C && c1 == C) chunk_first[C] = acc;
+}
+
+// outputs padded (+inf, -1), bounds and the fix-up flags cleared
+__global__ __launch_bounds__(256) void wide_init_kernel(int64_t P, int32_t ldo, float* __restrict__ d,
+                                                        int32_t* __restrict__ pos, int32_t* __restrict__ row,
+                                                        uint32_t* __restrict__ bound_ord,
+                                                        int32_t* __restrict__ fix) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t < P * ldo) {
+        d[t] = __builtin_inff();
+        pos[t] = -1;
+        if (row) row[t] = -1;
+    }
+    if (t < P) {
+        bound_ord[t] = 0u;
+        fix[t] = 0;
+    }
+}
+
+// Per grouped pair of the chunk-list scan (one 64-lane workgroup): the kw-th
+// smallest distance ordinal over its chunk lists (each the part's own top-15,
+// so at least kw rows lie within it) by a 4-digit radix select; fewer than
+// kw entries: no bound, the pair goes to the fix-up passes.
+__global__ __launch_bounds__(64) void kth_bound_kernel(
+    const uint64_t* __restrict__ partial, int32_t max_chunks, int32_t S,
+    const int32_t* __restrict__ pair_q, const int32_t* __restrict__ pair_bucket,
+    const int32_t* __restrict__ chunk_first, const uint32_t* __restrict__ split_mask, int32_t P,
+    int32_t kw, uint32_t* __restrict__ bound_ord, int32_t* __restrict__ fix) {
+    constexpr int KL = 15;
+    const int pp = blockIdx.x;
+    const int c = pair_bucket[pp];
+    if (c < 0) return;
+    const int p = pair_q[pp];
+    if (p < 0 || p >= P) return;
+    const uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
+    const int nch_c = chunk_first[c + 1] - chunk_first[c];
+    const int nl = nch_c + (S - 1) * __popc(sm);
+    const int X = max_chunks / S;
+    const uint64_t* base = partial + (size_t)pp * max_chunks * KL;
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t s_prefix, s_mask, s_rem, s_n;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_n = 0u;
+    __syncthreads();
+    uint32_t n = 0;
+    for (int e = tid; e < nl * KL; e += 64) {
+        const uint64_t key = base[(size_t)wide_slot(e / KL, nch_c, sm, S, X) * KL + e % KL];
+        n += key != kEmptyKey ? 1u : 0u;
+    }
+    atomicAdd(&s_n, n);
+    if (tid == 0) {
+        s_prefix = 0u;
+        s_mask = 0u;
+        s_rem = (uint32_t)kw;
+    }
+    __syncthreads();
+    if (s_n < (uint32_t)kw) {
+        if (tid == 0) fix[p] = 1;  // (bound_ord stays 0: the collect takes nothing)
+        return;
+    }
+    for (int shift = 24; shift >= 0; shift -= 8) {
+        for (int i = tid; i < 256; i += 64) hist[i] = 0u;
+        __syncthreads();
+        const uint32_t prefix = s_prefix, mask = s_mask;
+        for (int e = tid; e < nl * KL; e += 64) {
+            const uint64_t key = base[(size_t)wide_slot(e / KL, nch_c, sm, S, X) * KL + e % KL];
+            const uint32_t h = (uint32_t)(key >> 32);
+            if (key != kEmptyKey && (h & mask) == prefix) atomicAdd(&hist[(h >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t rem = s_rem, dg = 0;
+            for (; dg < 255u && hist[dg] < rem; ++dg) rem -= hist[dg];
+            s_rem = rem;
+            s_prefix = prefix | (dg << shift);
+            s_mask = mask | (255u << shift);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) bound_ord[p] = s_prefix;
+}
+
+// the collect scan's per-grouped-pair bound (thr_g: the distance ordinal in
+// the high word) and candidate count
+__global__ __launch_bounds__(256) void set_bound_kernel(const int32_t* __restrict__ pair_q, int32_t P,
+                                                        const uint32_t* __restrict__ bound_ord,
+                                                        unsigned long long* __restrict__ thr_g,
+                                                        uint32_t* __restrict__ ccount) {
+    const int pp = blockIdx.x * 256 + threadIdx.x;
+    if (pp >= P) return;
+    const int p = pair_q[pp];
+    const uint32_t b = (p < 0 || p >= P) ? 0u : bound_ord[p];
+    thr_g[pp] = ((unsigned long long)b << 32) | 0xffffffffull;
+    ccount[pp] = 0u;
+}
+
+// Per grouped pair of the collect scan (one 256-lane workgroup): its
+// candidates sorted by (distance, row) -- rows ascend with global position
+// inside a bucket, so this is the reference's (distance, g.index) order --
+// and the first kw written as (d, global position, row).  A pair whose
+// candidates overflowed (or, never for a sound scan, came back short) goes to
+// the fix-up passes.
+__global__ __launch_bounds__(256) void collect_select_kernel(
+    const uint64_t* __restrict__ cand, const uint32_t* __restrict__ ccount, int32_t cap,
+    const int32_t* __restrict__ pair_q, const int32_t* __restrict__ pair_bucket,
+    const int32_t* __restrict__ gpos, int32_t P, int32_t kw, int32_t ldo, int32_t* __restrict__ fix,
+    float* __restrict__ out_d, int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row) {
+    extern __shared__ uint64_t keys[];
+    const int pp = blockIdx.x;
+    if (pair_bucket[pp] < 0) return;
+    const int p = pair_q[pp];
+    if (p < 0 || p >= P || fix[p]) return;
+    const uint32_t n = ccount[pp];
+    const int tid = threadIdx.x;
+    if (n > (uint32_t)cap || n < (uint32_t)kw) {
+        if (tid == 0) fix[p] = 1;
+        return;
+    }
+    uint32_t m = 1;
+    while (m < n) m <<= 1;
+    const uint64_t* src = cand + (size_t)pp * cap;
+    for (uint32_t i = tid; i < m; i += 256) keys[i] = i < n ? src[i] : kEmptyKey;
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= m; k2 <<= 1) {
+        for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < m; i += 256) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = keys[i], y = keys[l];
+                    const bool up = (i & k2) == 0;
+                    if ((x > y) == up) {
+                        keys[i] = y;
+                        keys[l] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const size_t o = (size_t)p * ldo;
+    for (int i = tid; i < kw; i += 256) {
+        const uint64_t key = keys[i];
+        const uint32_t r = (uint32_t)key;
+        out_d[o + i] = ord2f((uint32_t)(key >> 32));
+        out_pos[o + i] = gpos[r];
+        if (out_row) out_row[o + i] = (int32_t)r;
+    }
+}
+
+// the fix-up passes' classes: the pair's class where it needs them, else -1
+// (out of range: the plan skips the pair)
+__global__ __launch_bounds__(256) void fix_classes_kernel(const int32_t* __restrict__ classes,
+                                                          const int32_t* __restrict__ fix, int32_t P,
+                                                          int32_t* __restrict__ cls_fix) {
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p < P) cls_fix[p] = fix[p] ? classes[p] : -1;
+}
+
+// the fix-up passes' lists over the outputs of the pairs that took them
+__global__ __launch_bounds__(256) void fix_combine_kernel(const int32_t* __restrict__ fix, int64_t P,
+                                                          int32_t ldo, const float* __restrict__ fd,
+                                                          const int32_t* __restrict__ fpos,
+                                                          const int32_t* __restrict__ frow,
+                                                          float* __restrict__ d, int32_t* __restrict__ pos,
+                                                          int32_t* __restrict__ row) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= P * ldo) return;
+    if (!fix[t / ldo]) return;
+    d[t] = fd[t];
+    pos[t] = fpos[t];
+    if (row) row[t] = frow[t];
+}
+
 // first k of every pair's pass list -> the caller's [P][k] outputs
 __global__ __launch_bounds__(256) void take_k_kernel(const float* __restrict__ d,
                                                      const int32_t* __restrict__ pos, int64_t P,
@@ -862,7 +1079,7 @@ extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq
     if (k <= LMI_MAX_K) return scan_workspace_bytes(idx, nq, R, k, qmode);
     int kp;
     const int ldo = passes_of(idx, qmode, k, &kp) * kp;
-    return 2 * align_up((size_t)nq * R * ldo * 4, 256) + passes_ws_bytes(idx, nq, R, k, qmode);
+    return 2 * align_up((size_t)nq * R * ldo * 4, 256) + wide_ws_bytes(idx, nq, R, k, qmode, ldo);
 }
 
 namespace {
@@ -902,8 +1119,8 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     auto* ws = reinterpret_cast<unsigned char*>(workspace);
     float* ld = reinterpret_cast<float*>(ws);
     int32_t* lp = reinterpret_cast<int32_t*>(ws + lists);
-    const int rc = bucket_topk_passes(idx, q, nq, ldq, classes, R, k, qmode, ld, lp, nullptr, ldo,
-                                      status, ws + 2 * lists, ws_bytes - 2 * lists, s);
+    const int rc = bucket_topk_wide(idx, q, nq, ldq, classes, R, k, qmode, ld, lp, nullptr, ldo,
+                                    status, ws + 2 * lists, ws_bytes - 2 * lists, s);
     if (rc != LMI_OK) return rc;
     hipLaunchKernelGGL(take_k_kernel, dim3((unsigned)((P * k + 255) / 256)), dim3(256), 0, s, ld, lp,
                        (int64_t)P, ldo, k, out_d, out_pos);
@@ -915,7 +1132,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                           const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                           int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                           size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g, int32_t ldo,
-                          bool prefill, bool seed_r0, float seed_margin, int phases) {
+                          bool prefill, bool seed_r0, float seed_margin, int phases,
+                          const WideScan* wide) {
     const bool do_plan = phases & kPhasePlan, do_scan = phases & kPhaseScan,
                do_merge = phases & kPhaseMerge;
     using namespace lmi;
@@ -1048,6 +1266,14 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         scan_off = (const int64_t*)(ws + w.ext_off);
     }
 
+    // the collect scan: every grouped pair's fixed bound (0 = takes nothing)
+    // and its candidate count
+    if (wide && wide->mode == 2 && do_scan) {
+        hipLaunchKernelGGL(set_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pair_q, P,
+                           wide->bound_ord, (unsigned long long*)(ws + w.thr_g), wide->ccount);
+        LMI_LAUNCH_CHECK("set_bound_kernel");
+    }
+
     ScanArgs a{};
     a.corpus = idx->corpus;
     a.d_pad = idx->d_pad;
@@ -1096,7 +1322,20 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         // (thr_g was reset by prep)
         if (!do_scan) rc = LMI_OK;
         else
-        if (w.use_v3 && LOP) {
+        if (wide) {
+            if (!w.use_v3 || LOP || (wide->mode == 1 ? KL != 15 : KL != 10)) {
+                set_error("internal: the wide scans take scan v3 with 15 (chunk lists) or 10 (collect) entries");
+                return LMI_E_INVALID;
+            }
+            b.cand = wide->cand;
+            b.ccount = wide->ccount;
+            b.cap = wide->cap;
+            b.bins = wide->bins;
+            b.nbins = wide->nbins;
+            b.chunk_take = wide->take;
+            rc = wide->mode == 1 ? launch_scan3_v<15, 0, false, 1>(b, s) : launch_scan3_v<10, 0, false, 2>(b, s);
+        }
+        else if (w.use_v3 && LOP) {
             // the passes' lists are 15 entries on v3 (passes_of)
             if (KL != 15) {
                 set_error("lower-bound scan passes take 15-entry lists on scan v3");
@@ -1194,6 +1433,175 @@ int bucket_topk_passes(const lmi_index_desc* idx, const float* q, int32_t nq, in
             LMI_LAUNCH_CHECK("next_lo_kernel");
         }
     }
+    return LMI_OK;
+}
+
+namespace {
+struct WideWs {
+    bool on;       // the bound + collect path (else bucket_topk_passes alone)
+    int kw, cap;   // list entries produced (passes * kp); candidate slots per pair
+    int sub;       // the bound pass's chunks: the index's chunk_rows / sub
+    size_t bound, fix, cls, ccount, cand, fd, fpos, frow, sub_first, bins, region, region_bytes, total;
+    int nbins;
+    int take;  // rows of every bound-pass chunk scanned (a sample: its first quarter)
+};
+
+// The bound pass scans chunks of chunk_rows / sub rows: a pair has a bound
+// when its bucket's chunk lists hold kw entries, i.e. ~kw / 15 chunks, so
+// finer chunks give a bound to pairs of smaller buckets and a tighter one to
+// the others (more tiles: each loads its pairs' fragments once).  Host-side
+// values only (workspace sizes must not read the device).
+lmi_index_desc bound_desc(const lmi_index_desc* idx, int sub, const int32_t* sub_first) {
+    lmi_index_desc b = *idx;
+    b.chunk_rows = idx->chunk_rows / sub;
+    b.max_chunks = std::max(idx->max_chunks, 1) * sub;
+    b.n_chunks = idx->n_chunks * sub;
+    b.chunk_first = sub_first;
+    b.chunk_centroid = nullptr;  // (the nearest-chunk-first plan's units are the index's chunks)
+    return b;
+}
+
+WideWs wide_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int ldo) {
+    WideWs w{};
+    int kp;
+    const int np = passes_of(idx, qmode, k, &kp);
+    w.kw = np * kp;
+    // (two passes are two scans either way: the passes, without the extra kernels)
+    w.on = v3_capable(idx, qmode) && kp == 15 && np >= 3 && !env_config().wide_passes;
+    // sub: about kw / 15 / 2 bound-pass chunks per index chunk, pow2, <= 8, and
+    // chunks of >= 256 rows, a multiple of 32
+    w.sub = 1;
+    while (w.sub < 8 && 2 * 15 * w.sub < w.kw && idx->chunk_rows % (64 * w.sub) == 0 &&
+           idx->chunk_rows / (2 * w.sub) >= 256)
+        w.sub *= 2;
+    const size_t P = (size_t)nq * R;
+    if (!w.on) {
+        w.region_bytes = w.total = passes_ws_bytes(idx, nq, R, k, qmode);
+        return w;
+    }
+    // the bound pass scans the first quarter of every chunk (>= 256 rows): the
+    // kw-th smallest of its lists is about the 4 kw-th distance of the pair,
+    // so the collect scan finds about 4 kw candidates; 8 kw (+ 64) slots
+    // before the fix-up passes take over
+    w.take = std::min(idx->chunk_rows / w.sub, std::max(256, idx->chunk_rows / w.sub / 4));
+    int cap = 256;
+    while (cap < 8 * w.kw + 64) cap <<= 1;
+    w.cap = std::min(cap, 8192);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = off;
+        off = align_up(off + bytes, 256);
+        return at;
+    };
+    w.bound = take(P * 4);
+    w.fix = take(P * 4);
+    w.cls = take(P * 4);
+    w.ccount = take(P * 4);
+    w.cand = take(P * (size_t)w.cap * 8);
+    w.fd = take(P * (size_t)ldo * 4);
+    w.fpos = take(P * (size_t)ldo * 4);
+    w.frow = take(P * (size_t)ldo * 4);
+    w.sub_first = take(((size_t)idx->n_buckets + 1) * 4);
+    w.nbins = np;  // (np * 15 = kw)
+    w.bins = take(P * (size_t)w.nbins * 4);
+    const lmi_index_desc bd = bound_desc(idx, w.sub, nullptr);
+    w.region_bytes = std::max({scan_workspace_bytes(&bd, nq, R, 15, qmode),
+                               scan_workspace_bytes(idx, nq, R, 10, qmode),
+                               passes_ws_bytes(idx, nq, R, k, qmode)});
+    w.region = take(w.region_bytes);
+    w.total = off;
+    return w;
+}
+}  // namespace
+
+size_t wide_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int ldo) {
+    return wide_ws(idx, nq, R, k, qmode, ldo).total;
+}
+
+int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                     const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
+                     int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
+                     void* workspace, size_t ws_bytes, hipStream_t s) {
+    const WideWs w = wide_ws(idx, nq, R, k, qmode, ldo);
+    if (!w.on || idx->n_rows == 0)
+        return bucket_topk_passes(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, out_row, ldo,
+                                  status, workspace, ws_bytes, s);
+    if (ldo < w.kw) {
+        set_error("lists of %d entries < %d", ldo, w.kw);
+        return LMI_E_INVALID;
+    }
+    if (ws_bytes < w.total) {
+        set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
+        return LMI_E_WORKSPACE;
+    }
+    if (nq == 0) return LMI_OK;
+    const int P = nq * R;
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    auto* bound = (uint32_t*)(ws + w.bound);
+    auto* fix = (int32_t*)(ws + w.fix);
+    auto* ccount = (uint32_t*)(ws + w.ccount);
+    auto* cand = (uint64_t*)(ws + w.cand);
+    auto* fd = (float*)(ws + w.fd);
+    auto* fpos = (int32_t*)(ws + w.fpos);
+    auto* frow = out_row ? (int32_t*)(ws + w.frow) : nullptr;
+    unsigned char* region = ws + w.region;
+    const int64_t PL = (int64_t)P * ldo;
+    hipLaunchKernelGGL(wide_init_kernel, dim3((unsigned)((PL + 255) / 256)), dim3(256), 0, s, (int64_t)P,
+                       ldo, out_d, out_pos, out_row, bound, fix);
+    LMI_LAUNCH_CHECK("wide_init_kernel");
+    const int plan_scan = kPhasePlan | kPhaseScan;
+    // 1. every (pair, bound-pass chunk part)'s own top-15 -> each pair's bound
+    auto* sub_first = (int32_t*)(ws + w.sub_first);
+    hipLaunchKernelGGL(sub_chunk_first_kernel, dim3(1), dim3(256), 0, s, idx->bucket_off, idx->n_buckets,
+                       idx->chunk_rows / w.sub, sub_first);
+    LMI_LAUNCH_CHECK("sub_chunk_first_kernel");
+    const lmi_index_desc bd = bound_desc(idx, w.sub, sub_first);
+    auto* bins = (uint32_t*)(ws + w.bins);
+    LMI_TRY(fill_u32(bins, 0xffffffffu, (size_t)P * w.nbins, s));
+    const WideScan m1{1, nullptr, nullptr, nullptr, 0, bins, w.nbins, w.take};
+    int rc = bucket_topk_impl(&bd, q, nq, ldq, classes, R, 15, qmode, fd, fpos, nullptr, status, region,
+                              w.region_bytes, s, nullptr, 0, false, false, 0.0f, plan_scan, &m1);
+    if (rc != LMI_OK) return rc;
+    {
+        const WsLayout l = ws_layout(&bd, nq, R, 15, qmode);
+        hipLaunchKernelGGL(kth_bound_kernel, dim3((unsigned)P), dim3(64), 0, s,
+                           (const uint64_t*)(region + l.partial), l.split_s * bd.max_chunks, l.split_s,
+                           (const int32_t*)(region + l.pair_q), (const int32_t*)(region + l.pair_bucket),
+                           sub_first, (const uint32_t*)(region + l.split_mask), P, w.kw, bound, fix);
+        LMI_LAUNCH_CHECK("kth_bound_kernel");
+    }
+    // 2. every row within the bound -> sorted, the first kw
+    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, 0};
+    rc = bucket_topk_impl(idx, q, nq, ldq, classes, R, 10, qmode, fd, fpos, nullptr, status, region,
+                          w.region_bytes, s, nullptr, 0, false, false, 0.0f, plan_scan, &m2);
+    if (rc != LMI_OK) return rc;
+    {
+        const WsLayout l = ws_layout(idx, nq, R, 10, qmode);
+        static std::once_flag once;
+        static hipError_t attr_err = hipSuccess;
+        std::call_once(once, [] {
+            attr_err = hipFuncSetAttribute((const void*)collect_select_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 8);
+        });
+        LMI_HIP_TRY(attr_err);
+        hipLaunchKernelGGL(collect_select_kernel, dim3((unsigned)P), dim3(256), (size_t)w.cap * 8, s, cand,
+                           ccount, w.cap, (const int32_t*)(region + l.pair_q),
+                           (const int32_t*)(region + l.pair_bucket), idx->gpos, P, w.kw, ldo, fix, out_d,
+                           out_pos, out_row);
+        LMI_LAUNCH_CHECK("collect_select_kernel");
+    }
+    // 3. the pairs without a bound or with too many candidates: the passes,
+    //    over their buckets only (every other pair's class is -1)
+    if (env_config().wide_no_fixup) return LMI_OK;
+    int32_t* cls = (int32_t*)(ws + w.cls);
+    hipLaunchKernelGGL(fix_classes_kernel, dim3((P + 255) / 256), dim3(256), 0, s, classes, fix, P, cls);
+    LMI_LAUNCH_CHECK("fix_classes_kernel");
+    rc = bucket_topk_passes(idx, q, nq, ldq, cls, R, k, qmode, fd, fpos, frow, ldo, status, region,
+                            w.region_bytes, s);
+    if (rc != LMI_OK) return rc;
+    hipLaunchKernelGGL(fix_combine_kernel, dim3((unsigned)((PL + 255) / 256)), dim3(256), 0, s, fix,
+                       (int64_t)P, ldo, fd, fpos, frow, out_d, out_pos, out_row);
+    LMI_LAUNCH_CHECK("fix_combine_kernel");
     return LMI_OK;
 }
 }  // namespace lmi

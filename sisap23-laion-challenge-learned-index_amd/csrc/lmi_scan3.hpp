@@ -289,9 +289,15 @@ __device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
     return x;
 }
 
-template <int KL, int ABL = 0, bool LO = false>
+// MODE (k > 16, bucket_topk_wide): 0 the product scan; 1 chunk lists -- every
+// (pair, chunk part) list is that part's own top-KL (no global bound read,
+// exchanged or published), the rows behind the wide path's per-pair bound;
+// 2 collect -- every row of a pair within its fixed bound (thr_g, set by the
+// plan) is appended to the pair's candidate buffer (Scan2Args::cand), no lists.
+template <int KL, int ABL = 0, bool LO = false, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
+    static_assert(MODE == 0 || (ABL == 0 && !LO), "the wide modes are product variants");
     // diagnostic builds only (results wrong for ABL != 0): 1 no insertion,
     // 2 DMA + barriers only, 3 no DMA, 4 no DMA and no insertion, 5 no DMA and
     // no epilogue, 6 = 5 without barriers, 7 event counters, 14 no DMA wait,
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     constexpr bool kNoIns = ABL == 1 || ABL == 4;
     constexpr bool kNoBar = ABL == 6 || ABL == 66 || ABL == 21 || ABL == 69 || ABL == 70;
     // bound exchange period in blocks (diagnostic: 40 none, 41 every 4, 42 every 8, 43 every 16)
-    constexpr int kXch = ABL == 40 ? 0 : ABL == 41 ? 4 : ABL == 42 ? 8 : ABL == 43 ? 16 : 32;
+    constexpr int kXch = (ABL == 40 || MODE != 0) ? 0 : ABL == 41 ? 4 : ABL == 42 ? 8 : ABL == 43 ? 16 : 32;
     // (ABL 53, round 1's placement: an LDS-DMA issue holds its wave for ~45-60
     // cycles, so the two waves of a SIMD issued theirs at different MFMAs)
     constexpr int kDmaTT = 2, kDmaLate = 10;
@@ -381,8 +387,9 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         const Tile tile = a.tiles[t];
         const int64_t bstart = a.bucket_off[tile.c];
         const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
+        // (chunk-list mode: the first chunk_take rows of the chunk, a sample)
         const int nrows = __builtin_amdgcn_readfirstlane(
-            (int)std::min<int64_t>(a.chunk_rows, a.bucket_off[tile.c + 1] - row0));
+            (int)std::min<int64_t>(MODE == 1 ? a.chunk_take : a.chunk_rows, a.bucket_off[tile.c + 1] - row0));
         const uint32_t r0lo = __builtin_amdgcn_readfirstlane((uint32_t)row0);
         const uint32_t r0hi = __builtin_amdgcn_readfirstlane((uint32_t)(row0 >> 32));
         const int64_t row0u = (int64_t)(((uint64_t)r0hi << 32) | r0lo);
@@ -475,8 +482,16 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 if (a.pair_pos && live) thr = std::min(thr, round0_seed(a, pp));
             }
             my_invq = live ? a.invq[q] : 0.0f;
+            if constexpr (MODE == 1) {
+                // (no bound until every bin holds a finished list's 15th)
+                if (live) {
+                    uint32_t bmax = 0u;
+                    for (int j = 0; j < a.nbins; ++j) bmax = std::max(bmax, a.bins[(size_t)pp * a.nbins + j]);
+                    thr = std::min(thr, bmax);
+                }
+            }
         }
-        {
+        if constexpr (MODE != 2) {
             uint64_t E[KL];
             list_clear<KL>(E);
             list_store<KL, 0, ES>(opaque_u(lbase), E);
@@ -535,6 +550,35 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                     atomicAdd(&a.dbg[1], (unsigned long long)nc);
                 }
             }
+            if constexpr (MODE == 2) {
+                // collect: the pair's two lanes reserve their candidates'
+                // slots with one atomic (lane hh = 0), then store them in
+                // row order; slots past cap are counted, not stored
+                if (__any(mask != 0)) {
+                    const uint32_t rb = (uint32_t)(row0u + eb * 32 + 4 * hh);
+                    const uint32_t c = (uint32_t)__builtin_popcount(mask);
+                    const uint32_t cp = partner_u32(c, hh);
+                    uint32_t base = 0;
+                    if (hh == 0 && c + cp != 0) base = atomicAdd(&a.ccount[pp], c + cp);
+                    const uint32_t bp = partner_u32(base, hh);
+                    uint32_t at = hh == 0 ? base : bp + cp;
+                    uint64_t* dst = a.cand + (size_t)pp * (uint32_t)a.cap;
+                    uint32_t m = mask;
+#pragma unroll 1
+                    while (__any(m != 0)) {
+                        if (m != 0) {
+                            const int hb = 31 - __builtin_clz(m);
+                            m ^= 1u << hb;
+                            const int rg = 15 - hb;
+                            const int i = (rg & 3) + 8 * (rg >> 2);
+                            const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
+                            const float d = fmaf(-select16(acc, rg), my_invq * n1, 1.0f);
+                            if (at < (uint32_t)a.cap) dst[at] = make_key(d, rb + (uint32_t)i);
+                            ++at;
+                        }
+                    }
+                }
+            } else
             if (!kNoIns && __any(mask != 0)) {
                 const uint32_t rb = (uint32_t)(row0u + eb * 32 + 4 * hh);
                 // Every lane walks its own candidates, lowest register first:
@@ -747,7 +791,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         }
         if (defer && nblk > 0) epilogue(nblk - 1);
         // lanes still in append mode hold an unsorted (EMPTY-padded) buffer
-        if (!kCoop && __any(cnt < KL)) {
+        if (MODE != 2 && !kCoop && __any(cnt < KL)) {
             if (cnt < KL) {
                 uint64_t L[KL];
                 list_load<KL>(lbase, L);
@@ -758,7 +802,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         __syncthreads();  // every wave's DMA drained (the tail waited vmcnt(0))
 
         // ---- merge the two partial lists of each query (lanes col, col+32) ----
-        if (h == 0 && live) {
+        if (MODE != 2 && h == 0 && live) {
             uint64_t L[KL], P[KL];
             list_load<KL, 0, ES>(lbase, L);
             list_load<KL, 32 * LSTR, ES>(lbase, P);
@@ -770,7 +814,9 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             uint64_t* out = a.partial + ((size_t)pp * a.max_chunks + tile.chunk) * KL;
 #pragma unroll
             for (int i = 0; i < KL; ++i) out[i] = L[i];
-            if (L[KL - 1] != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)L[KL - 1]);
+            if (MODE == 0 && L[KL - 1] != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)L[KL - 1]);
+            if (MODE == 1 && L[KL - 1] != kEmptyKey)
+                atomicMin(&a.bins[(size_t)pp * a.nbins + tile.chunk % a.nbins], (uint32_t)(L[KL - 1] >> 32));
         }
     }
     if constexpr (ABL != 0) {
@@ -791,13 +837,13 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
 
 // one launch of the persistent grid (one workgroup per CU, dynamic LDS);
 // HIP events around it while lmi_timing_enable is on
-template <int KL, int ABL, bool LO = false>
+template <int KL, int ABL, bool LO = false, int MODE = 0>
 int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
     constexpr size_t lds = v3::lds_bytes<KL>();
     static std::once_flag once;
     static hipError_t attr_err = hipSuccess;
     std::call_once(once, [] {
-        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<KL, ABL, LO>,
+        attr_err = hipFuncSetAttribute((const void*)scan3_kernel<KL, ABL, LO, MODE>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     LMI_HIP_TRY(attr_err);
@@ -807,7 +853,7 @@ int launch_scan3_v(const Scan2Args& b, hipStream_t s) {
         const int rc = timing_record(s, true, ev);
         if (rc != LMI_OK) return rc;
     }
-    hipLaunchKernelGGL((scan3_kernel<KL, ABL, LO>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
+    hipLaunchKernelGGL((scan3_kernel<KL, ABL, LO, MODE>), dim3(num_cus()), dim3(v3::NW * 64), lds, s, b);
     LMI_LAUNCH_CHECK("scan3_kernel");
     if (timed) return timing_record(s, false, ev);
     return LMI_OK;

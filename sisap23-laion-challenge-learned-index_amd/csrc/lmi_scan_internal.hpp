@@ -126,6 +126,19 @@ struct Scan2Args {
     const int32_t* pair_pos;    // LMI_Q_SEED_ROUND0: [P] grouped position of the pair's (q, 0), -1 if none; else null
     float seed_margin;          //   (distance added to the seed: 2 eps in the float64 mode)
     unsigned long long* dbg;    // diagnostic counters of the ABL != 0 variants (lmi_scan_abl.hip); null
+    // collect mode (k > 16, scan3_kernel MODE 2): every row of a pair within
+    // its fixed bound goes to cand[pp * cap + i], i from ccount[pp] (grouped
+    // position pp; a count past cap means the pair overflowed)
+    uint64_t* cand;
+    uint32_t* ccount;
+    int32_t cap;
+    // chunk-list mode (MODE 1): nbins distance ordinals per grouped pair, bin
+    // j = the smallest 15th entry of the pair's finished chunk lists j mod
+    // nbins; their maximum bounds nbins * 15 >= kw entries, so entries above
+    // it cannot change the kw-th smallest of the lists (the bound)
+    uint32_t* bins;
+    int32_t nbins;
+    int32_t chunk_take;  // MODE 1: rows scanned from the start of each chunk (<= chunk_rows)
 };
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],
