@@ -151,7 +151,8 @@ struct WideScan {
     int32_t cap;
     uint32_t* bins;  // mode 1: [P][nbins], all ones at the start (Scan2Args::bins)
     int32_t nbins;
-    int32_t take;    // mode 1: rows sampled from the start of every chunk
+    const int32_t* sub_rows;  // mode 1: Scan2Args::sub_rows / sub_take
+    const int32_t* sub_take;
 };
 int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                      const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,

@@ -675,18 +675,31 @@ __device__ inline int wide_slot(int j, int nch_c, uint32_t sm, int S, int X) {
     return part * X + __builtin_ctz(sm);
 }
 
-// the bound pass's chunk table: chunk_first of chunk_rows-row chunks over
-// the index's buckets (one workgroup: a thread per contiguous run of buckets,
-// then a prefix over the threads)
-__global__ __launch_bounds__(256) void sub_chunk_first_kernel(const int64_t* __restrict__ bucket_off,
-                                                              int32_t C, int32_t chunk_rows,
-                                                              int32_t* __restrict__ chunk_first) {
+// The bound pass's lists (one workgroup): bucket c of n_c rows gets L =
+// min(lists, n_c / 32) lists of r_c = n_c / L rows (up to a multiple of 32),
+// each scanning its first take_c = max(128, r_c / 4) rows (a sample); chunk_first
+// is the prefix of the list counts (a thread per contiguous run of buckets, then
+// a prefix over the threads).
+__global__ __launch_bounds__(256) void bound_lists_kernel(const int64_t* __restrict__ bucket_off, int32_t C,
+                                                          int32_t lists, int32_t* __restrict__ chunk_first,
+                                                          int32_t* __restrict__ sub_rows,
+                                                          int32_t* __restrict__ sub_take) {
     __shared__ int32_t part[256];
     const int t = threadIdx.x;
     const int per = (C + 255) / 256;
     const int c0 = min(C, t * per), c1 = min(C, c0 + per);
+    auto count = [&](int c) {
+        const int64_t n = bucket_off[c + 1] - bucket_off[c];
+        if (n <= 0) return 0;
+        const int64_t L = std::max<int64_t>(1, std::min<int64_t>(lists, n / 32));
+        const int64_t r = (n + L - 1) / L;
+        const int32_t rr = (int32_t)((r + 31) / 32 * 32);
+        sub_rows[c] = rr;
+        sub_take[c] = std::min(rr, std::max(128, (rr / 4 + 31) / 32 * 32));
+        return (int)((n + rr - 1) / rr);
+    };
     int32_t acc = 0;
-    for (int c = c0; c < c1; ++c) acc += (int32_t)((bucket_off[c + 1] - bucket_off[c] + chunk_rows - 1) / chunk_rows);
+    for (int c = c0; c < c1; ++c) acc += count(c);
     part[t] = acc;
     __syncthreads();
     if (t == 0) {
@@ -701,7 +714,8 @@ __global__ __launch_bounds__(256) void sub_chunk_first_kernel(const int64_t* __r
     acc = part[t];
     for (int c = c0; c < c1; ++c) {
         chunk_first[c] = acc;
-        acc += (int32_t)((bucket_off[c + 1] - bucket_off[c] + chunk_rows - 1) / chunk_rows);
+        const int64_t n = bucket_off[c + 1] - bucket_off[c];
+        acc += n <= 0 ? 0 : (int32_t)((n + sub_rows[c] - 1) / sub_rows[c]);
     }
     if (c0 < C && c1 == C) chunk_first[C] = acc;
 }
@@ -731,7 +745,8 @@ __global__ __launch_bounds__(64) void kth_bound_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, int32_t S,
     const int32_t* __restrict__ pair_q, const int32_t* __restrict__ pair_bucket,
     const int32_t* __restrict__ chunk_first, const uint32_t* __restrict__ split_mask, int32_t P,
-    int32_t kw, uint32_t* __restrict__ bound_ord, int32_t* __restrict__ fix) {
+    int32_t kw, const int64_t* __restrict__ bucket_off, int32_t cap, uint32_t* __restrict__ bound_ord,
+    int32_t* __restrict__ fix) {
     constexpr int KL = 15;
     const int pp = blockIdx.x;
     const int c = pair_bucket[pp];
@@ -761,7 +776,13 @@ __global__ __launch_bounds__(64) void kth_bound_kernel(
     }
     __syncthreads();
     if (s_n < (uint32_t)kw) {
-        if (tid == 0) fix[p] = 1;  // (bound_ord stays 0: the collect takes nothing)
+        // too few list entries: a bucket of no more rows than the slots is
+        // collected whole (no bound), else the pair takes the fix-up passes
+        // (bound_ord stays 0: the collect takes nothing)
+        if (tid == 0) {
+            if (bucket_off[c + 1] - bucket_off[c] <= cap) bound_ord[p] = 0xffffffffu;
+            else fix[p] = 1;
+        }
         return;
     }
     for (int shift = 24; shift >= 0; shift -= 8) {
@@ -809,8 +830,9 @@ __global__ __launch_bounds__(256) void set_bound_kernel(const int32_t* __restric
 __global__ __launch_bounds__(256) void collect_select_kernel(
     const uint64_t* __restrict__ cand, const uint32_t* __restrict__ ccount, int32_t cap,
     const int32_t* __restrict__ pair_q, const int32_t* __restrict__ pair_bucket,
-    const int32_t* __restrict__ gpos, int32_t P, int32_t kw, int32_t ldo, int32_t* __restrict__ fix,
-    float* __restrict__ out_d, int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row) {
+    const int32_t* __restrict__ gpos, int32_t P, int32_t kw, int32_t ldo,
+    const uint32_t* __restrict__ bound_ord, int32_t* __restrict__ fix, float* __restrict__ out_d,
+    int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row) {
     extern __shared__ uint64_t keys[];
     const int pp = blockIdx.x;
     if (pair_bucket[pp] < 0) return;
@@ -818,7 +840,9 @@ __global__ __launch_bounds__(256) void collect_select_kernel(
     if (p < 0 || p >= P || fix[p]) return;
     const uint32_t n = ccount[pp];
     const int tid = threadIdx.x;
-    if (n > (uint32_t)cap || n < (uint32_t)kw) {
+    // (fewer than kw: only a bucket collected whole, every row under the
+    // all-ones bound; never for a sound scan otherwise)
+    if (n > (uint32_t)cap || (n < (uint32_t)kw && bound_ord[p] != 0xffffffffu)) {
         if (tid == 0) fix[p] = 1;
         return;
     }
@@ -844,7 +868,7 @@ __global__ __launch_bounds__(256) void collect_select_kernel(
         }
     }
     const size_t o = (size_t)p * ldo;
-    for (int i = tid; i < kw; i += 256) {
+    for (int i = tid; i < kw && i < (int)n; i += 256) {
         const uint64_t key = keys[i];
         const uint32_t r = (uint32_t)key;
         out_d[o + i] = ord2f((uint32_t)(key >> 32));
@@ -1216,7 +1240,9 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
     // tail split (scan v3): K = the queue's share of the grid; plan_fill leaves
     // K (S - 1) free slots after every queue for its parts
-    const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ? 0
+    // (not in the wide path's bound scan: its lists are the bucket's own)
+    const int split_k = !w.use_v3 || nearest_first || env_config().scan_split < 0 ||
+                        (wide && wide->mode == 1) ? 0
                         : std::min(kSplitMaxK, env_config().scan_split > 0 ? env_config().scan_split
                                                                             : (num_cus() + ng - 1) / ng);
     if (split_k > 0 && w.split_s < 2) {
@@ -1332,7 +1358,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
             b.cap = wide->cap;
             b.bins = wide->bins;
             b.nbins = wide->nbins;
-            b.chunk_take = wide->take;
+            b.sub_rows = wide->sub_rows;
+            b.sub_take = wide->sub_take;
             rc = wide->mode == 1 ? launch_scan3_v<15, 0, false, 1>(b, s) : launch_scan3_v<10, 0, false, 2>(b, s);
         }
         else if (w.use_v3 && LOP) {
@@ -1440,24 +1467,22 @@ namespace {
 struct WideWs {
     bool on;       // the bound + collect path (else bucket_topk_passes alone)
     int kw, cap;   // list entries produced (passes * kp); candidate slots per pair
-    int sub;       // the bound pass's chunks: the index's chunk_rows / sub
-    size_t bound, fix, cls, ccount, cand, fd, fpos, frow, sub_first, bins, region, region_bytes, total;
-    int nbins;
-    int take;  // rows of every bound-pass chunk scanned (a sample: its first quarter)
+    int lists;     // bound-scan lists per bucket (at most; bound_lists_kernel)
+    int nbins;     // the bound scan's pruning bins per pair (Scan2Args::bins)
+    size_t bound, fix, cls, ccount, cand, fd, fpos, frow, sub_first, sub_rows, sub_take, bins, region,
+        region_bytes, total;
 };
 
-// The bound pass scans chunks of chunk_rows / sub rows: a pair has a bound
-// when its bucket's chunk lists hold kw entries, i.e. ~kw / 15 chunks, so
-// finer chunks give a bound to pairs of smaller buckets and a tighter one to
-// the others (more tiles: each loads its pairs' fragments once).  Host-side
-// values only (workspace sizes must not read the device).
-lmi_index_desc bound_desc(const lmi_index_desc* idx, int sub, const int32_t* sub_first) {
+// The bound scan's index: the same rows and buckets, each bucket cut into at
+// most `lists` lists (bound_lists_kernel; their rows per bucket in sub_rows),
+// no chunk centroids (the nearest-chunk-first plan's units are the index's
+// chunks).  Host-side values only: the workspace size must not read the device.
+lmi_index_desc bound_desc(const lmi_index_desc* idx, int lists, const int32_t* sub_first) {
     lmi_index_desc b = *idx;
-    b.chunk_rows = idx->chunk_rows / sub;
-    b.max_chunks = std::max(idx->max_chunks, 1) * sub;
-    b.n_chunks = idx->n_chunks * sub;
+    b.max_chunks = lists;
+    b.n_chunks = idx->n_buckets * lists;
     b.chunk_first = sub_first;
-    b.chunk_centroid = nullptr;  // (the nearest-chunk-first plan's units are the index's chunks)
+    b.chunk_centroid = nullptr;
     return b;
 }
 
@@ -1468,22 +1493,19 @@ WideWs wide_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int l
     w.kw = np * kp;
     // (two passes are two scans either way: the passes, without the extra kernels)
     w.on = v3_capable(idx, qmode) && kp == 15 && np >= 3 && !env_config().wide_passes;
-    // sub: about kw / 15 / 2 bound-pass chunks per index chunk, pow2, <= 8, and
-    // chunks of >= 256 rows, a multiple of 32
-    w.sub = 1;
-    while (w.sub < 8 && 2 * 15 * w.sub < w.kw && idx->chunk_rows % (64 * w.sub) == 0 &&
-           idx->chunk_rows / (2 * w.sub) >= 256)
-        w.sub *= 2;
     const size_t P = (size_t)nq * R;
     if (!w.on) {
         w.region_bytes = w.total = passes_ws_bytes(idx, nq, R, k, qmode);
         return w;
     }
-    // the bound pass scans the first quarter of every chunk (>= 256 rows): the
-    // kw-th smallest of its lists is about the 4 kw-th distance of the pair,
-    // so the collect scan finds about 4 kw candidates; 8 kw (+ 64) slots
-    // before the fix-up passes take over
-    w.take = std::min(idx->chunk_rows / w.sub, std::max(256, idx->chunk_rows / w.sub / 4));
+    // Bound scan: 2 kw / 15 lists per bucket, so a pair's lists hold 2 kw
+    // entries, each the top-15 of the first quarter of its list's rows: their
+    // kw-th smallest is about the pair's 4 kw-th distance, and the collect scan
+    // finds about 4 kw rows within it; 8 kw (+ 64) slots before the fix-up
+    // passes take over.  Buckets of fewer lists' entries than kw but no more
+    // rows than the slots are collected whole.
+    w.lists = 2 * np;
+    w.nbins = np;  // (np * 15 = kw)
     int cap = 256;
     while (cap < 8 * w.kw + 64) cap <<= 1;
     w.cap = std::min(cap, 8192);
@@ -1502,9 +1524,10 @@ WideWs wide_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int l
     w.fpos = take(P * (size_t)ldo * 4);
     w.frow = take(P * (size_t)ldo * 4);
     w.sub_first = take(((size_t)idx->n_buckets + 1) * 4);
-    w.nbins = np;  // (np * 15 = kw)
+    w.sub_rows = take((size_t)idx->n_buckets * 4);
+    w.sub_take = take((size_t)idx->n_buckets * 4);
     w.bins = take(P * (size_t)w.nbins * 4);
-    const lmi_index_desc bd = bound_desc(idx, w.sub, nullptr);
+    const lmi_index_desc bd = bound_desc(idx, w.lists, nullptr);
     w.region_bytes = std::max({scan_workspace_bytes(&bd, nq, R, 15, qmode),
                                scan_workspace_bytes(idx, nq, R, 10, qmode),
                                passes_ws_bytes(idx, nq, R, k, qmode)});
@@ -1552,13 +1575,15 @@ int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int3
     const int plan_scan = kPhasePlan | kPhaseScan;
     // 1. every (pair, bound-pass chunk part)'s own top-15 -> each pair's bound
     auto* sub_first = (int32_t*)(ws + w.sub_first);
-    hipLaunchKernelGGL(sub_chunk_first_kernel, dim3(1), dim3(256), 0, s, idx->bucket_off, idx->n_buckets,
-                       idx->chunk_rows / w.sub, sub_first);
-    LMI_LAUNCH_CHECK("sub_chunk_first_kernel");
-    const lmi_index_desc bd = bound_desc(idx, w.sub, sub_first);
+    auto* sub_rows = (int32_t*)(ws + w.sub_rows);
+    auto* sub_take = (int32_t*)(ws + w.sub_take);
+    hipLaunchKernelGGL(bound_lists_kernel, dim3(1), dim3(256), 0, s, idx->bucket_off, idx->n_buckets,
+                       w.lists, sub_first, sub_rows, sub_take);
+    LMI_LAUNCH_CHECK("bound_lists_kernel");
+    const lmi_index_desc bd = bound_desc(idx, w.lists, sub_first);
     auto* bins = (uint32_t*)(ws + w.bins);
     LMI_TRY(fill_u32(bins, 0xffffffffu, (size_t)P * w.nbins, s));
-    const WideScan m1{1, nullptr, nullptr, nullptr, 0, bins, w.nbins, w.take};
+    const WideScan m1{1, nullptr, nullptr, nullptr, 0, bins, w.nbins, sub_rows, sub_take};
     int rc = bucket_topk_impl(&bd, q, nq, ldq, classes, R, 15, qmode, fd, fpos, nullptr, status, region,
                               w.region_bytes, s, nullptr, 0, false, false, 0.0f, plan_scan, &m1);
     if (rc != LMI_OK) return rc;
@@ -1567,11 +1592,12 @@ int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int3
         hipLaunchKernelGGL(kth_bound_kernel, dim3((unsigned)P), dim3(64), 0, s,
                            (const uint64_t*)(region + l.partial), l.split_s * bd.max_chunks, l.split_s,
                            (const int32_t*)(region + l.pair_q), (const int32_t*)(region + l.pair_bucket),
-                           sub_first, (const uint32_t*)(region + l.split_mask), P, w.kw, bound, fix);
+                           sub_first, (const uint32_t*)(region + l.split_mask), P, w.kw, idx->bucket_off,
+                           w.cap, bound, fix);
         LMI_LAUNCH_CHECK("kth_bound_kernel");
     }
     // 2. every row within the bound -> sorted, the first kw
-    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, 0};
+    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
     rc = bucket_topk_impl(idx, q, nq, ldq, classes, R, 10, qmode, fd, fpos, nullptr, status, region,
                           w.region_bytes, s, nullptr, 0, false, false, 0.0f, plan_scan, &m2);
     if (rc != LMI_OK) return rc;
@@ -1586,8 +1612,8 @@ int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int3
         LMI_HIP_TRY(attr_err);
         hipLaunchKernelGGL(collect_select_kernel, dim3((unsigned)P), dim3(256), (size_t)w.cap * 8, s, cand,
                            ccount, w.cap, (const int32_t*)(region + l.pair_q),
-                           (const int32_t*)(region + l.pair_bucket), idx->gpos, P, w.kw, ldo, fix, out_d,
-                           out_pos, out_row);
+                           (const int32_t*)(region + l.pair_bucket), idx->gpos, P, w.kw, ldo, bound, fix,
+                           out_d, out_pos, out_row);
         LMI_LAUNCH_CHECK("collect_select_kernel");
     }
     // 3. the pairs without a bound or with too many candidates: the passes,

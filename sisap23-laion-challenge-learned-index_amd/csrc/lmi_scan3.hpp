@@ -386,10 +386,11 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         if (t < 0) break;
         const Tile tile = a.tiles[t];
         const int64_t bstart = a.bucket_off[tile.c];
-        const int64_t row0 = bstart + (int64_t)tile.chunk * a.chunk_rows;
-        // (chunk-list mode: the first chunk_take rows of the chunk, a sample)
+        // (chunk-list mode: the bucket's own list rows, and of each list the
+        // first sub_take rows, a sample)
+        const int64_t row0 = bstart + (int64_t)tile.chunk * (MODE == 1 ? a.sub_rows[tile.c] : a.chunk_rows);
         const int nrows = __builtin_amdgcn_readfirstlane(
-            (int)std::min<int64_t>(MODE == 1 ? a.chunk_take : a.chunk_rows, a.bucket_off[tile.c + 1] - row0));
+            (int)std::min<int64_t>(MODE == 1 ? a.sub_take[tile.c] : a.chunk_rows, a.bucket_off[tile.c + 1] - row0));
         const uint32_t r0lo = __builtin_amdgcn_readfirstlane((uint32_t)row0);
         const uint32_t r0hi = __builtin_amdgcn_readfirstlane((uint32_t)(row0 >> 32));
         const int64_t row0u = (int64_t)(((uint64_t)r0hi << 32) | r0lo);

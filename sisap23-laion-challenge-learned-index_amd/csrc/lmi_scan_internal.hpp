@@ -138,7 +138,8 @@ struct Scan2Args {
     // it cannot change the kw-th smallest of the lists (the bound)
     uint32_t* bins;
     int32_t nbins;
-    int32_t chunk_take;  // MODE 1: rows scanned from the start of each chunk (<= chunk_rows)
+    const int32_t* sub_rows;  // MODE 1: [C] rows per list of each bucket (its chunks)
+    const int32_t* sub_take;  //   and the rows scanned from the start of each (a sample)
 };
 
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] + vmcnt[5:4] at [15:14],

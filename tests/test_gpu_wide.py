@@ -1,8 +1,9 @@
 """k > 16 by bound + collect (csrc/lmi_scan.hip, bucket_topk_wide): a chunk-list
-scan (every chunk part's own top-15) gives each pair a bound -- the kw-th
-smallest of its chunk-list distances --, a collect scan gathers every row
-within it, a sort keeps the first kw; pairs without a bound (too few chunk-list
-entries) or whose candidates overflow take the lower-bound passes.  Every list
+scan (every bucket cut into 2 kw / 15 lists, each the top-15 of a sample of its
+rows) gives each pair a bound -- the kw-th smallest of its lists' distances --,
+a collect scan gathers every row within it, a sort keeps the first kw; buckets
+too small for kw list entries are collected whole, pairs whose candidates
+overflow take the lower-bound passes.  Every list
 entry must equal the passes alone (LMI_WIDE_PASSES=1) bit for bit, in both
 arithmetics, with and without the tail split, and the oracle.  (k of three
 passes or more: two passes are two scans either way and stay passes.)"""
@@ -45,18 +46,6 @@ def _fixed_pairs(ix, q, ct, k, d1, p1, dist="f32"):
     return int((pn != p1).reshape(-1, pn.shape[-1]).any(axis=1).sum())
 
 
-def _no_bound(w, classes, k, chunk_rows):
-    """Pairs whose bucket cannot give a bound: its bound-pass chunks
-    (chunk_rows / sub rows, the rule of lmi_scan.hip wide_ws) hold fewer than
-    kw list entries (split parts, which add lists, ignored: an upper count)."""
-    kw = -(-k // 15) * 15
-    sub = 1
-    while sub < 8 and 30 * sub < kw and chunk_rows % (64 * sub) == 0 and chunk_rows // (2 * sub) >= 256:
-        sub *= 2
-    n_c = np.bincount(w["labels"], minlength=w["C"])[classes]
-    return int((-(-n_c // (chunk_rows // sub)) * 15 < kw).sum())
-
-
 def _setup(w, R, chunk_rows):
     ix = I.DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=chunk_rows, device="cuda")
     classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
@@ -79,10 +68,9 @@ def test_wide_equals_passes(label_mode, k, chunk_rows):
         ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, w["C"])
         assert O.compare_lists(ref_d, ref_p, d1, p1) == 0
     if label_mode != "dup":
-        # the fix-up passes answer the pairs whose bucket cannot give a bound,
-        # and few others
-        assert _fixed_pairs(ix, q, ct, k, d1, p1) <= _no_bound(w, classes, k, chunk_rows) + \
-            classes.size // 20
+        # every bucket gives a bound (2 kw / 15 lists) or is collected whole:
+        # the fix-up passes answer few pairs (candidates past the slots)
+        assert _fixed_pairs(ix, q, ct, k, d1, p1) <= classes.size // 20
 
 
 @pytest.mark.parametrize("split,parts", [(-1, None), (256, None), (256, 4), (3, 3)])
@@ -148,9 +136,9 @@ def test_wide_few_workgroups_and_r1():
 
 @pytest.mark.parametrize("k", [40, 100])
 def test_wide_sampled_bound(k):
-    """Buckets of many chunks: the bound pass scans the first quarter of every
-    bound-pass chunk (a sample); its kw-th smallest still bounds the pair's
-    kw-th distance, the collect scan finds ~4 kw rows within it."""
+    """Large buckets: the bound scan reads the first quarter of every list (a
+    sample); its kw-th smallest still bounds the pair's kw-th distance, the
+    collect scan finds ~4 kw rows within it."""
     w = workloads.clustered(n=60000, nq=300, C=6, seed=83, label_mode="router")
     R = 2
     ix, classes, ct, q = _setup(w, R, 2048)
@@ -158,8 +146,6 @@ def test_wide_sampled_bound(k):
     d1, p1 = _lists(ix, q, ct, k)
     np.testing.assert_array_equal(p1, p0)
     np.testing.assert_array_equal(d1, d0)
-    nb = _no_bound(w, classes, k, 2048)
-    assert nb < classes.size
-    assert _fixed_pairs(ix, q, ct, k, d1, p1) <= nb + classes.size // 20
+    assert _fixed_pairs(ix, q, ct, k, d1, p1) <= classes.size // 20
     ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, w["C"])
     assert O.compare_lists(ref_d, ref_p, d1, p1) == 0
