@@ -77,6 +77,32 @@ def test_workspace_size_is_monotone():
     assert 0 < a < b
 
 
+def test_wide_k_workspace_follows_the_switch(monkeypatch):
+    """k > 30 on the fp16 scan sizes the bound + collect path (candidate slots,
+    both scans' plans, the fix-up passes); LMI_WIDE_PASSES=1 the passes alone;
+    k <= 30 is the passes either way."""
+    lib = _lib.load()
+    d = _lib.IndexDesc()
+    d.dtype, d.d, d.d_pad, d.n_rows, d.n_buckets = _lib.LMI_F16, 768, 768, 10**6, 122
+    d.chunk_rows, d.n_chunks, d.max_chunks = 8192, 200, 5
+    size = lambda k: lib.lmi_scan_workspace_bytes(C.byref(d), 10000, 4, k, _lib.LMI_Q_F16)
+    try:
+        monkeypatch.delenv("LMI_WIDE_PASSES", raising=False)
+        lib.lmi_config_reload()
+        wide100, wide30 = size(100), size(30)
+        monkeypatch.setenv("LMI_WIDE_PASSES", "1")
+        lib.lmi_config_reload()
+        passes100, passes30 = size(100), size(30)
+    finally:
+        monkeypatch.delenv("LMI_WIDE_PASSES", raising=False)
+        lib.lmi_config_reload()
+    assert wide30 == passes30 > 0
+    # the wide workspace holds the passes' own (its fix-up) and 40000 pairs x
+    # 1024 candidate slots of 8 bytes
+    assert wide100 > passes100 + 40000 * 1024 * 8
+    assert size(100) == wide100
+
+
 def test_replay_rejects_the_reference_assert_case():
     """k larger than the merged width: the reference asserts (LearnedIndex.py:99)."""
     from li.index import replay
