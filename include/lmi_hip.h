@@ -167,15 +167,16 @@ size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R
  * 1 <= k <= LMI_MAX_K_PASSES.  k > LMI_MAX_K (the reference takes any k on its
  * R == 1 path, search.py:134-140 -> LearnedIndex.py:103-111, and in
  * Baseline.py:14-19) returns the first kw = 15 * ceil(k/15) entries of the
- * (distance, position) order, computed by the wide path: k <= 30, two scan
- * passes (each keeps the next 15 entries after the previous pass's last); k
- * > 30 on the fp16 scan (fp16 corpus, fp16-exact queries, d = 768), a bound
- * scan (the top-15 of a sample of every chunk: the kw-th smallest of those
- * entries bounds the pair's kw-th distance), a collect scan (every row within
- * the bound) and a sort, two scans whatever k; pairs without a bound (buckets
- * of too few chunks) or with too many candidates take the passes.  Bitwise
- * the same lists either way (LMI_WIDE_PASSES=1: the passes alone).  Same
- * workspace contract (lmi_scan_workspace_bytes). */
+ * (distance, position) order.  On the fp16 scan (fp16 corpus, fp16-exact
+ * queries, d = 768): a bound scan (every bucket cut into 2 kw/15 lists, each
+ * the top-15 of a sample of its rows: the kw-th smallest of those entries
+ * bounds the pair's kw-th distance), a collect scan (every row within the
+ * bound) and a sort -- two scans whatever k; buckets of fewer than ~2 kw rows
+ * are collected whole, pairs whose candidates overflow take lower-bound passes
+ * (ceil(k/15) scans, each keeping the next 15 entries after the previous
+ * pass's last), as does every pair off the fp16 scan.  Bitwise the same lists
+ * either way (LMI_WIDE_PASSES=1: the passes alone).  Same workspace contract
+ * (lmi_scan_workspace_bytes). */
 int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                     const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
                     float* out_d, int32_t* out_pos, int32_t* status,

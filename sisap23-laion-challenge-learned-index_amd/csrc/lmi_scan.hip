@@ -1491,8 +1491,7 @@ WideWs wide_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int l
     int kp;
     const int np = passes_of(idx, qmode, k, &kp);
     w.kw = np * kp;
-    // (two passes are two scans either way: the passes, without the extra kernels)
-    w.on = v3_capable(idx, qmode) && kp == 15 && np >= 3 && !env_config().wide_passes;
+    w.on = v3_capable(idx, qmode) && kp == 15 && !env_config().wide_passes;
     const size_t P = (size_t)nq * R;
     if (!w.on) {
         w.region_bytes = w.total = passes_ws_bytes(idx, nq, R, k, qmode);
