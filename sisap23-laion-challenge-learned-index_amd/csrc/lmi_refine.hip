@@ -147,6 +147,58 @@ __device__ inline double row_dist64(const TC* row, int d, int nps, const double 
     return 1.0 - dot / n;
 }
 
+// row_dist64 of up to kB fp16 rows at once (d % 4 == 0): every row's pieces
+// are loaded before any is used, so a wave waits one memory latency per kB
+// rows instead of one per row, and the 2 kB wave reductions interleave; each
+// row's value is computed in exactly row_dist64's order (the same bits)
+constexpr int kB = 4;
+__device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const int32_t (&r)[kB], int d,
+                                       int nps, const double (&qh)[kMaxPieces][4], double (&out)[kB]) {
+    const int lane = threadIdx.x & 63;
+    uint2 raw[kB][kMaxPieces];
+#pragma unroll
+    for (int b = 0; b < kB; ++b)
+#pragma unroll
+        for (int i = 0; i < kMaxPieces; ++i) {
+            const int e0 = 4 * (lane + 64 * i);
+            raw[b][i] = (r[b] >= 0 && i < nps && e0 + 4 <= d)
+                            ? *reinterpret_cast<const uint2*>(base + (size_t)r[b] * d_pad + e0)
+                            : make_uint2(0u, 0u);
+        }
+    double dot[kB], ss[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        dot[b] = 0.0;
+        ss[b] = 0.0;
+#pragma unroll
+        for (int i = 0; i < kMaxPieces; ++i) {
+            if (i < nps) {
+                _Float16 h[4];
+                __builtin_memcpy(h, &raw[b][i], 8);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double v = (double)h[j];
+                    dot[b] = fma(qh[i][j], v, dot[b]);
+                    ss[b] = fma(v, v, ss[b]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            dot[b] += __shfl_xor(dot[b], off);
+            ss[b] += __shfl_xor(ss[b], off);
+        }
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        double n = sqrt(ss[b]);
+        if (n < 10.0 * kEps64) n = 1.0;
+        out[b] = 1.0 - dot[b] / n;
+    }
+}
+
 __device__ inline bool lt_dp(double a, int32_t pa, double b, int32_t pb) {
     return a < b || (a == b && pa < pb);
 }
@@ -220,11 +272,7 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
     double mine[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) mine[s] = __builtin_inf();
-    for (int j = 0; j < m; ++j) {
-        const int32_t r = shfl_slot(rj, j);
-        if (r < 0 || r >= a.n_rows) continue;
-        const TC* row = rows_of<TC>(a) + (size_t)r * a.d_pad;
-        const double dv = row_dist64<TC>(row, a.d, nps, qh);
+    auto keep = [&](int j, double dv) {
         if (lane == (j & 63)) {
             const int s = j >> 6;
             mine[0] = s == 0 ? dv : mine[0];
@@ -232,7 +280,33 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
             mine[2] = s == 2 ? dv : mine[2];
             mine[3] = s == 3 ? dv : mine[3];
         }
+    };
+    if constexpr (sizeof(TC) == 2) {
+        if (a.d % 4 == 0) {
+            // (the stored fp16 rows: kB at a time)
+            for (int j0 = 0; j0 < m; j0 += kB) {
+                int32_t r[kB];
+#pragma unroll
+                for (int b = 0; b < kB; ++b) {
+                    const int32_t x = j0 + b < m ? shfl_slot(rj, j0 + b) : -1;
+                    r[b] = (x < 0 || x >= a.n_rows) ? -1 : x;
+                }
+                double dv[kB];
+                rows_dist64_f16(rows_of<TC>(a), (size_t)a.d_pad, r, a.d, nps, qh, dv);
+#pragma unroll
+                for (int b = 0; b < kB; ++b)
+                    if (r[b] >= 0) keep(j0 + b, dv[b]);
+            }
+            goto ranked;
+        }
     }
+    for (int j = 0; j < m; ++j) {
+        const int32_t r = shfl_slot(rj, j);
+        if (r < 0 || r >= a.n_rows) continue;
+        const TC* row = rows_of<TC>(a) + (size_t)r * a.d_pad;
+        keep(j, row_dist64<TC>(row, a.d, nps, qh));
+    }
+ranked:
     // rank of every refined entry among the m by (d64, position)
     int rank[kSlots] = {};
     for (int i = 0; i < m; ++i) {
