@@ -102,12 +102,12 @@ __device__ inline void load_piece(const TC* row, int piece, int d, double (&v)[4
 constexpr int kMaxPieces = 4;  // d <= 1024 (4 pieces of 4 per lane)
 
 // q^ for this lane's pieces (sklearn normalize of the query row, float64)
-template <typename TQ>
-__device__ inline void query_hat(const TQ* qrow, int d, int nps, double (&qh)[kMaxPieces][4]) {
+template <typename TQ, int NP = kMaxPieces>
+__device__ inline void query_hat(const TQ* qrow, int d, int nps, double (&qh)[NP][4]) {
     const int lane = threadIdx.x & 63;
     double ss = 0.0;
 #pragma unroll
-    for (int i = 0; i < kMaxPieces; ++i) {
+    for (int i = 0; i < NP; ++i) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int e = 4 * (lane + 64 * i) + j;
@@ -119,18 +119,18 @@ __device__ inline void query_hat(const TQ* qrow, int d, int nps, double (&qh)[kM
     double n = sqrt(wave_sum_d(ss));
     if (n < 10.0 * kEps64) n = 1.0;  // sklearn _handle_zeros_in_scale
 #pragma unroll
-    for (int i = 0; i < kMaxPieces; ++i)
+    for (int i = 0; i < NP; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) qh[i][j] = qh[i][j] / n;
 }
 
 // 1 - <q^, y/|y|> of one stored row, float64 (every lane gets the value)
-template <typename TC>
-__device__ inline double row_dist64(const TC* row, int d, int nps, const double (&qh)[kMaxPieces][4]) {
+template <typename TC, int NP = kMaxPieces>
+__device__ inline double row_dist64(const TC* row, int d, int nps, const double (&qh)[NP][4]) {
     const int lane = threadIdx.x & 63;
     double dot = 0.0, ss = 0.0;
 #pragma unroll
-    for (int i = 0; i < kMaxPieces; ++i) {
+    for (int i = 0; i < NP; ++i) {
         if (i < nps) {
             double v[4];
             load_piece<TC>(row, lane + 64 * i, d, v);
@@ -151,15 +151,17 @@ __device__ inline double row_dist64(const TC* row, int d, int nps, const double 
 // are loaded before any is used, so a wave waits one memory latency per kB
 // rows instead of one per row, and the 2 kB wave reductions interleave; each
 // row's value is computed in exactly row_dist64's order (the same bits)
+// (NPS: pieces per lane known at compile time, 3 for d in (512, 768])
 constexpr int kB = 4;
+template <int NPS>
 __device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const int32_t (&r)[kB], int d,
-                                       int nps, const double (&qh)[kMaxPieces][4], double (&out)[kB]) {
+                                       int nps, const double (&qh)[NPS][4], double (&out)[kB]) {
     const int lane = threadIdx.x & 63;
-    uint2 raw[kB][kMaxPieces];
+    uint2 raw[kB][NPS];
 #pragma unroll
     for (int b = 0; b < kB; ++b)
 #pragma unroll
-        for (int i = 0; i < kMaxPieces; ++i) {
+        for (int i = 0; i < NPS; ++i) {
             const int e0 = 4 * (lane + 64 * i);
             raw[b][i] = (r[b] >= 0 && i < nps && e0 + 4 <= d)
                             ? *reinterpret_cast<const uint2*>(base + (size_t)r[b] * d_pad + e0)
@@ -171,7 +173,7 @@ __device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const
         dot[b] = 0.0;
         ss[b] = 0.0;
 #pragma unroll
-        for (int i = 0; i < kMaxPieces; ++i) {
+        for (int i = 0; i < NPS; ++i) {
             if (i < nps) {
                 _Float16 h[4];
                 __builtin_memcpy(h, &raw[b][i], 8);
@@ -226,8 +228,9 @@ __device__ inline const TQ* query_of(const RefineArgs& a, int64_t q) {
     else return a.q + (size_t)q * a.ldq;
 }
 
-template <typename TC, typename TQ>
-__global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
+// NP: pieces of 4 per lane held for the query (3: d <= 768; 4: d <= 1024)
+template <typename TC, typename TQ, int NP>
+__global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void refine_kernel(RefineArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t p = (int64_t)blockIdx.x * (kRefT / 64) + (threadIdx.x >> 6);
     const int64_t P = (int64_t)a.nq * a.R;
@@ -247,6 +250,10 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
         gj[s] = has ? a.lpos[li + e] : -1;
         n_valid += __popcll(__ballot(rj[s] >= 0));
     }
+    // (the query's loads go out beside the list's)
+    const int nps = (a.d + 255) / 256;
+    double qh[NP][4];
+    query_hat<TQ, NP>(query_of<TQ>(a, p / a.R), a.d, nps, qh);
     double* od = a.out_d + (size_t)p * k;
     int32_t* op = a.out_pos + (size_t)p * k;
     int m;
@@ -266,9 +273,6 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
 #pragma unroll
     for (int s = 0; s < kSlots; ++s)
         if (rj[s] >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);
-    const int nps = (a.d + 255) / 256;
-    double qh[kMaxPieces][4];
-    query_hat(query_of<TQ>(a, p / a.R), a.d, nps, qh);
     double mine[kSlots];
 #pragma unroll
     for (int s = 0; s < kSlots; ++s) mine[s] = __builtin_inf();
@@ -292,7 +296,7 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
                     r[b] = (x < 0 || x >= a.n_rows) ? -1 : x;
                 }
                 double dv[kB];
-                rows_dist64_f16(rows_of<TC>(a), (size_t)a.d_pad, r, a.d, nps, qh, dv);
+                rows_dist64_f16<NP>(rows_of<TC>(a), (size_t)a.d_pad, r, a.d, nps, qh, dv);
 #pragma unroll
                 for (int b = 0; b < kB; ++b)
                     if (r[b] >= 0) keep(j0 + b, dv[b]);
@@ -304,7 +308,7 @@ __global__ __launch_bounds__(kRefT) void refine_kernel(RefineArgs a) {
         const int32_t r = shfl_slot(rj, j);
         if (r < 0 || r >= a.n_rows) continue;
         const TC* row = rows_of<TC>(a) + (size_t)r * a.d_pad;
-        keep(j, row_dist64<TC>(row, a.d, nps, qh));
+        keep(j, row_dist64<TC, NP>(row, a.d, nps, qh));
     }
 ranked:
     // rank of every refined entry among the m by (d64, position)
@@ -466,7 +470,11 @@ namespace lmi {
 namespace {
 template <typename TC, typename TQ>
 void launch_refine(const RefineArgs& a, dim3 grid, dim3 fgrid, hipStream_t s) {
-    hipLaunchKernelGGL((refine_kernel<TC, TQ>), grid, dim3(kRefT), 0, s, a);
+    // (d <= 768: three pieces per lane, the registers of the fourth freed)
+    if (a.d <= 3 * 256)
+        hipLaunchKernelGGL((refine_kernel<TC, TQ, 3>), grid, dim3(kRefT), 0, s, a);
+    else
+        hipLaunchKernelGGL((refine_kernel<TC, TQ, kMaxPieces>), grid, dim3(kRefT), 0, s, a);
     // one workgroup per queued pair (the grid strides over the queue; the
     // queue length is read on the device, usually 0)
     hipLaunchKernelGGL((fallback_kernel<TC, TQ>), fgrid, dim3(kFbT), 0, s, a);
