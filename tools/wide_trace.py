@@ -16,7 +16,10 @@ def main(root):
     starts = [i for i, r in enumerate(rows) if "wide_init_kernel" in r["Kernel_Name"]]
     # per k: warm-up, timed, then (after the passes) the no-fix-up call
     for n, i0 in enumerate(starts[1::3]):
-        i1 = next(i for i in range(i0, len(rows)) if "fix_combine" in rows[i]["Kernel_Name"]) + 1
+        i1 = next((i for i in range(i0, len(rows)) if "fix_combine" in rows[i]["Kernel_Name"]), None)
+        if i1 is None:
+            break
+        i1 += 1
         span = (int(rows[i1 - 1]["End_Timestamp"]) - int(rows[i0]["Start_Timestamp"])) / 1e6
         agg = {}
         for r in rows[i0:i1]:
