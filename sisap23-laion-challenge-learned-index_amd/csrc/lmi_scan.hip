@@ -1508,6 +1508,13 @@ WideWs wide_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode, int l
     int cap = 256;
     while (cap < 8 * w.kw + 64) cap <<= 1;
     w.cap = std::min(cap, 8192);
+    // (candidate slots past 8 GiB -- huge batches at large k -- : the passes,
+    // whose lists are 8x smaller)
+    if (P * (size_t)w.cap * 8 > (size_t(8) << 30)) {
+        w.on = false;
+        w.region_bytes = w.total = passes_ws_bytes(idx, nq, R, k, qmode);
+        return w;
+    }
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t at = off;
