@@ -148,3 +148,28 @@ def test_wide_sampled_bound(k):
     assert _fixed_pairs(ix, q, ct, k, d1, p1) <= classes.size // 20
     ref_d, ref_p = O.bucket_lists(w["labels"], w["x"], w["q"], classes, R, k, w["C"])
     assert O.compare_lists(ref_d, ref_p, d1, p1) == 0
+
+
+def test_wide_edges_tiny_batch_max_k_and_out_of_range_classes():
+    """One query, R = 1, k = 17; k = 1024 on buckets smaller than k (pads past
+    the bucket); pairs whose class is out of range (-1, C) keep (+inf, -1) --
+    all equal to the passes."""
+    w = workloads.clustered(n=6000, nq=64, C=8, seed=89, label_mode="skewed")
+    ix, _, ct, q = _setup(w, 2, 256)
+    d0, p0 = _lists(ix, q[:1], ct[:1, :1].contiguous(), 17, LMI_WIDE_PASSES=1)
+    d1, p1 = _lists(ix, q[:1], ct[:1, :1].contiguous(), 17)
+    np.testing.assert_array_equal(p1, p0)
+    np.testing.assert_array_equal(d1, d0)
+    d0, p0 = _lists(ix, q, ct, 1024, LMI_WIDE_PASSES=1)
+    d1, p1 = _lists(ix, q, ct, 1024)
+    np.testing.assert_array_equal(p1, p0)
+    np.testing.assert_array_equal(d1, d0)
+    assert (p1 == -1).any()  # buckets under 1024 rows: padded
+    bad = ct.clone()
+    bad[::3, 0] = -1
+    bad[1::3, 1] = w["C"]
+    d0, p0 = _lists(ix, q, bad, 40, LMI_WIDE_PASSES=1)
+    d1, p1 = _lists(ix, q, bad, 40)
+    np.testing.assert_array_equal(p1, p0)
+    np.testing.assert_array_equal(d1, d0)
+    assert (p1[::3, 0] == -1).all() and np.isinf(d1[::3, 0]).all()
