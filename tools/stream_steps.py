@@ -15,6 +15,7 @@ ap.add_argument("--eager", action="store_true", help="launch the three branches 
 ap.add_argument("--modes", default="stream", help="comma list of stream (default: lookahead behind the finish), stream-nola (no lookahead), stream-eager, graph-pipe, graph")
 ap.add_argument("--dist", default="f32", choices=["f32", "f64"])
 ap.add_argument("--chunks", default="", help="comma list of chunk rows to try (default: the bench's by W)")
+ap.add_argument("--all-ranks", action="store_true", help="time every rank's stripe of each W (not only rank 0)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
@@ -24,10 +25,11 @@ dist.init_process_group("nccl", rank=0, world_size=1)   # a one-process group: r
 x, q, qn, xn, layers = synth.build_lmi_workload(10_000_000, 10_000, 122, "MLP-5", dev)
 router = DeviceRouter(layers)
 labels = router.argmax(xn); del xn
-for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
-              for ck in (list(map(int, a.chunks.split(","))) if a.chunks else
-                         [8192 if W == 1 else 4096 if W <= 4 else 2048])]:
-    ix = DeviceIndex(x, labels, 122, chunk_rows=ck, rank=0, world=W)
+for W, ck, rk in [(W, ck, rk) for W in map(int, a.worlds.split(","))
+                  for ck in (list(map(int, a.chunks.split(","))) if a.chunks else
+                             [8192 if W == 1 else 4096 if W <= 4 else 2048])
+                  for rk in (range(W) if a.all_ranks else [0])]:
+    ix = DeviceIndex(x, labels, 122, chunk_rows=ck, rank=rk, world=W)
     s = Searcher(ix, router)
     for mode in a.modes.split(","):
         if mode.startswith("stream"):
@@ -43,7 +45,7 @@ for W, ck in [(W, ck) for W in map(int, a.worlds.split(","))
         for _ in range(a.steps):
             fn()
         torch.cuda.synchronize()
-        print(f"world {W} chunk {ck} {a.dist}: {mode} {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step "
+        print(f"world {W} rank {rk} chunk {ck} {a.dist}: {mode} {(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms/step "
               f"(scan WGs {os.environ.get('LMI_SCAN_WGS', 'all CUs')})", flush=True)
         del st, fn
     del s, ix; torch.cuda.empty_cache()
