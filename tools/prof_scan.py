@@ -37,11 +37,16 @@ if a.check:
 runs = [(abl, "") for abl in a.abl.split(",")]
 if a.variants:
     runs = [(abl, v) for v in a.variants.split("|") for abl in a.abl.split(",")]
+prev = []
 for abl, var in runs:
     os.environ["LMI_SCAN_ABL"] = abl
+    for kk in prev:  # (a variant's settings end with it)
+        os.environ.pop(kk, None)
+    prev = []
     for kv in filter(None, var.split(",")):
         kk, vv = kv.split("=")
         os.environ[kk] = vv
+        prev.append(kk)
     _lib.load().lmi_config_reload()
     for _ in range(2):
         bucket_topk(ix, q, classes, 10)
