@@ -41,7 +41,7 @@ sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd
 
 from li import _lib, synth  # noqa: E402
 from li.dist import init_from_env  # noqa: E402
-from li.index import DeviceIndex, DeviceRouter, RowSource, Searcher  # noqa: E402
+from li.index import DeviceIndex, DeviceRouter, RowSource, Searcher, default_chunk_rows  # noqa: E402
 
 METRIC = "queries/sec @ recall≥90% on 10M clip768, 10k-query batch; % HBM roofline"
 PUBLISHED_QPS_10M = 19.42  # README:17,30 — 514.91 s for 10k queries, EPYC 7532, 1 core
@@ -291,12 +291,9 @@ STEP_TEXT = {
                                           "+ K3" if a.gpus > 1 else "") + " + replay + D2H of the "
                          "answer of the batch of three launches before (each a captured graph); every "
                          "batch passes every stage, each timed launch answers one batch"),
-    "graph": lambda a: ("hip-graph replay, batches streamed: each step's H2D of the host batch runs on a "
-                        "copy stream during the previous step's search (double-buffered), + search + D2H "
-                        "of the answer" + ("; the next step is launched before this one's answer is "
-                                           "read (one launch ahead)" if a.one_ahead else "")
-                        if not a.no_pipeline else
-                        "hip-graph replay (H2D of the host batch + search + D2H of the answer)"),
+    "graph": lambda a: ("hip-graph replay per step: a new host batch staged, then its H2D (inside the "
+                        "step: the next batch is not known before it is staged) + search + D2H of "
+                        "the answer"),
     "eager": lambda a: "eager launches (H2D of the host batch + search + D2H)",
 }
 
@@ -348,56 +345,18 @@ def marker_pop():
 
 
 def _gpus_arg(argv):
-    for i, a in enumerate(argv):
-        if a == "--gpus" and i + 1 < len(argv):
-            return int(argv[i + 1])
-        if a.startswith("--gpus="):
-            return int(a.split("=", 1)[1])
-    return 1
+    from li.dist import gpus_arg
+    return gpus_arg(argv)
 
 
 def launch_ranks(n: int, argv, script: str = None) -> int:
     """`python bench.py --gpus N` without a launcher: start N rank processes of
-    this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, one
-    GPU each: LOCAL_RANK = rank mod the visible device count, so on a 1-GPU box
-    with LMI_DIST_BACKEND=gloo the ranks share device 0 as a control-flow
-    rehearsal), relay rank 0's JSON line, and exit with the first failing
-    rank's code (the others are stopped: they would wait at a collective).
-    This process never initialises the GPU (it only counts devices)."""
-    import socket
-    import subprocess
-    ndev = max(1, torch.cuda.device_count())
-    if n > ndev and os.environ.get("LMI_DIST_BACKEND") != "gloo":
-        print(f"[bench] --gpus {n} but {ndev} visible GPU(s): RCCL needs one GPU per rank "
-              f"(LMI_DIST_BACKEND=gloo rehearses the ranks on shared devices)", file=sys.stderr)
-        return 2
-    sk = socket.socket()
-    sk.bind(("127.0.0.1", 0))
-    port = sk.getsockname()[1]
-    sk.close()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r % ndev), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv),
-                                      env=env, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    rc = 0
-    live = set(range(n))
-    while live:
-        for r in sorted(live):
-            c = procs[r].poll()
-            if c is None:
-                continue
-            live.discard(r)
-            if c != 0 and rc == 0:
-                rc = c
-                for o in live:
-                    procs[o].terminate()
-        time.sleep(0.05)
-    out = procs[0].stdout.read().decode()
-    sys.stdout.write(out)
-    sys.stdout.flush()
-    return rc
+    this script (li.dist.launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* in their env, one GPU each), relay rank 0's JSON line, and exit
+    with the first failing rank's code (the other ranks are stopped: they
+    would wait at a collective).  This process never initialises the GPU."""
+    from li.dist import launch_ranks as _launch
+    return _launch(n, argv, script or os.path.abspath(__file__), relay_stdout=True)
 
 
 def main():
@@ -435,12 +394,9 @@ def main():
                          "copy stream) instead of the batch stream (StreamedSearch, the default: the "
                          "H2D + plan of batch b+2, the scan of b+1 and the merge/replay/D2H of b per "
                          "launch on four streams; DESIGN.md §5)")
-    ap.add_argument("--one-ahead", action="store_true",
-                    help="launch each step before reading the previous step's answer "
-                         "(GraphedSearch.launch / result; measured no faster, DESIGN.md §5)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="upload each batch inside its own step instead of during the previous "
-                         "step's search (GraphedSearch(pipeline=True), the default)")
+                    help="one captured graph instead of two (GraphedSearch(pipeline=False)); with "
+                         "a new batch staged per step either way uploads inside the step")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager step (every launch from the host) instead of the "
                          "HIP-graph replay of the captured step")
@@ -456,7 +412,7 @@ def main():
 
     rank, world, local = init_from_env()
     if args.chunk_rows is None:
-        args.chunk_rows = 8192 if world == 1 else 4096 if world <= 4 else 2048
+        args.chunk_rows = default_chunk_rows(world)
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world} (set by the launcher); "
             f"using {world}")
@@ -790,28 +746,31 @@ def main():
     tflops = flops / (scan_ms * 1e-3) / 1e12
     # the committed PMC passes profile the default (10M, 1 GPU) command only
     traffic, traffic_src = pmc_traffic(scan_ms) if (args.scale == "10M" and world == 1) else (None, None)
-    # the bound is the roof the kernel's arithmetic intensity puts it under:
-    # flops / algorithmic bytes above the dense-fp16 ridge (2.5 PF / 8 TB/s =
-    # 312 flop/B) means MFMA-bound (401 flop/B at configs[2])
-    # north_star and BASELINE.md state the target as a fraction of the HBM
-    # roofline, so `frac` is the HBM fraction; the kernel's arithmetic intensity
-    # (flops / algorithmic bytes, 401 flop/B at configs[2]) is above the dense
-    # fp16 ridge (2.5 PF / 8 TB/s = 312 flop/B), so the MFMA roof is the lower
-    # one: its fraction rides beside as mfma_frac
+    # `bound` is the roof the kernel's arithmetic intensity selects: flops /
+    # algorithmic bytes (401 flop/B at configs[2]) above the dense-fp16 ridge
+    # (2.5 PF / 8 TB/s = 312 flop/B) means MFMA-bound, and achieved / peak /
+    # frac are then flops against the dense fp16 peak.  north_star states its
+    # target as a fraction of the HBM roofline: that fraction rides beside as
+    # hbm_frac (algorithmic bytes / kernel time / 8 TB/s) whichever roof binds.
     ai = flops / byts
     mfma_roof = ai > F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9)
-    roof = {"bound": "hbm",
-            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "lower_roof_by_intensity": "mfma" if mfma_roof else "hbm",
+    if mfma_roof:
+        head = {"bound": "mfma", "achieved": round(tflops, 1), "peak": F16_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(tflops / F16_PEAK_TFLOPS, 4)}
+    else:
+        head = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    roof = {**head,
             "traffic": None if traffic is None else int(traffic),
             "traffic_source": traffic_src,
             "kernel": "scan3_kernel (lmi_bucket_topk)", "kernel_ms": round(scan_ms, 4),
             "kernel_ms_source": scan_stats.get(args.dist) or
                                 "HIP events around the scan kernel over K eager steps (lmi_timing)",
             "arithmetic_intensity_flop_per_byte": round(ai, 1),
+            "ridge_flop_per_byte": round(F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9), 1),
             "algorithmic_bytes": int(byts), "flops": flops,
             "hbm_gbs": round(achieved, 1), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+            "hbm_target_note": "north_star's target is >= 0.50 of the HBM roofline (hbm_frac)",
             "mfma_tflops": round(tflops, 1), "mfma_frac": round(tflops / F16_PEAK_TFLOPS, 4)}
     sample = min(args.recall_sample, args.nq)
     truth = exact_knn(x, q[:sample], args.k)
@@ -846,8 +805,7 @@ def main():
                                          "bytes_per_rank": int(h2d[2]),
                                          "queries_staged_as": "f16" if q16_exact else "f32",
                                          "in_step": True,
-                                         "overlapped": step_mode.get(args.dist) == "stream" or (
-                                             step_mode.get(args.dist) == "graph" and not args.no_pipeline)},
+                                         "overlapped": step_mode.get(args.dist, "").startswith("stream")},
         "dist": args.dist,
         "step": STEP_TEXT[step_mode.get(args.dist, "eager").split(" ")[0]](args) +
                 step_mode.get(args.dist, "eager")[len(step_mode.get(args.dist, "eager").split(" ")[0]):] +

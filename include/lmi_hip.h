@@ -373,7 +373,11 @@ int32_t lmi_abi_version(void);
 /* The LMI_* environment switches (diagnostic variants and tuning knobs; results
  * never depend on them) are read once, at the first launch.  Diagnostics that
  * change them inside one process call this to re-read them; not for use while
- * another thread launches. */
+ * another thread launches.  The scan's workspace layout depends on the tail
+ * split knobs (LMI_SCAN_SPLIT, LMI_SCAN_SPLIT_PARTS, LMI_SCAN_NO_PREF): after a
+ * reload, size the workspaces again (lmi_scan_workspace_bytes /
+ * lmi_scan_f64_workspace_bytes) -- a workspace sized under the old knobs may
+ * be refused with LMI_E_WORKSPACE, never overrun. */
 int lmi_config_reload(void);
 
 #ifdef __cplusplus

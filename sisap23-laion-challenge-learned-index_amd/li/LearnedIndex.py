@@ -24,9 +24,21 @@ reference re-gathers every bucket on every call: LearnedIndex.py:152-153, :168).
 calls with the SAME objects skip the content hash: the caller promises not to
 change those frames in place (or calls `attach` again).  search.py's CLI
 attaches before its timed loop, as it never mutates its frames.
+
+Process-group mode (an addition): one process per GPU, every
+rank holding the same frames and making the same calls.  `use_process_group`
+(automatic under a launcher that sets WORLD_SIZE > 1, e.g. torchrun or
+`search.py --gpus N`; LMI_SHARD=0 turns that off) makes each rank build only
+its stripe of every bucket (li.index.BucketLayout.shard) and run
+`search` / `search_single` as li.index.Searcher's striped path: the router
+sharded by queries, K2 on the stripe, one all-gather of the packed lists,
+K3 and the replay on every rank -- so every rank returns the same answer,
+bitwise the one-process answer.  `build` trains on rank 0 and broadcasts the
+router and the object labels, so every rank indexes the same buckets.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import numpy as np
@@ -38,6 +50,12 @@ from .model import NeuralNetwork, data_X_to_torch, LIDataset
 
 torch.manual_seed(2023)
 np.random.seed(2023)
+
+# LMI_AUTO_ATTACH=1: the first search / search_single call attaches its frames
+# (LearnedIndex.attach), so an unchanged caller (the reference's own search.py)
+# does not hash the corpus on every later call; the caller then must not change
+# the frames in place.  Off by default: every call checks the content.
+_AUTO_ATTACH = os.environ.get("LMI_AUTO_ATTACH") == "1"
 
 
 def content_key(a) -> tuple:
@@ -120,6 +138,7 @@ class LearnedIndex(Logger):
     _searcher = None
     _attached_labels = None
     _cat_written = None
+    _pg = None        # process-group mode: (group, rank, world, chunk_rows)
 
     def __init__(self):
         self.model = None
@@ -132,9 +151,40 @@ class LearnedIndex(Logger):
         """Pickle (save_as_pickle, utils.py:46-60) what the reference pickles:
         the model; the HBM index and its caches stay out of the file."""
         st = dict(self.__dict__)
-        for key in ("_index", "_cache_key", "_trusted", "_searcher", "_attached_labels", "_cat_written"):
+        for key in ("_index", "_cache_key", "_trusted", "_searcher", "_attached_labels", "_cat_written",
+                    "_pg"):
             st.pop(key, None)
         return st
+
+    # ---- process-group mode --------------------------------------------------
+    def use_process_group(self, group=None, chunk_rows=None):
+        """Shard this index over the ranks of `group` (default: the default
+        process group, which must be initialised: li.dist.init_from_env).
+        Rank g builds slice g of every bucket; search / search_single return
+        the whole answer on every rank.  `chunk_rows`: the scan's chunk of a
+        stripe (default li.index.default_chunk_rows(world))."""
+        import torch.distributed as dist
+        from .index import default_chunk_rows
+        if not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("use_process_group: torch.distributed is not initialised "
+                               "(li.dist.init_from_env)")
+        world = dist.get_world_size(group)
+        self._pg = (group, dist.get_rank(group), world,
+                    int(chunk_rows) if chunk_rows else default_chunk_rows(world))
+        self._index = self._searcher = self._cache_key = self._trusted = None
+        self._cat_written = None
+        return self
+
+    def _proc_group(self):
+        """The process-group mode's (group, rank, world, chunk_rows), or None.
+        Entered on first use when a launcher set WORLD_SIZE > 1 (torchrun,
+        search.py --gpus N), unless LMI_SHARD=0."""
+        if self._pg is None and int(os.environ.get("WORLD_SIZE", "1")) > 1 and \
+                os.environ.get("LMI_SHARD", "1") != "0":
+            from .dist import init_from_env
+            init_from_env()
+            self.use_process_group()
+        return self._pg
 
     # ---- index ------------------------------------------------------------
     def _identity(self, data_navigation, data_search, labels):
@@ -199,7 +249,9 @@ class LearnedIndex(Logger):
         n_buckets = self._n_buckets(labels)
         self._index = None
         self._searcher = None
-        self._index = DeviceIndex(rows, labels, n_buckets, ids=ids)
+        pg = self._proc_group()
+        shard = {} if pg is None else dict(rank=pg[1], world=pg[2], chunk_rows=pg[3])
+        self._index = DeviceIndex(rows, labels, n_buckets, ids=ids, **shard)
         self._cache_key = key
         return self._index
 
@@ -210,7 +262,8 @@ class LearnedIndex(Logger):
         router = self.model.router() if self.model is not None else None
         s = self._searcher
         if s is None or s.index is not index or s.router is not router:
-            s = self._searcher = Searcher(index, router)
+            pg = self._proc_group()
+            s = self._searcher = Searcher(index, router, None if pg is None else pg[0])
         return s
 
     def _n_buckets(self, labels):
@@ -228,6 +281,8 @@ class LearnedIndex(Logger):
         `semantics="exact"` (an addition; default off) returns the exact top-k of
         the union of the probed buckets instead of the reference's round merge."""
         assert self.model is not None, 'Model is not trained, call `build` first.'
+        if _AUTO_ATTACH and self._trusted is None:
+            self.attach(data_navigation, data_search, pred_categories)
         self._set_category(data_navigation, pred_categories)   # :67 (caller-visible side effect)
         index = self._device_index(data_navigation, data_search, pred_categories)
         q_nav = data_X_to_torch(queries_navigation).to(index.device)
@@ -242,6 +297,8 @@ class LearnedIndex(Logger):
         is the per-query bucket; object labels come from
         data_navigation['category'] as in the reference's groupby (:143)."""
         from .index import replay, replay_device
+        if _AUTO_ATTACH and self._trusted is None:
+            self.attach(data_navigation, data_search, np.asarray(data_navigation['category']))
         index = self._device_index(data_navigation, data_search,
                                    data_navigation['category'] if self._trusted is None
                                    else self._labels_of(data_navigation))
@@ -301,16 +358,44 @@ class LearnedIndex(Logger):
         """LearnedIndex.py:197-240: cluster, train the router, label the data
         with the router's argmax (predict on the GPU router kernel)."""
         s = time.time()
-        _, labels = self.cluster(data, n_categories)
-        dataset = LIDataset(data, labels)
-        train_loader = torch.utils.data.DataLoader(
-            dataset, batch_size=256,
-            sampler=torch.utils.data.SubsetRandomSampler(data.index.values.tolist()))
-        nn = NeuralNetwork(input_dim=data.shape[1], output_dim=n_categories, lr=lr,
-                           model_type=model_type)
-        nn.train_batch(train_loader, epochs=epochs, logger=self.logger)
-        self.model = nn
-        return nn.predict(data_X_to_torch(data)), time.time() - s
+        pg = self._proc_group()
+        if pg is None or pg[1] == 0:
+            _, labels = self.cluster(data, n_categories)
+            dataset = LIDataset(data, labels)
+            train_loader = torch.utils.data.DataLoader(
+                dataset, batch_size=256,
+                sampler=torch.utils.data.SubsetRandomSampler(data.index.values.tolist()))
+            nn = NeuralNetwork(input_dim=data.shape[1], output_dim=n_categories, lr=lr,
+                               model_type=model_type)
+            nn.train_batch(train_loader, epochs=epochs, logger=self.logger)
+            self.model = nn
+            pred = nn.predict(data_X_to_torch(data))
+        if pg is not None:
+            # every rank must index the same buckets: rank 0's router and
+            # labels, broadcast (GPU training is not promised bit-reproducible)
+            pred = self._share_build(pg, None if pg[1] else (self.model, pred),
+                                     data.shape[1], n_categories, lr, model_type)
+        return pred, time.time() - s
+
+    def _share_build(self, pg, built, input_dim, n_categories, lr, model_type):
+        """Broadcast rank 0's trained router (state_dict) and object labels to
+        every rank of the process group; returns the labels."""
+        import torch.distributed as dist
+        group = pg[0]
+        src = 0 if group is None else dist.get_global_rank(group, 0)
+        if built is not None:
+            nn, pred = built
+            state = {k: v.detach().cpu().numpy() for k, v in nn.model.state_dict().items()}
+            obj = [(state, np.asarray(pred), nn.model.n_output_neurons)]
+        else:
+            obj = [None]
+        dist.broadcast_object_list(obj, src=src, group=group)
+        state, pred, n_out = obj[0]
+        if built is None:
+            nn = NeuralNetwork(input_dim=input_dim, output_dim=n_out, lr=lr, model_type=model_type)
+            nn.model.load_state_dict({k: torch.from_numpy(v) for k, v in state.items()})
+            self.model = nn
+        return pred
 
     def cluster(self, data, n_clusters):
         """LearnedIndex.py:242-282: k-means labels of the navigation data.  The

@@ -39,7 +39,9 @@ def init_from_env(backend: Optional[str] = None):
         # GPU (RCCL refuses two ranks on one device); collectives then stage
         # through host memory (_all_gather).  The product path is RCCL.
         backend = os.environ.get("LMI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
-    if backend == "nccl":
+    if backend == "nccl" or torch.cuda.is_available():
+        # the rank's own GPU (gloo ranks too: on a 1-GPU rehearsal LOCAL_RANK
+        # is 0 for every rank)
         torch.cuda.set_device(local)
     if not dist.is_initialized():
         # a rank that dies or raises inside a collective must not leave the
@@ -49,6 +51,79 @@ def init_from_env(backend: Optional[str] = None):
         timeout = datetime.timedelta(seconds=float(os.environ.get("LMI_DIST_TIMEOUT_S", "300")))
         dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout)
     return rank, world, local
+
+
+def rank_world(group=None):
+    """(rank, world) of an initialised process group, else (0, 1)."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group), dist.get_world_size(group)
+    return 0, 1
+
+
+def is_writer(group=None) -> bool:
+    """True on the rank that writes files (results, pickles): rank 0 of an
+    initialised process group, or the only process."""
+    return rank_world(group)[0] == 0
+
+
+def gpus_arg(argv, flag: str = "--gpus") -> int:
+    """The value of `--gpus N` / `--gpus=N` in argv (1 when absent), read
+    before argparse so a launcher can start its ranks before any GPU call."""
+    for i, a in enumerate(argv):
+        if a == flag and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith(flag + "="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def launch_ranks(n: int, argv, script: str, relay_stdout: bool = True) -> int:
+    """Start n rank processes of `script` (one GPU each) without a launcher:
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in every child's env, LOCAL_RANK
+    = rank mod the visible device count (on a 1-GPU box with
+    LMI_DIST_BACKEND=gloo the ranks share device 0, a control-flow rehearsal).
+    With `relay_stdout` rank 0's stdout is captured and relayed when the ranks
+    end (bench.py's single JSON line) and the other ranks' is dropped;
+    otherwise every child inherits this process's streams.  Returns the first
+    failing rank's exit code (the other ranks are then stopped: they would
+    wait at a collective), else 0.  This process never initialises the GPU
+    (it only counts devices) and never execs: the ranks are children."""
+    import socket
+    import subprocess
+    import sys
+    import time
+    ndev = max(1, torch.cuda.device_count())
+    if n > ndev and os.environ.get("LMI_DIST_BACKEND") != "gloo":
+        print(f"[launch] {n} ranks but {ndev} visible GPU(s): RCCL needs one GPU per rank "
+              f"(LMI_DIST_BACKEND=gloo rehearses the ranks on shared devices)", file=sys.stderr)
+        return 2
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r % ndev), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out = (subprocess.PIPE if r == 0 else subprocess.DEVNULL) if relay_stdout else None
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env, stdout=out))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c
+                for o in live:
+                    procs[o].terminate()
+        time.sleep(0.05)
+    if relay_stdout:
+        sys.stdout.write(procs[0].stdout.read().decode())
+        sys.stdout.flush()
+    return rc
 
 
 def _all_gather(out: torch.Tensor, part: torch.Tensor, group=None):

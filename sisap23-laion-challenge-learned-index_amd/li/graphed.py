@@ -224,6 +224,9 @@ class GraphedSearch:
         self.graph = self.graphs[0]
         self._slot = 0
         self._fresh = [True, True]   # d_blks[slot] holds the staged batch
+        # upload the staged batch into the idle slot while a step runs (a batch
+        # replayed again, run() without arguments); off once run() stages
+        self._prefetch = True
         torch.cuda.synchronize(dev)
 
     def stage(self, q_nav, q_search) -> bool:
@@ -277,6 +280,10 @@ class GraphedSearch:
         if q_nav is not None or q_search is not None:
             if q_nav is None or q_search is None:
                 raise ValueError("stage both q_nav and q_search")
+            # a caller that stages per run replaces the host batch before the
+            # next run: uploading this one into the other slot ahead would be
+            # wasted PCIe traffic, so the prefetch is off from now on
+            self._prefetch = False
             if not self.stage(q_nav, q_search):
                 return self._eager(q_nav, q_search)
         if self.pipeline:
@@ -331,8 +338,11 @@ class GraphedSearch:
 
     def _run_pipelined(self, dev):
         """Replay the current slot's graph; meanwhile upload the staged batch
-        into the other slot for the next run (a stream of batches: the copy
-        engine moves batch i + 1 while batch i is searched)."""
+        into the other slot for the next run when it will replay the same
+        staged batch (the copy engine moves it while this step searches).  A
+        caller that stages a new batch per run (run(q_nav, q_search)) uploads
+        each batch into its slot just before that slot's replay: then the H2D
+        is inside the step, not beside the previous one."""
         main = torch.cuda.current_stream(dev)
         slot = self._slot
         if not self._fresh[slot]:
@@ -342,7 +352,7 @@ class GraphedSearch:
         self._done_ev[slot].record(main)
         self._fresh[slot] = False
         nxt = 1 - slot
-        if not self._fresh[nxt]:
+        if not self._fresh[nxt] and self._prefetch:
             self._upload(nxt)
         self._slot = nxt
 

@@ -34,6 +34,13 @@ from . import _lib
 from ._lib import check, ptr
 
 DEFAULT_CHUNK_ROWS = 8192
+
+
+def default_chunk_rows(world: int) -> int:
+    """The scan's chunk (rows) for a shard of a `world`-rank index: 8192 on one
+    GPU, 4096 on 2-4, 2048 on more, so a 1/world stripe still cuts into enough
+    tiles to fill 256 CUs (DESIGN.md §5 "Chunk size"; tools/gpu_shards.sh)."""
+    return DEFAULT_CHUNK_ROWS if world <= 1 else 4096 if world <= 4 else 2048
 # LMI_Q_SEED_ROUND0 in the thresholded reference replay (LMI_NO_SEED=1: off,
 # for A/B measurements; results are the same either way)
 _SEED_ROUND0 = os.environ.get("LMI_NO_SEED") != "1"

@@ -76,8 +76,10 @@ def data_to_torch(data, labels) -> Tuple[torch.FloatTensor, torch.LongTensor]:
 
 
 def get_device() -> torch.device:
+    """model.py:99-111 (cuda:0 there): the process's current device, which is
+    cuda:0 in one process and the rank's own GPU under a launcher."""
     use_cuda = torch.cuda.is_available()
-    device = torch.device("cuda:0" if use_cuda else "cpu")
+    device = torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu")
     torch.backends.cudnn.benchmark = True
     return device
 
@@ -101,6 +103,14 @@ class NeuralNetwork(Logger):
         self.optimizer = torch.optim.Adam(self.model.parameters(), lr=lr)
         self._router = None
         self._router_version = None
+
+    def __getstate__(self):
+        """Pickle what the reference pickles: the device router (ctypes
+        descriptors over HBM) is rebuilt from the weights after loading."""
+        st = dict(self.__dict__)
+        st.pop("_router", None)
+        st.pop("_router_version", None)
+        return st
 
     # ---- training (index build; unchanged semantics, torch) ----------------
     def train(self, data_X, data_y, epochs=500, logger=None):

@@ -13,7 +13,10 @@ from pathlib import Path
 
 
 def save_as_pickle(filename: str, obj):
-    """utils.py:46-60."""
+    """utils.py:46-60 (in a process group, rank 0 writes the file)."""
+    from .dist import is_writer
+    if not is_writer():
+        return
     with open(filename, "wb") as f:
         pickle.dump(obj, f)
 
@@ -31,7 +34,11 @@ def prepare(kind, size):
 def store_results(dst, algo, kind, dists, anns, buildtime, querytime, params, size):
     """utils.py:85-97: HDF5 with attrs algo/data/buildtime/querytime/size/params
     and datasets knns (uint32) and dists (float64), read by eval/ — written by
-    the native libhdf5 shim (li.h5, liblmi_h5.so)."""
+    the native libhdf5 shim (li.h5, liblmi_h5.so).  In a process group every
+    rank holds the same answer and rank 0 writes the file."""
     from . import h5
+    from .dist import is_writer
+    if not is_writer():
+        return
     os.makedirs(Path(dst).parent, exist_ok=True)
     h5.write_results(dst, algo, kind, dists, anns, buildtime, querytime, params, size)

@@ -8,6 +8,14 @@ result/{kind}/{size}/learned-index-...h5 (utils.py:85-97) read by eval/.
 
 Differences: the data must already be under data/ (no network here), and
 `--synthetic N` runs the same flow on an N-row synthetic clip768-like set.
+
+`--gpus N` (an addition) shards the index over N GPUs of one node: without a
+launcher the script starts its own N rank processes before any GPU call
+(li.dist.launch_ranks; under torchrun it runs as one of the ranks).  Every
+rank loads the same files and runs the same flow; li.LearnedIndex's
+process-group mode builds one stripe of every bucket per rank and returns the
+whole answer on every rank; rank 0 writes the H5 file.  The results are
+bitwise those of one GPU.
 """
 import argparse
 import logging
@@ -64,6 +72,14 @@ def _synthetic(n, nq=10_000):
 def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc=None,
         n_categories=None, epochs=100, model_type='MLP', lr=0.1, preprocess=False, save=False,
         synthetic=0, semantics='reference', index_path=None):
+    rank, world = 0, 1
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        # one rank of `--gpus N` / torchrun: the process group (and this
+        # rank's GPU) first, before the router or the index touch a device
+        from li.dist import init_from_env
+        rank, world, _ = init_from_env()
+        if rank:
+            logging.getLogger().setLevel(logging.WARNING)
     n_buckets_perc = [int((b / 100) * n_categories) for b in n_buckets_perc]   # search.py:37-38
     n_buckets_perc = list(set([b for b in n_buckets_perc if b > 0]))
     LOG.info(f'Running with: kind={kind}, key={key}, size={size}, n_buckets_perc={n_buckets_perc}, '
@@ -113,6 +129,11 @@ def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc
         save_as_pickle(f'./models/{kind}-{size}-ep={epochs}-lr={lr}-cat={n_categories}'
                        f'-model={model_type}-prep={preprocess}.pkl', li)
     for bucket in n_buckets_perc:
+        if world > 1:
+            # the ranks enter the timed span together, so rank 0's clock is
+            # the job's (each call ends in collectives every rank joins)
+            import torch.distributed as dist
+            dist.barrier()
         s = time.time()
         LOG.info(f'Searching with {bucket} buckets')
         if bucket > 1:
@@ -137,6 +158,11 @@ def run(kind, key, size='100K', k=10, index_type='learned-index', n_buckets_perc
 
 
 if __name__ == "__main__":
+    from li.dist import gpus_arg, launch_ranks
+    if gpus_arg(sys.argv[1:]) > 1 and "WORLD_SIZE" not in os.environ:
+        # before anything touches a GPU: the ranks are child processes
+        sys.exit(launch_ranks(gpus_arg(sys.argv[1:]), sys.argv[1:], os.path.abspath(__file__),
+                              relay_stdout=False))
     parser = argparse.ArgumentParser()
     parser.add_argument("--dataset", default="pca96v2")
     parser.add_argument("--emb", default="pca96")
@@ -156,6 +182,9 @@ if __name__ == "__main__":
     parser.add_argument("--semantics", default="reference", choices=["reference", "exact"],
                         help='reference: LearnedIndex.search round merge (default); exact: exact '
                              'top-k over the probed buckets')
+    parser.add_argument("--gpus", default=1, type=int,
+                        help='shard the index over N GPUs of this node (one process per GPU, '
+                             'started by this script unless a launcher set WORLD_SIZE)')
     parser.add_argument("--index", default=None,
                         help='load a pickled LearnedIndex (save_as_pickle format) instead of '
                              'building one; its router labels the data')

@@ -1,7 +1,7 @@
 """Device replay (K4) timing on bench-shaped random lists: 10k queries, R=4,
 122 buckets of skewed popularity, k=10; torch events around lmi_replay_device.
-With LMI_LIB_NAME=liblmi_hip_abl.so, LMI_REPLAY_ABL=1/2/3 stop the group kernel
-after grouping / U / selection (diagnostic: results then wrong)."""
+(The round-2 phase study's LMI_REPLAY_ABL stops are no longer in the library;
+profiles/r02_replay_phases.txt keeps its numbers.)"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
