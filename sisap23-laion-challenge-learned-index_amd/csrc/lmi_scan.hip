@@ -1413,6 +1413,47 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     return LMI_OK;
 }
 
+#ifdef LMI_DIAG
+// Diagnostic (the `make ablation` library only): lower every pair's global
+// bound before the SCAN phase, e.g. to the final k-th distance of the
+// all-rank lists (tools/bound_study.py: how much of a stripe's scan the
+// per-rank bound costs).  Call after the PLAN phase of lmi_bucket_topk with
+// the same arguments; seed_ord[pair id] is a distance ordinal (f2ord), the
+// bound keeps every row at or under it (ties survive).
+namespace {
+__global__ __launch_bounds__(256) void debug_seed_bounds_kernel(const int32_t* __restrict__ pair_q, int32_t P,
+                                                                const uint32_t* __restrict__ seed_ord,
+                                                                unsigned long long* __restrict__ thr_g) {
+    const int pp = blockIdx.x * 256 + threadIdx.x;
+    if (pp >= P) return;
+    const int p = pair_q[pp];
+    if (p < 0 || p >= P) return;
+    const unsigned long long v = ((unsigned long long)seed_ord[p] << 32) | 0xffffffffull;
+    if (v < thr_g[pp]) thr_g[pp] = v;
+}
+}  // namespace
+
+extern "C" int lmi_debug_seed_bounds(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
+                                     int32_t qmode, const uint32_t* seed_ord, void* workspace,
+                                     void* stream) {
+    using namespace lmi;
+    qmode &= ~LMI_Q_SEED_ROUND0;
+    take_phases(qmode);
+    const WsLayout w = ws_layout(idx, nq, R, k, qmode);
+    if (!w.use_v3) {
+        set_error("seeded bounds need scan v3");
+        return LMI_E_UNSUPPORTED;
+    }
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    const int P = nq * R;
+    hipLaunchKernelGGL(debug_seed_bounds_kernel, dim3((P + 255) / 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), (const int32_t*)(ws + w.pair_q), P, seed_ord,
+                       (unsigned long long*)(ws + w.thr_g));
+    LMI_LAUNCH_CHECK("debug_seed_bounds_kernel");
+    return LMI_OK;
+}
+#endif
+
 namespace lmi {
 // k > 16: ceil(k / kp) scan passes of kp-entry lists (kp = 15 on scan v3, else
 // 16), each keeping the next kp entries of the (distance, position) order

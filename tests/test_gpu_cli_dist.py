@@ -30,9 +30,13 @@ def _cli(cwd, extra, timeout=240, **env_extra):
     os.makedirs(cwd, exist_ok=True)
     env = dict(os.environ, LMI_DIST_BACKEND="gloo", LMI_DIST_TIMEOUT_S="120", **env_extra)
     env.pop("WORLD_SIZE", None)
+    import time
+    t0 = time.time()
     r = subprocess.run([sys.executable, CLI] + ARGS + list(extra), cwd=cwd, env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stderr[-4000:]
+    # (progress for a long run: each CLI run is one build or load + 2 searches)
+    print(f"search.py {' '.join(extra)}: {time.time() - t0:.1f} s", flush=True)
     return r
 
 
