@@ -15,7 +15,9 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblmi_h5.so")
+# LMI_H5_LIB_NAME: the host-sanitizer build (csrc `make asan`: liblmi_h5_asan.so)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        os.environ.get("LMI_H5_LIB_NAME", "liblmi_h5.so"))
 F32, F16, F64, U32, I64 = 0, 1, 2, 3, 4
 EXPORTS = ("lmi_h5_dataset_info", "lmi_h5_read_f32", "lmi_h5_read_stored", "lmi_h5_write_results",
            "lmi_h5_write_f32", "lmi_h5_write_stored", "lmi_h5_last_error")
