@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 8
+#define LMI_ABI_VERSION 9
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -143,6 +143,25 @@ typedef struct lmi_index_desc {
      * and fallback distances from these rows, i.e. on the values sklearn sees
      * (utils.py:11, :19).  Results of the float32 mode do not depend on it. */
     const double* corpus64;
+    /* ABI 9: optional (NULL = none) device [n_rows][d_pad] float32: the rows
+     * as the caller gave them when they are float32 but NOT fp16-exact.
+     * `corpus` then holds each row L2-normalised and rounded to fp16 (dtype
+     * LMI_F16, inv_norm = 1/||that fp16 row||), and the search is exact in two
+     * steps (lmi_bucket_topk, _f64, _f64q, k <= LMI_MAX_K; queries as given,
+     * float32, rounded inside the call the same way):
+     *   1. the fp16 scan on the rounded rows and queries gives each (query,
+     *      probe)'s approximate k-th distance d~_k; every row's rounded
+     *      distance lies within eps_x of its exact one, eps_x =
+     *      lmi_split_eps(d) (1.0e-3 at d = 768), so the exact top-k lies
+     *      within d~_k + 2 eps_x;
+     *   2. a collect scan gathers every row under that bound, whose exact
+     *      distances are computed in float64 from these rows (or from
+     *      corpus64 when set, for the float64 mode) and the query, sorted by
+     *      (distance, position) -- rounded to float32 first for the float32
+     *      mode -- and the first k kept; a pair with more candidates than the
+     *      collect buffer holds is scanned whole in float64.
+     * Needs d_pad == 768 (the fp16 scan's width) and no phase flags. */
+    const float* corpus32;
 } lmi_index_desc;
 
 /* Host helper: fills chunk_first_out[C+1] from host bucket offsets and returns
@@ -229,8 +248,15 @@ int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, int32_t nq, 
                          const double* q64, int32_t ldq64, const int32_t* classes, int32_t R,
                          int32_t k, int32_t qmode, double eps, double* out_d, int32_t* out_pos,
                          int32_t* status, void* workspace, size_t ws_bytes, void* stream);
+/* ABI 9: the split mode's bound eps_x on |d~ - d| (lmi_index_desc.corpus32),
+ * for rows of d_pad elements; a host function (≈ 9.9e-4 at d_pad = 768).  In the
+ * split mode the eps argument of lmi_bucket_topk_f64* is ignored (this one
+ * is used), and so is the fp16 / fp32 class of qmode (the queries are
+ * normalised and rounded inside the call). */
+double lmi_split_eps(int32_t d_pad);
 /* Diagnostic (synchronises `stream`): how many (query, probe) pairs of the
- * last lmi_bucket_topk_f64 call on this workspace took the whole-bucket path. */
+ * last lmi_bucket_topk_f64 call on this workspace took the whole-bucket path
+ * (the split mode: also of lmi_bucket_topk, whose workspace has the same layout). */
 int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx, int32_t nq,
                               int32_t R, int32_t k, int32_t qmode, int32_t* count_out,
                               void* stream);

@@ -182,6 +182,42 @@ int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int3
                      const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
                      int32_t* out_pos, int32_t* out_row, int32_t ldo, int32_t* status,
                      void* workspace, size_t ws_bytes, hipStream_t s);
+// The split mode's exact step (lmi_refine.hip; ABI 9, idx->corpus32): per
+// grouped pair of the collect scan, the exact distances of its candidates,
+// sorted, the first k; overflowed pairs scanned whole.
+struct XArgs {
+    const float* rows32;   // [n_rows][d_pad] the caller's float32 rows
+    const double* rows64;  // [n_rows][d_pad] float64 rows (idx->corpus64) or null
+    int32_t d, d_pad;
+    const int32_t* gpos;
+    const int64_t* bucket_off;
+    int64_t n_rows;
+    const float* q;        // [nq][ldq] float32 queries
+    int32_t ldq;
+    const double* q64;     // float64 queries or null
+    int32_t ldq64;
+    const int32_t* classes;
+    int32_t nq, R, k;
+    const int32_t* pair_q;       // grouped pair -> pair id (the collect scan's plan)
+    const int32_t* pair_bucket;  // grouped pair -> bucket (-1: none)
+    const uint64_t* cand;        // [grouped pair][cap] (ord(d~) << 32 | row)
+    const uint32_t* ccount;
+    int32_t cap;
+    void* out_d;                 // [nq*R][k] float (out_f64 = 0) or double
+    int32_t out_f64;
+    int32_t* out_pos;
+    int32_t* failed;
+    int32_t* n_failed;
+    int32_t* status;
+};
+int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
+double split_eps(int d_pad);
+size_t x_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k);
+size_t x_nfailed_offset(const lmi_index_desc* idx, int nq, int R, int k);
+int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq, const double* q64,
+                  int32_t ldq64, const int32_t* classes, int32_t R, int32_t k, void* out_d, int out_f64,
+                  int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes, hipStream_t s);
+
 // n_words 32-bit words of `value` from p (4-byte aligned) on stream s, by a
 // kernel (lmi_merge.hip): workspace initialisation stays a kernel node when a
 // caller captures the launch sequence in a HIP graph (no memset nodes).

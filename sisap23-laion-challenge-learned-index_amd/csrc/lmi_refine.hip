@@ -28,6 +28,7 @@
 #include "lmi_common.hpp"
 
 #include <algorithm>
+#include <mutex>
 
 namespace lmi {
 namespace {
@@ -458,11 +459,302 @@ int num_cus_ref() {
 }  // namespace
 }  // namespace lmi
 
+// ---------------------------------------------------------------------------
+// The split mode (ABI 9, idx->corpus32): a float32 corpus that is not
+// fp16-exact.  lmi_scan.hip's bucket_topk_x runs the fp16 scan on the
+// normalised, rounded rows and queries and then a collect scan of every row
+// within d~_k + 2 eps_x of each pair (its candidates); here the candidates'
+// exact distances are computed in float64 from the caller's rows and query,
+// sorted, and the first k written (x_select_kernel); a pair whose candidates
+// overflowed the collect buffer is scanned whole (x_fallback_kernel).
+// ---------------------------------------------------------------------------
+namespace lmi {
+namespace {
+
+constexpr double kEps32 = 1.1920928955078125e-07;
+
+// 1 - <q^, y/|y|> of kB rows of float32 or float64 values at once (every row's
+// pieces loaded before any is used), in row_dist64's order; sklearn's zero
+// rule with the eps of the output dtype
+template <typename TC, int NPS>
+__device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t (&r)[kB], int d, int nps,
+                                     const double (&qh)[NPS][4], double zero_eps, double (&out)[kB]) {
+    const int lane = threadIdx.x & 63;
+    double v[kB][NPS][4];
+#pragma unroll
+    for (int b = 0; b < kB; ++b)
+#pragma unroll
+        for (int i = 0; i < NPS; ++i) {
+            if (r[b] >= 0 && i < nps) {
+                load_piece<TC>(base + (size_t)r[b] * d_pad, lane + 64 * i, d, v[b][i]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[b][i][j] = 0.0;
+            }
+        }
+    double dot[kB], ss[kB];
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        dot[b] = 0.0;
+        ss[b] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NPS; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                dot[b] = fma(qh[i][j], v[b][i][j], dot[b]);
+                ss[b] = fma(v[b][i][j], v[b][i][j], ss[b]);
+            }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            dot[b] += __shfl_xor(dot[b], off);
+            ss[b] += __shfl_xor(ss[b], off);
+        }
+#pragma unroll
+    for (int b = 0; b < kB; ++b) {
+        double n = sqrt(ss[b]);
+        if (n < 10.0 * zero_eps) n = 1.0;
+        out[b] = 1.0 - dot[b] / n;
+    }
+}
+
+// q^ with the zero rule of the output dtype (query_hat is float64's)
+template <typename TQ, int NP>
+__device__ inline void query_hat_x(const TQ* qrow, int d, int nps, double zero_eps, double (&qh)[NP][4]) {
+    const int lane = threadIdx.x & 63;
+    double ss = 0.0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 4 * (lane + 64 * i) + j;
+            const double v = (i < nps && e < d) ? (double)qrow[e] : 0.0;
+            qh[i][j] = v;
+            ss = fma(v, v, ss);
+        }
+    double n = sqrt(wave_sum_d(ss));
+    if (n < 10.0 * zero_eps) n = 1.0;
+#pragma unroll
+    for (int i = 0; i < NP; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) qh[i][j] = qh[i][j] / n;
+}
+
+template <bool OUT64>
+__device__ inline double out_value(double x) {
+    if constexpr (OUT64) return x;
+    else return (double)(float)x;  // the float32 mode orders its own (rounded) values
+}
+
+template <typename TC, typename TQ>
+__device__ inline const TC* x_rows(const XArgs& a) {
+    if constexpr (sizeof(TC) == 8) return a.rows64;
+    else return a.rows32;
+}
+template <typename TQ>
+__device__ inline const TQ* x_query(const XArgs& a, int64_t q) {
+    if constexpr (sizeof(TQ) == 8) return a.q64 + (size_t)q * a.ldq64;
+    else return a.q + (size_t)q * a.ldq;
+}
+
+template <bool OUT64>
+__device__ inline void x_store(const XArgs& a, size_t o, double v, int32_t pos) {
+    if constexpr (OUT64) reinterpret_cast<double*>(a.out_d)[o] = v;
+    else reinterpret_cast<float*>(a.out_d)[o] = (float)v;
+    a.out_pos[o] = pos;
+}
+
+constexpr int kXT = 256;  // x_select: 4 waves on one pair
+
+// One workgroup per grouped pair of the collect scan: the exact distance of
+// every candidate (a wave per kB rows), a bitonic sort of (distance, row) in
+// LDS -- rows ascend with global position inside a bucket shard, so this is
+// the reference's (distance, g.index) order -- and the first k written.
+template <typename TC, typename TQ, bool OUT64>
+__global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
+    extern __shared__ double x_lds[];
+    double* sd = x_lds;
+    int32_t* sr = reinterpret_cast<int32_t*>(x_lds + a.cap);
+    const int pp = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (a.pair_bucket[pp] < 0) return;
+    const int p = a.pair_q[pp];
+    const int64_t P = (int64_t)a.nq * a.R;
+    if (p < 0 || p >= P) return;
+    const uint32_t n = a.ccount[pp];
+    if (n > (uint32_t)a.cap) {  // the collect buffer overflowed: the whole shard
+        if (tid == 0) a.failed[atomicAdd(a.n_failed, 1)] = p;
+        return;
+    }
+    const double zero_eps = OUT64 ? kEps64 : kEps32;
+    const int nps = (a.d + 255) / 256;
+    double qh[3][4];
+    query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
+    const uint64_t* src = a.cand + (size_t)pp * a.cap;
+    for (uint32_t j0 = (uint32_t)w * kB; j0 < n; j0 += (kXT / 64) * kB) {
+        int32_t r[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int64_t x = j0 + b < n ? (int64_t)(uint32_t)src[j0 + b] : -1;
+            r[b] = (x < 0 || x >= a.n_rows) ? -1 : (int32_t)x;
+            if (j0 + b < n && r[b] < 0 && lane == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
+        }
+        double dv[kB];
+        rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
+        if (lane == 0) {
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+                if (j0 + b < n) {
+                    sd[j0 + b] = r[b] >= 0 ? out_value<OUT64>(dv[b]) : __builtin_inf();
+                    sr[j0 + b] = r[b] >= 0 ? r[b] : INT32_MAX;
+                }
+        }
+    }
+    uint32_t m = 1;
+    while (m < n) m <<= 1;
+    for (uint32_t i = n + tid; i < m; i += kXT) {
+        sd[i] = __builtin_inf();
+        sr[i] = INT32_MAX;
+    }
+    __syncthreads();
+    for (uint32_t k2 = 2; k2 <= m; k2 <<= 1) {
+        for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = tid; i < m; i += kXT) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const double xd = sd[i], yd = sd[l];
+                    const int32_t xr = sr[i], yr = sr[l];
+                    const bool up = (i & k2) == 0;
+                    const bool gt = xd > yd || (xd == yd && xr > yr);
+                    if (gt == up) {
+                        sd[i] = yd;
+                        sd[l] = xd;
+                        sr[i] = yr;
+                        sr[l] = xr;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const size_t o = (size_t)p * a.k;
+    for (int i = tid; i < a.k; i += kXT) {
+        const bool has = i < (int)n && sr[i] != INT32_MAX;
+        x_store<OUT64>(a, o + i, has ? sd[i] : __builtin_inf(), has ? a.gpos[sr[i]] : -1);
+    }
+}
+
+// One workgroup per overflowed pair: the exact distance of every row of its
+// bucket shard (a wave per kB rows), lane 0 of each wave keeps the wave's
+// top-k by (distance, row) in LDS, thread 0 merges the waves' lists.
+template <typename TC, typename TQ, bool OUT64>
+__global__ __launch_bounds__(kFbT) void x_fallback_kernel(XArgs a) {
+    __shared__ double sd[kFbT / 64][LMI_MAX_K];
+    __shared__ int32_t sr[kFbT / 64][LMI_MAX_K];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nf = *a.n_failed;
+    const int k = a.k;
+    const int nps = (a.d + 255) / 256;
+    const double zero_eps = OUT64 ? kEps64 : kEps32;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        const int64_t p = a.failed[f];
+        const int c = a.classes[p];  // classes [nq][R]: pair p = q*R + r
+        const int64_t b0 = a.bucket_off[c], b1 = a.bucket_off[c + 1];
+        double qh[3][4];
+        query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
+        double* L = sd[w];
+        int32_t* G = sr[w];
+        if (lane == 0)
+            for (int i = 0; i < k; ++i) {
+                L[i] = __builtin_inf();
+                G[i] = INT32_MAX;
+            }
+        for (int64_t r0 = b0 + (int64_t)w * kB; r0 < b1; r0 += (int64_t)(kFbT / 64) * kB) {
+            int32_t r[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) r[b] = r0 + b < b1 ? (int32_t)(r0 + b) : -1;
+            double dv[kB];
+            rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
+            if (lane == 0) {
+#pragma unroll
+                for (int b = 0; b < kB; ++b) {
+                    if (r[b] < 0) break;
+                    const double x = out_value<OUT64>(dv[b]);
+                    if (!lt_dp(x, r[b], L[k - 1], G[k - 1])) continue;
+                    int i = k - 1;
+                    while (i > 0 && lt_dp(x, r[b], L[i - 1], G[i - 1])) {
+                        L[i] = L[i - 1];
+                        G[i] = G[i - 1];
+                        --i;
+                    }
+                    L[i] = x;
+                    G[i] = r[b];
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int head[kFbT / 64] = {};
+            const size_t o = (size_t)p * k;
+            for (int j = 0; j < k; ++j) {
+                int best = -1;
+                for (int v = 0; v < kFbT / 64; ++v) {
+                    if (head[v] >= k) continue;
+                    if (best < 0 || lt_dp(sd[v][head[v]], sr[v][head[v]], sd[best][head[best]],
+                                          sr[best][head[best]]))
+                        best = v;
+                }
+                const double x = sd[best][head[best]];
+                const int32_t rr = sr[best][head[best]];
+                ++head[best];
+                const bool empty = rr == INT32_MAX;
+                x_store<OUT64>(a, o + j, empty ? __builtin_inf() : x, empty ? -1 : a.gpos[rr]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <typename TC, typename TQ, bool OUT64>
+int launch_x3(const XArgs& a, int64_t P, hipStream_t s) {
+    const size_t lds = (size_t)a.cap * (sizeof(double) + sizeof(int32_t));
+    static std::once_flag once;
+    static hipError_t attr_err = hipSuccess;
+    std::call_once(once, [] {
+        attr_err = hipFuncSetAttribute((const void*)x_select_kernel<TC, TQ, OUT64>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    });
+    LMI_HIP_TRY(attr_err);
+    hipLaunchKernelGGL((x_select_kernel<TC, TQ, OUT64>), dim3((unsigned)P), dim3(kXT), lds, s, a);
+    LMI_LAUNCH_CHECK("x_select_kernel");
+    const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref()));
+    hipLaunchKernelGGL((x_fallback_kernel<TC, TQ, OUT64>), dim3(fg), dim3(kFbT), 0, s, a);
+    LMI_LAUNCH_CHECK("x_fallback_kernel");
+    return LMI_OK;
+}
+}  // namespace
+
+int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s) {
+    if (a.d > 3 * 256) {
+        set_error("split mode: d=%d > 768", a.d);
+        return LMI_E_UNSUPPORTED;
+    }
+    if (a.out_f64) {
+        if (a.rows64) return a.q64 ? launch_x3<double, double, true>(a, P, s) : launch_x3<double, float, true>(a, P, s);
+        return a.q64 ? launch_x3<float, double, true>(a, P, s) : launch_x3<float, float, true>(a, P, s);
+    }
+    return launch_x3<float, float, false>(a, P, s);
+}
+}  // namespace lmi
+
 extern "C" size_t lmi_scan_f64_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R,
                                                int32_t k, int32_t qmode) {
     qmode &= ~LMI_Q_SEED_ROUND0;
     lmi::take_phases(qmode);
     if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_F64) return 0;
+    if (idx->corpus32) return k <= LMI_MAX_K ? lmi::x_ws_bytes(idx, nq, R, k) : 0;
     return lmi::refine_ws(idx, nq, R, k, qmode).total;
 }
 
@@ -514,6 +806,14 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     if (nq == 0) return LMI_OK;
     LMI_CHECK_ARG(q && classes && out_d && out_pos && status && workspace, "null pointer");
     LMI_CHECK_ARG(q64 == nullptr || ldq64 >= idx->d, "ldq64 < d");
+    if (idx->corpus32) {
+        if (phases != kPhaseAll) {
+            set_error("phase flags are not supported in the split mode (corpus32)");
+            return LMI_E_UNSUPPORTED;
+        }
+        return bucket_topk_x(idx, q, nq, ldq, q64, ldq64, classes, R, k, out_d, 1, out_pos, status,
+                             workspace, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+    }
     const RefineWs w = refine_ws(idx, nq, R, k, qmode);
     if (ws_bytes < w.total) {
         set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
@@ -584,8 +884,8 @@ extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_
     LMI_CHECK_ARG(workspace && idx && count_out, "null pointer");
     qmode &= ~LMI_Q_SEED_ROUND0;
     take_phases(qmode);
-    const RefineWs w = refine_ws(idx, nq, R, k, qmode);
-    LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + w.nfailed, 4,
+    const size_t at = idx->corpus32 ? x_nfailed_offset(idx, nq, R, k) : refine_ws(idx, nq, R, k, qmode).nfailed;
+    LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + at, 4,
                                hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
     LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
     return LMI_OK;

@@ -34,6 +34,7 @@
 #include "lmi_scan_internal.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <mutex>
 #include <utility>
@@ -915,6 +916,66 @@ __global__ __launch_bounds__(256) void take_k_kernel(const float* __restrict__ d
 }
 
 // ---------------------------------------------------------------------------
+// the split mode (ABI 9, idx->corpus32; bucket_topk_x below)
+// ---------------------------------------------------------------------------
+// One wave per query: q^ = q / |q| (float64 norm, sklearn's zero rule) rounded
+// to fp16, written as float32 rows of d_pad (zero-padded) -- the fp16-exact
+// queries the fp16 scan takes; float64 queries (q64) are rounded the same way.
+__global__ __launch_bounds__(kThreads) void x_round_queries_kernel(const float* __restrict__ q, int32_t ldq,
+                                                                   const double* __restrict__ q64,
+                                                                   int32_t ldq64, int32_t nq, int32_t d,
+                                                                   int32_t d_pad, float* __restrict__ out) {
+    const int row = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= nq) return;
+    double ss = 0.0;
+    for (int e = lane; e < d; e += 64) {
+        const double v = q64 ? q64[(size_t)row * ldq64 + e] : (double)q[(size_t)row * ldq + e];
+        ss = fma(v, v, ss);
+    }
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+    double n = sqrt(ss);
+    if (n < 10.0 * 1.1920928955078125e-07) n = 1.0;
+    for (int e = lane; e < d_pad; e += 64) {
+        float h = 0.0f;
+        if (e < d) {
+            const double v = q64 ? q64[(size_t)row * ldq64 + e] : (double)q[(size_t)row * ldq + e];
+            h = (float)(_Float16)(float)(v / n);
+        }
+        out[(size_t)row * d_pad + e] = h;
+    }
+}
+
+// (+inf, -1) over every output entry (pairs whose class is out of range keep it)
+__global__ __launch_bounds__(256) void x_prefill_kernel(int64_t n, void* __restrict__ out_d, int32_t out_f64,
+                                                        int32_t* __restrict__ out_pos) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n) return;
+    if (out_f64) reinterpret_cast<double*>(out_d)[t] = __builtin_inf();
+    else reinterpret_cast<float*>(out_d)[t] = __builtin_inff();
+    out_pos[t] = -1;
+}
+
+// Per pair (by id): the collect bound d~_k + 2 eps as a distance ordinal,
+// rounded up (every row whose rounded distance is at most the real sum
+// passes); a list with fewer than k entries (a bucket shard of fewer rows)
+// collects its whole shard.
+__global__ __launch_bounds__(256) void x_bound_kernel(int64_t P, int32_t k, const float* __restrict__ ld,
+                                                      double two_eps, uint32_t* __restrict__ bound_ord) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const float dk = ld[(size_t)p * k + k - 1];
+    if (!(dk < __builtin_inff())) {
+        bound_ord[p] = 0xffffffffu;
+        return;
+    }
+    const double b = (double)dk + two_eps;
+    const float f = (float)b;
+    // (the ordinal of the next float up when the float rounded the sum down)
+    bound_ord[p] = f2ord(f) + ((double)f < b ? 1u : 0u);
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 struct WsLayout {
@@ -1100,6 +1161,7 @@ extern "C" size_t lmi_scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq
     qmode &= ~LMI_Q_SEED_ROUND0;
     take_phases(qmode);
     if (!idx || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_PASSES) return 0;
+    if (idx->corpus32) return k <= LMI_MAX_K ? x_ws_bytes(idx, nq, R, k) : 0;
     if (k <= LMI_MAX_K) return scan_workspace_bytes(idx, nq, R, k, qmode);
     int kp;
     const int ldo = passes_of(idx, qmode, k, &kp) * kp;
@@ -1120,6 +1182,14 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
     qmode &= ~LMI_Q_SEED_ROUND0;
     const int phases = take_phases(qmode);
+    if (idx && idx->corpus32) {
+        if (phases != kPhaseAll) {
+            set_error("phase flags are not supported in the split mode (corpus32)");
+            return LMI_E_UNSUPPORTED;
+        }
+        return bucket_topk_x(idx, q, nq, ldq, nullptr, 0, classes, R, k, out_d, 0, out_pos, status, workspace,
+                             ws_bytes, s);
+    }
     if (k <= LMI_MAX_K)
         return bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
                                 status, workspace, ws_bytes, s, nullptr, 0, true, seed, 0.0f, phases);
@@ -1413,6 +1483,150 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     return LMI_OK;
 }
 
+namespace lmi {
+// |d~ - d| for every (query, row) of the split mode, d~ the fp16 scan's
+// distance on the normalised, fp16-rounded vectors and d the exact one:
+// rounding a unit vector to fp16 moves it by delta <= 2^-11 (relative, normal
+// range; + 2^-22 for the float32 step before it) + sqrt(d) 2^-25 (absolute,
+// the subnormal range), i.e. by an angle <= asin(delta); the angle between
+// query and row moves by at most the two angles, and a cosine by at most the
+// angle.  Plus the fp16 scan's own arithmetic on the rounded vectors
+// (refine_eps of li/index.py, the fp16 path: gamma(2 (d_pad/16 + 16)) for the
+// dot, the two norms, the scale and the final fma) and 2^-24 for rounding the
+// exact value to float32 (ties of the rounded values then order by position).
+double split_eps(int d_pad) {
+    const double u = std::ldexp(1.0, -24);
+    auto gamma = [&](double n) { return n * u / (1.0 - n * u); };
+    const double delta = std::ldexp(1.0, -11) + std::ldexp(1.0, -22) + std::sqrt((double)d_pad) * std::ldexp(1.0, -25);
+    const double h = 2.0 * (d_pad / 16 + 16), hq = 4.0 * ((d_pad + 255) / 256) + 6.0;
+    const double scan = gamma(h) + gamma(2 * hq) / 2 + 4 * u + u + 2 * u + 2 * u;
+    return 2.0 * std::asin(delta) + scan + u;
+}
+
+namespace {
+struct XWs {
+    size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, region, region_bytes, total;
+    int32_t cap;
+};
+
+XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
+    XWs w{};
+    const size_t P = (size_t)nq * R;
+    // collect slots per pair: 2048 (the rows within 2 eps of the k-th, ~20 on
+    // the clip768-like mixture), fewer for huge batches (<= 2 GiB of slots)
+    int cap = 2048;
+    while (cap > 256 && P * (size_t)cap * 8 > (size_t(2) << 30)) cap >>= 1;
+    w.cap = cap;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = off;
+        off = align_up(off + bytes, 256);
+        return at;
+    };
+    w.qr = take((size_t)nq * idx->d_pad * 4);
+    w.ld = take(P * k * 4);
+    w.lpos = take(P * k * 4);
+    w.bound = take(P * 4);
+    w.ccount = take(P * 4);
+    w.cand = take(P * (size_t)cap * 8);
+    w.failed = take(P * 4);
+    w.nfailed = take(256);
+    w.region_bytes = std::max(ws_layout(idx, nq, R, k, LMI_Q_F16).total, ws_layout(idx, nq, R, 10, LMI_Q_F16).total);
+    w.region = take(w.region_bytes);
+    w.total = off;
+    return w;
+}
+}  // namespace
+
+size_t x_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k) { return x_ws(idx, nq, R, k).total; }
+size_t x_nfailed_offset(const lmi_index_desc* idx, int nq, int R, int k) { return x_ws(idx, nq, R, k).nfailed; }
+
+// The split mode: see lmi_index_desc.corpus32 (include/lmi_hip.h).  out_d is
+// float (out_f64 = 0) or double [nq*R][k]; qmode is ignored (the queries are
+// rounded here whatever their class).
+int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq, const double* q64,
+                  int32_t ldq64, const int32_t* classes, int32_t R, int32_t k, void* out_d, int out_f64,
+                  int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes, hipStream_t s) {
+    LMI_CHECK_ARG(idx != nullptr, "null index");
+    LMI_CHECK_ARG(idx->corpus32 != nullptr && idx->dtype == LMI_F16 && idx->d_pad == v2::D,
+                  "split mode needs corpus32, an fp16 scan corpus and d_pad %d", v2::D);
+    LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K, "split mode: k=%d outside [1, %d]", k, LMI_MAX_K);
+    LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
+    if (nq == 0) return LMI_OK;
+    LMI_CHECK_ARG((q || q64) && classes && out_d && out_pos && status && workspace, "null pointer");
+    LMI_CHECK_ARG(q64 ? ldq64 >= idx->d : ldq >= idx->d, "ldq < d");
+    const XWs w = x_ws(idx, nq, R, k);
+    if (ws_bytes < w.total) {
+        set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
+        return LMI_E_WORKSPACE;
+    }
+    const int P = nq * R;
+    auto* ws = reinterpret_cast<unsigned char*>(workspace);
+    float* qr = (float*)(ws + w.qr);
+    float* ld = (float*)(ws + w.ld);
+    int32_t* lpos = (int32_t*)(ws + w.lpos);
+    auto* bound = (uint32_t*)(ws + w.bound);
+    auto* ccount = (uint32_t*)(ws + w.ccount);
+    auto* cand = (uint64_t*)(ws + w.cand);
+    unsigned char* region = ws + w.region;
+    hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)), dim3(kThreads),
+                       0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
+    LMI_LAUNCH_CHECK("x_round_queries_kernel");
+    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
+    // 1. the fp16 scan on the rounded vectors: every pair's approximate k-th
+    int rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
+                              region, w.region_bytes, s);
+    if (rc != LMI_OK) return rc;
+    hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld,
+                       2.0 * split_eps(idx->d_pad), bound);
+    LMI_LAUNCH_CHECK("x_bound_kernel");
+    // 2. every row under the bound (the collect scan, as the wide path's)
+    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
+    rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status, region,
+                          w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhasePlan | kPhaseScan, &m2);
+    if (rc != LMI_OK) return rc;
+    // 3. the candidates' exact distances, sorted; overflowed pairs whole
+    const WsLayout l = ws_layout(idx, nq, R, 10, LMI_Q_F16);
+    XArgs a{};
+    a.rows32 = idx->corpus32;
+    a.rows64 = out_f64 ? idx->corpus64 : nullptr;
+    a.d = idx->d;
+    a.d_pad = idx->d_pad;
+    a.gpos = idx->gpos;
+    a.bucket_off = idx->bucket_off;
+    a.n_rows = idx->n_rows;
+    a.q = q;
+    a.ldq = ldq;
+    a.q64 = out_f64 ? q64 : nullptr;
+    a.ldq64 = ldq64;
+    if (!a.q64 && !q) {
+        set_error("split mode: float32 output needs the float32 queries");
+        return LMI_E_INVALID;
+    }
+    a.classes = classes;
+    a.nq = nq;
+    a.R = R;
+    a.k = k;
+    a.pair_q = (const int32_t*)(region + l.pair_q);
+    a.pair_bucket = (const int32_t*)(region + l.pair_bucket);
+    a.cand = cand;
+    a.ccount = ccount;
+    a.cap = w.cap;
+    a.out_d = out_d;
+    a.out_f64 = out_f64;
+    a.out_pos = out_pos;
+    a.failed = (int32_t*)(ws + w.failed);
+    a.n_failed = (int32_t*)(ws + w.nfailed);
+    a.status = status;
+    // (pairs whose class is out of range keep the prefill of step 1's prep:
+    // the outputs are prefilled here, by pair id, in step 3's own buffers)
+    hipLaunchKernelGGL(x_prefill_kernel, dim3((unsigned)(((int64_t)P * k + 255) / 256)), dim3(256), 0, s,
+                       (int64_t)P * k, out_d, out_f64, out_pos);
+    LMI_LAUNCH_CHECK("x_prefill_kernel");
+    return launch_x_refine(a, P, s);
+}
+}  // namespace lmi
+
 #ifdef LMI_DIAG
 // Diagnostic (the `make ablation` library only): lower every pair's global
 // bound before the SCAN phase, e.g. to the final k-th distance of the
@@ -1679,6 +1893,8 @@ int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int3
 }
 }  // namespace lmi
 
+
+extern "C" double lmi_split_eps(int32_t d_pad) { return d_pad > 0 ? lmi::split_eps(d_pad) : 0.0; }
 
 extern "C" int lmi_timing_enable(int32_t on) {
     lmi::Timing& t = lmi::timing();

@@ -58,6 +58,7 @@ EXPORTS = (
     "lmi_bucket_topk_f64",
     "lmi_bucket_topk_f64q",
     "lmi_refine_fallback_count",
+    "lmi_split_eps",
     "lmi_merge_topk_f64",
     "lmi_packed_rank_words",
     "lmi_merge_topk_packed",
@@ -99,7 +100,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 
 class IndexDesc(C.Structure):
@@ -119,6 +120,7 @@ class IndexDesc(C.Structure):
         ("max_chunks", C.c_int32),
         ("chunk_centroid", C.c_void_p),  # ABI 2
         ("corpus64", C.c_void_p),        # ABI 6
+        ("corpus32", C.c_void_p),        # ABI 9
     ]
 
 
@@ -138,6 +140,7 @@ _SIGNATURES = {
                                       C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_bucket_topk_f64q": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _P, _I32,
                                        _I32, _I32, C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
+    "lmi_split_eps": (C.c_double, [_I32]),
     "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,
                                             _P]),
     "lmi_merge_topk_f64": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),

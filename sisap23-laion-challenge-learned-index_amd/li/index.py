@@ -34,6 +34,7 @@ from . import _lib
 from ._lib import check, ptr
 
 DEFAULT_CHUNK_ROWS = 8192
+SPLIT_D_PAD = 768  # the split mode's (storage "f32x") row width: the fp16 scan's
 
 
 def default_chunk_rows(world: int) -> int:
@@ -191,9 +192,18 @@ class RowSource:
 
 
 class DeviceIndex:
-    """One shard of the bucket-sorted search corpus, resident in HBM."""
+    """One shard of the bucket-sorted search corpus, resident in HBM.
+
+    storage: "f16" (every value fp16-exact: the fp16 MFMA scan is exact),
+    "f32x" (float32 values that are not: the split mode of ABI 9 -- the fp16
+    scan runs on each row L2-normalised and rounded to fp16, `corpus`, and the
+    rows within its rounding bound of every pair's k-th distance are re-scored
+    exactly from the float32 rows, `corpus32`; d_pad 768), or "f32" (the
+    general exact-fp32 MFMA scan).  "auto" picks the first that applies."""
 
     corpus64 = None  # float64 rows (float64 input that float32 rounding changes)
+    corpus32 = None  # float32 rows of the split mode (storage "f32x")
+    inv_norm32 = None  # 1/||y|| of corpus32 (the general scan's, k > 16 in f32x)
 
     def __init__(self, data, labels, n_buckets: int, *, ids=None, device=None,
                  storage: str = "auto", chunk_rows: int = DEFAULT_CHUNK_ROWS,
@@ -274,19 +284,37 @@ class DeviceIndex:
                     0, rows[a:a + step].to(src64.device)).to(self.device)
         if storage == "auto":
             storage = "f16" if src.dtype == torch.float16 or all(
-                fp16_exact(src[a:a + step].to(self.device)) for a in range(0, n, step)) else "f32"
-        if storage not in ("f16", "f32"):
-            raise ValueError("storage must be 'auto', 'f16' or 'f32'")
+                fp16_exact(src[a:a + step].to(self.device)) for a in range(0, n, step)) else \
+                ("f32x" if self.d_pad == SPLIT_D_PAD else "f32")
+        if storage not in ("f16", "f32", "f32x"):
+            raise ValueError("storage must be 'auto', 'f16', 'f32' or 'f32x'")
+        if storage == "f32x" and self.d_pad != SPLIT_D_PAD:
+            raise ValueError(f"storage='f32x' needs d_pad {SPLIT_D_PAD}")
         self.storage = storage
-        tdt = torch.float16 if storage == "f16" else torch.float32
+        tdt = torch.float32 if storage == "f32" else torch.float16
         n_rows = int(gpos.size)
         self.corpus = torch.zeros((n_rows, self.d_pad), dtype=tdt, device=self.device)
         self.inv_norm = torch.empty((n_rows,), dtype=torch.float32, device=self.device)
+        if storage == "f32x":
+            self.corpus32 = torch.zeros((n_rows, self.d_pad), dtype=torch.float32, device=self.device)
+            self.inv_norm32 = torch.empty((n_rows,), dtype=torch.float32, device=self.device)
         for a in range(0, n_rows, step):
             blk = src.index_select(0, rows[a:a + step].to(src.device)).to(self.device)
             f = blk.float()
             if storage == "f16" and blk.dtype != torch.float16 and not fp16_exact(f):
                 raise ValueError("storage='f16' needs fp16-representable data (exact products)")
+            if storage == "f32x":
+                # the rows as given, and each row / its float64 norm (sklearn's
+                # zero rule) rounded to fp16: the split mode's scan rows
+                self.corpus32[a:a + step, : self.d] = f
+                self.inv_norm32[a:a + step] = _inv_norm(f)
+                nrm = torch.sqrt((f.double() * f.double()).sum(dim=1))
+                nrm = torch.where(nrm < 10 * float(np.finfo(np.float32).eps), torch.ones_like(nrm), nrm)
+                h = (f.double() / nrm[:, None]).float().half()
+                self.corpus[a:a + step, : self.d] = h
+                self.inv_norm[a:a + step] = _inv_norm(h)
+                del blk, f, h, nrm
+                continue
             self.corpus[a:a + step, : self.d] = blk.to(tdt)
             self.inv_norm[a:a + step] = _inv_norm(blk.to(tdt))
             del blk, f
@@ -372,9 +400,20 @@ class DeviceIndex:
     def desc(self) -> _lib.IndexDesc:
         return self._desc.desc
 
+    def desc_for(self, k: int) -> _lib.IndexDesc:
+        """The descriptor a call with k entries per list takes: the split mode
+        (storage "f32x") holds k <= LMI_MAX_K; wider lists scan the float32
+        rows with the general exact-fp32 kernel (a second descriptor over
+        corpus32)."""
+        if self.storage != "f32x" or k <= _lib.LMI_MAX_K:
+            return self.desc
+        if getattr(self, "_desc32", None) is None:
+            self._desc32 = IndexDescHolder(self, general32=True)
+        return self._desc32.desc
+
     def workspace(self, nq: int, R: int, k: int, qmode: int) -> torch.Tensor:
         lib = _lib.load()
-        need = lib.lmi_scan_workspace_bytes(C.byref(self.desc), nq, R, k, qmode)
+        need = lib.lmi_scan_workspace_bytes(C.byref(self.desc_for(k)), nq, R, k, qmode)
         ws = self._ws.get("buf")
         if ws is None or ws.numel() < need:
             ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
@@ -383,14 +422,14 @@ class DeviceIndex:
 
 
 class IndexDescHolder:
-    def __init__(self, ix: DeviceIndex):
+    def __init__(self, ix: DeviceIndex, general32: bool = False):
         d = _lib.IndexDesc()
-        d.corpus = ptr(ix.corpus)
-        d.dtype = _lib.LMI_F16 if ix.storage == "f16" else _lib.LMI_F32
+        d.corpus = ptr(ix.corpus32 if general32 else ix.corpus)
+        d.dtype = _lib.LMI_F32 if (general32 or ix.storage == "f32") else _lib.LMI_F16
         d.d = ix.d
         d.d_pad = ix.d_pad
         d.n_rows = ix.n_rows
-        d.inv_norm = ptr(ix.inv_norm)
+        d.inv_norm = ptr(ix.inv_norm32 if general32 else ix.inv_norm)
         d.gpos = ptr(ix.gpos)
         d.n_buckets = ix.n_buckets
         d.bucket_off = ptr(ix.bucket_off_local)
@@ -400,6 +439,7 @@ class IndexDescHolder:
         d.max_chunks = ix.max_chunks
         d.chunk_centroid = ptr(ix.chunk_centroid) if ix.chunk_centroid is not None else None
         d.corpus64 = ptr(ix.corpus64) if ix.corpus64 is not None else None
+        d.corpus32 = ptr(ix.corpus32) if (ix.corpus32 is not None and not general32) else None
         self.desc = d
 
 
@@ -511,6 +551,7 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
         raise ValueError("query shape does not match the index")
     if qmode is None:
         qmode = _lib.LMI_Q_F16 if index.storage == "f16" else _lib.LMI_Q_F32
+    desc = index.desc_for(k)
     if out is None:
         out_d = torch.empty((nq, R, k), dtype=torch.float32, device=index.device)
         out_pos = torch.empty((nq, R, k), dtype=torch.int32, device=index.device)
@@ -520,10 +561,12 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
     if ws is None:
         ws = index.workspace(nq, R, k, qmode)
     else:
-        _workspace(ws, lib.lmi_scan_workspace_bytes(C.byref(index.desc), nq, R, k, qmode), "scan")
+        _workspace(ws, lib.lmi_scan_workspace_bytes(C.byref(desc), nq, R, k, qmode), "scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
+    if index.storage == "f32x":
+        seed_round0 = False  # (the split mode scans every pair whole)
     flags = (_lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0) | phases
-    check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(index.desc), ptr(q), nq, q.stride(0),
+    check("lmi_bucket_topk", lib.lmi_bucket_topk(C.byref(desc), ptr(q), nq, q.stride(0),
                                                  ptr(classes), R, k, qmode | flags, ptr(out_d),
                                                  ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
     return out_d, out_pos, status
@@ -563,7 +606,8 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
         status = torch.zeros((1,), dtype=torch.int32, device=index.device)
     else:
         out_d, out_pos, status = out
-    need = lib.lmi_scan_f64_workspace_bytes(C.byref(index.desc), nq, R, k, qmode)
+    desc = index.desc_for(k)
+    need = lib.lmi_scan_f64_workspace_bytes(C.byref(desc), nq, R, k, qmode)
     if ws is None:
         ws = index._ws.get("f64")
         if ws is None or ws.numel() < need:
@@ -572,16 +616,18 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     else:
         _workspace(ws, need, "float64 scan")
     s = stream if stream is not None else _lib.stream_handle(index.device)
+    if index.storage == "f32x":
+        seed_round0 = False  # (the split mode scans every pair whole)
     flags = (_lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0) | phases
     check("lmi_bucket_topk_f64q", lib.lmi_bucket_topk_f64q(
-        C.byref(index.desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
+        C.byref(desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
         ptr(classes), R, k, qmode | flags, float(eps), ptr(out_d), ptr(out_pos), ptr(status),
         ptr(ws), ws.numel(), s))
     if not fallback_count:
         return out_d, out_pos, status
     n = C.c_int32(0)
     check("lmi_refine_fallback_count", lib.lmi_refine_fallback_count(
-        ptr(ws), C.byref(index.desc), nq, R, k, qmode, C.byref(n), s))
+        ptr(ws), C.byref(desc), nq, R, k, qmode, C.byref(n), s))
     return out_d, out_pos, status, int(n.value)
 
 

@@ -1,0 +1,172 @@
+"""The split mode (ABI 9, lmi_index_desc.corpus32): float32 corpora that are
+not fp16-exact.  The fp16 scan runs on the normalised fp16 rounding of rows
+and queries, every row within d~_k + 2 eps_x is collected, and the
+candidates are re-scored exactly (float64, rounded to float32 for the float32
+arithmetic).  Checked against the oracle's lists (the reference's float32 /
+float64 arithmetic restated, pinned by tests/golden/reference_outputs_r5.npz)
+and the reference's own outputs through the drop-in (test_gpu_golden_r5.py's
+cases live here too)."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import lmi_oracle as O
+import workloads
+from li import _lib
+from li.index import DeviceIndex, DeviceRouter, Searcher, bucket_topk, bucket_topk_f64
+from test_oracle_golden_r5 import BASES, CASES, G5, SINGLES, check, inputs_r5
+
+pytestmark = pytest.mark.gpu
+T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+
+
+def _x(mode, seed, n=6000, nq=200, C=16):
+    w = workloads.clustered(n=n, nq=nq, C=C, seed=seed, label_mode=mode)
+    x32, q32 = workloads.float32_inputs(w, seed)
+    return w, x32, q32
+
+
+def test_split_eps_bound():
+    lib = _lib.load()
+    eps = lib.lmi_split_eps(768)
+    # 2 asin(2^-11 + 2^-22 + sqrt(768) 2^-25) + the fp16 scan's arithmetic
+    assert 9.7e-4 < eps < 1.0e-3
+
+
+@pytest.mark.parametrize("mode,seed", [("near", 601), ("dup", 602), ("skewed", 603)])
+@pytest.mark.parametrize("k", [1, 10, 16])
+def test_split_lists_match_oracle(mode, seed, k):
+    w, x, q = _x(mode, seed)
+    C, R = w["C"], 4
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
+    assert ix.storage == "f32x" and ix.corpus32 is not None
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    cls = T(classes.astype(np.int32))
+    d, p, st = bucket_topk(ix, T(q), cls, k)
+    assert int(st.item()) == 0
+    ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, R, k, C)
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-5, tie=1e-6) == 0
+    # the float64 arithmetic (float64 queries: the reference computes in float64)
+    q64 = q.astype(np.float64)
+    d64, p64, st64, nfb = bucket_topk_f64(ix, T(q64), cls, k, fallback_count=True)
+    assert int(st64.item()) == 0 and nfb == 0
+    ref_d64, ref_p64 = O.bucket_lists(w["labels"], x, q64, classes, R, k, C)
+    assert O.compare_lists(ref_d64, ref_p64, d64.cpu().numpy(), p64.cpu().numpy(), atol=1e-12,
+                           tie=1e-12) == 0
+
+
+def test_split_overflow_takes_the_whole_shard():
+    """A bucket of 3000 copies of one vector (relative noise 1e-4: one fp16
+    value after normalising and rounding, distinct exact distances): every
+    pair probing it collects more rows than the buffer holds (2048) and is
+    scanned whole in float64."""
+    w, x, q = _x("skewed", 611, n=8000, nq=64)
+    rng = np.random.default_rng(5)
+    big = int(np.bincount(w["labels"]).argmax())
+    rows = np.nonzero(w["labels"] == big)[0][:3000]
+    assert rows.size == 3000
+    x = x.copy()
+    x[rows] = (x[rows[0]].astype(np.float64) * (1 + 1e-4 * rng.standard_normal((3000, x.shape[1])))
+               ).astype(np.float32)
+    q = q.copy()
+    q[:16] = x[rows[0]] * np.float32(1.0001)
+    C = w["C"]
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
+    classes = np.full((q.shape[0], 1), big, np.int64)
+    cls = T(classes.astype(np.int32))
+    d, p, st = bucket_topk(ix, T(q), cls, 10)
+    ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, 1, 10, C)
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-5, tie=1e-6) == 0
+    d64, p64, st64, nfb = bucket_topk_f64(ix, T(q.astype(np.float64)), cls, 10, fallback_count=True)
+    assert nfb > 0  # the whole-shard path ran
+    ref_d64, ref_p64 = O.bucket_lists(w["labels"], x, q.astype(np.float64), classes, 1, 10, C)
+    assert O.compare_lists(ref_d64, ref_p64, d64.cpu().numpy(), p64.cpu().numpy(), atol=1e-12,
+                           tie=1e-12) == 0
+
+
+def test_split_search_and_striped_shards_match_oracle():
+    """Searcher.search end to end (router, lists, device replay) in both
+    arithmetics, and the lists of a 3-way striped index merged = one GPU."""
+    from li.index import merge_topk
+    w, x, q = _x("near", 621)
+    C = w["C"]
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
+    s = Searcher(ix, DeviceRouter(w["layers"], device="cuda"))
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))
+    ids = np.arange(1, x.shape[0] + 1)
+    for dist_, qq in (("f32", q), ("f64", q.astype(np.float64))):
+        d, a = s.search(T(w["qn"]), T(qq), 4, k=10, dist=dist_)
+        ref_d, ref_a = O.search_direct(w["labels"], ids, x, qq, classes, n_buckets=4, k=10,
+                                       use_threshold=True)
+        tol = dict(atol=1e-5, tie=1e-6) if dist_ == "f32" else dict(atol=1e-12, tie=1e-12)
+        assert O.compare_lists(ref_d, ref_a, d, a, **tol) == 0
+    cls = T(classes[:, :4].astype(np.int32))
+    d1, p1, _ = bucket_topk(ix, T(q), cls, 10)
+    parts = [bucket_topk(DeviceIndex(x, w["labels"], C, chunk_rows=256, device="cuda", rank=g, world=3),
+                         T(q), cls, 10) for g in range(3)]
+    md, mp = merge_topk(torch.stack([p_[0] for p_ in parts]), torch.stack([p_[1] for p_ in parts]), 10)
+    assert torch.equal(md, d1) and torch.equal(mp, p1)
+
+
+def test_split_wide_k_uses_the_general_scan():
+    """k > 16 in the split mode scans the float32 rows (the general exact-fp32
+    kernel, a second descriptor over corpus32)."""
+    w, x, q = _x("dup", 631)
+    C = w["C"]
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :1]
+    d, p, st = bucket_topk(ix, T(q), T(classes.astype(np.int32)), 30)
+    ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, 1, 30, C)
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-5, tie=1e-6) == 0
+
+
+# ---- the drop-in against the reference's own outputs (r5 fixtures) ------------
+def _frames(w, x):
+    data = pd.DataFrame(w["xn"])
+    data.index += 1
+    data_search = pd.DataFrame(x)
+    data_search.index += 1
+    return data, data_search
+
+
+@pytest.mark.parametrize("name", list(CASES))
+def test_split_dropin_search_matches_reference(name):
+    from li.LearnedIndex import LearnedIndex, dist_dtype
+    from test_gpu_golden_r2 import _nn
+    _, n, nq, C, R, k, mode, arch, seed, thr, qdt = CASES[name]
+    w, x, q, arith = inputs_r5(name)
+    li = LearnedIndex()
+    li.model = _nn(w["layers"], arch, C)
+    data, data_search = _frames(w, x)
+    assert dist_dtype(data_search, q) == arith
+    dists, anns = li.search(data, w["qn"], data_search, q, w["labels"], n_buckets=R, k=k,
+                            use_threshold=thr)
+    assert li._index.storage == "f32x"
+    check(name, dists, anns, arith)
+
+
+@pytest.mark.parametrize("name", list(SINGLES))
+def test_split_dropin_search_single_matches_reference(name):
+    from li.LearnedIndex import LearnedIndex
+    from test_gpu_golden_r2 import _nn
+    _, n, nq, C, R, k, mode, arch, seed = SINGLES[name]
+    w, x, q, arith = inputs_r5(name)
+    li = LearnedIndex()
+    li.model = _nn(w["layers"], arch, C)
+    data, data_search = _frames(w, x)
+    data["category"] = w["labels"]
+    classes = G5[f"search_{name}__classes"].astype(np.int64)
+    dists, anns = li.search_single(data, data_search, q, classes[:, 0], k=k)
+    check(name, dists, anns, arith)
+
+
+@pytest.mark.parametrize("name", list(BASES))
+def test_split_dropin_baseline_matches_reference(name):
+    from li.Baseline import Baseline
+    _, n, nq, k, mode, seed = BASES[name]
+    w = workloads.clustered(n=n, nq=nq, C=16, seed=seed, label_mode=mode)
+    x32, q32 = workloads.float32_inputs(w, seed)
+    dists, nns, _ = Baseline().search(q32, x32, k=k)
+    ref_d, ref_n = G5[f"base_{name}__dists"], G5[f"base_{name}__nns"]
+    assert O.compare_lists(ref_d, ref_n, dists, nns, atol=1e-5, tie=1e-6) == 0

@@ -90,3 +90,19 @@ def float64_inputs(w, seed, rel=2e-10):
     q64 *= 1.0 + rel * rng.standard_normal(q64.shape)
     assert np.array_equal(x64.astype(np.float32), w["x"]) and np.array_equal(q64.astype(np.float32), w["q"])
     return x64, q64
+
+
+def float32_inputs(w, seed, rel=2e-5, rel_q=None):
+    """Float32 corpus and queries that are NOT fp16-exact, for the split mode
+    (lmi_index_desc.corpus32): the workload's fp16-exact values times
+    (1 + rel N(0, 1)).  rel = 2e-5 is below half an fp16 ulp (2^-12), so the
+    normalised fp16 rounding the split mode scans maps most rows back onto
+    their fp16 originals: near-duplicates and exact duplicates of the
+    workload become ties of the fp16 scan that only the exact float32
+    distances order -- the step the split mode has to get right."""
+    rng = np.random.Generator(np.random.PCG64(seed + 32))
+    rel_q = rel if rel_q is None else rel_q
+    x32 = (w["x"].astype(np.float64) * (1.0 + rel * rng.standard_normal(w["x"].shape))).astype(np.float32)
+    q32 = (w["q"].astype(np.float64) * (1.0 + rel_q * rng.standard_normal(w["q"].shape))).astype(np.float32)
+    assert not np.array_equal(x32.astype(np.float16).astype(np.float32), x32)
+    return x32, q32
