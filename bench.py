@@ -84,6 +84,8 @@ def build_workload(args, device, rank, world):
     router = DeviceRouter(layers, device=device)
     labels = router.argmax(xn)
     del xn
+    if args.corpus == "f32":
+        x, q = not_fp16(x, 11), not_fp16(q, 12)
     torch.cuda.synchronize()
     log(f"[bench] workload n={n} built in {time.time() - t0:.1f}s")
     t0 = time.time()
@@ -94,6 +96,20 @@ def build_workload(args, device, rank, world):
         f"in {time.time() - t0:.1f}s; bucket sizes min/median/max = "
         f"{index.bucket_size.min()}/{int(np.median(index.bucket_size))}/{index.bucket_size.max()}")
     return x, q, qn, router, index, labels
+
+
+@torch.no_grad()
+def not_fp16(x, seed, rel=2e-5, chunk=1 << 20):
+    """--corpus f32: float32 values that are NOT fp16-exact (x (1 + rel N)),
+    generated on x's device in chunks (a seeded torch generator per call):
+    the split mode's workload (lmi_index_desc.corpus32)."""
+    g = torch.Generator(device=x.device)
+    g.manual_seed(seed)
+    out = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+    for a in range(0, x.shape[0], chunk):
+        blk = x[a:a + chunk].float()
+        out[a:a + chunk] = blk * (1.0 + rel * torch.randn(blk.shape, generator=g, device=x.device))
+    return out
 
 
 @torch.no_grad()
@@ -121,7 +137,7 @@ def algorithmic_bytes(index, classes, nq):
     probed = np.unique(classes)
     loc = index.bucket_off_local.cpu().numpy()
     rows = int(sum(loc[c + 1] - loc[c] for c in probed))
-    s = 2 if index.storage == "f16" else 4
+    s = 4 if index.storage == "f32" else 2   # (f32x: its scans stream the fp16 rounding)
     byts = rows * (index.d_pad * s + 4) + nq * index.d_pad * s
     sizes = np.diff(loc)
     flops = 2.0 * index.d * float(sizes[classes].sum())
@@ -146,7 +162,7 @@ def cpu_baseline(index, q, classes, lists_d, args, budget_s=15.0):
     import lmi_oracle as O
     off = index.layout.bucket_off
     qh = q.cpu().numpy()
-    xh = index.corpus[:, : index.d].cpu().numpy()  # the corpus on the host (untimed)
+    xh = (index.corpus32 if index.corpus32 is not None else index.corpus)[:, : index.d].cpu().numpy()
     R, k = args.R, args.k
     ld = lists_d.cpu().numpy().astype(np.float64)
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
@@ -234,7 +250,7 @@ def list_parity(index, x, q, classes, lists_d, lists_pos, n_sample, f64, seed=5)
     for c in np.unique(cls):
         a, b = int(off[c]), int(off[c + 1])
         if full:
-            y = index.corpus[a:b, :index.d]
+            y = (index.corpus32 if index.corpus32 is not None else index.corpus)[a:b, :index.d]
         else:
             y = x[order[a:b].to(x.device)].to(dev)
         y = y.double()
@@ -403,6 +419,11 @@ def main():
     ap.add_argument("--batches", type=int, default=4,
                     help="distinct 10k-query batches the timed loop rotates through (host "
                          "arrays, each staged into pinned memory inside the timed loop)")
+    ap.add_argument("--corpus", default="f16", choices=["f16", "f32"],
+                    help="f16: the synthetic clip768 values are fp16-exact (stored float32, as "
+                         "clip768v2's float16 data widened); f32: float32 values that are NOT "
+                         "fp16-exact (x (1 + 2e-5 N)): the split mode (storage f32x), timed with "
+                         "the per-batch step graph (the batch stream is the fp16 scan's)")
     ap.add_argument("--dist", default="f32", choices=["f32", "f64"],
                     help="distance arithmetic of the headline line: f32 = the reference's on "
                          "float32 DataFrames (the synthetic corpus is float32 holding fp16-exact "
@@ -426,6 +447,8 @@ def main():
     qb = synth.query_batches(max(1, args.batches), args.nq, device,
                              kind="random" if args.scale == "100M" else "mixture",
                              centres=args.centres)
+    if args.corpus == "f32":
+        qb = [(q if i == 0 else not_fp16(b_q, 100 + i), b_qn) for i, (b_q, b_qn) in enumerate(qb)]
     host_batches = [(b_qn.cpu().numpy(), b_q.cpu().numpy()) for b_q, b_qn in qb]
     del qb
 
@@ -791,8 +814,9 @@ def main():
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
         "higher_is_better": True, "scaling": "strong",
         "vs_baseline": round(value / PUBLISHED_QPS_10M, 1) if args.scale == "10M" else None,
-        "dtype": "f16" if args.dist == "f32" else "f16+f64", "data": "synthetic",
-        "config": {"workload": f"{args.scale} {'random unit (configs[4])' if args.scale == '100M' else 'clip768-like'} synthetic (fp16-exact), {args.n_buckets} "
+        "dtype": ("f16" if args.dist == "f32" else "f16+f64") if args.corpus == "f16" else
+                 ("f16 scan + f64 re-score" if args.dist == "f32" else "f16 scan + f64"), "data": "synthetic",
+        "config": {"workload": f"{args.scale} {'random unit (configs[4])' if args.scale == '100M' else 'clip768-like'} synthetic ({'fp16-exact' if args.corpus == 'f16' else 'float32, not fp16-exact: split mode'}), {args.n_buckets} "
                                f"buckets, R={args.R}, k={args.k}, {args.nq} queries, router "
                                f"{args.arch}", "n": SCALES[args.scale], "d": 768, "nq": args.nq,
                    "R": args.R, "k": args.k, "n_buckets": args.n_buckets, "router": args.arch,

@@ -340,6 +340,29 @@ int lmi_replay_device_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t
                           const double* thr_round0, double* dists_out, uint32_t* anns_out,
                           int32_t* status, void* workspace, size_t ws_bytes, void* stream);
 
+/* ABI 9: the device replay in two phases, so that a stream of batches runs the
+ * part that depends on the classes only beside the scan:
+ *   LMI_REPLAY_PHASE_GROUPS  every round's groups (queries by category, in
+ *                            ascending q) and round 0's prologue; zeroes
+ *                            *status (the phased call owns the word);
+ *   LMI_REPLAY_PHASE_ROUNDS  the rounds and the answer (lists needed).
+ * Both = lmi_replay_device / _f64 (the caller zeroes *status then).  Calls of
+ * one replay take the same arguments and workspace, GROUPS first (lists_d /
+ * lists_pos / pos_to_id / dists_out / anns_out may be NULL in a GROUPS call);
+ * lists_f64 selects float64 lists.  With k_round <= 20 and k_final + k_round
+ * <= 20 every round r >= 1 is one launch: the merge of round r - 1 runs inside
+ * round r's group workgroups, a thread per query, and the last merge writes
+ * the answer (the same results, tests/test_gpu_replay.py). */
+#define LMI_REPLAY_PHASE_GROUPS 1
+#define LMI_REPLAY_PHASE_ROUNDS 2
+int lmi_replay_device_phase(int32_t phases, int32_t lists_f64, const int32_t* classes, int32_t nq,
+                            int32_t R, int32_t k_list, const void* lists_d, const int32_t* lists_pos,
+                            int32_t k_round, int32_t k_final, const int64_t* bucket_size,
+                            int32_t n_buckets, const int64_t* pos_to_id, int64_t n_total,
+                            int32_t use_threshold, const double* thr_round0, double* dists_out,
+                            uint32_t* anns_out, int32_t* status, void* workspace, size_t ws_bytes,
+                            void* stream);
+
 /* ---- k-means for the index build (ABI 3) -------------- */
 /* Replaces faiss.Kmeans(d, k, seed=2023).train(X) and
  * kmeans.index.search(X, 1) (LearnedIndex.py:242-282); the Lloyd loop, the

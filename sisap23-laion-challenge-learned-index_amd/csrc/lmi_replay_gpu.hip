@@ -594,8 +594,10 @@ __global__ __launch_bounds__(kT) void replay_thr_kernel(int32_t nq, int32_t kr, 
                                                         const double* __restrict__ thr0,
                                                         double* __restrict__ thr,
                                                         double* __restrict__ dr_d,
-                                                        int32_t* __restrict__ dr_p) {
+                                                        int32_t* __restrict__ dr_p,
+                                                        int32_t* __restrict__ zero_status) {
     const int q = blockIdx.x * kT + threadIdx.x;
+    if (zero_status && q == 0) *zero_status = 0;  // (the phased replay's GROUPS phase)
     if (q >= nq) return;
     for (int j = 0; j < kr; ++j) {
         dr_d[(size_t)q * kr + j] = kFill;
@@ -663,6 +665,105 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
         Fp_out[(size_t)q * fs + rank] = j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF];
     }
     if (thr_next && rank == wn - 1) thr_next[q] = dj;  // the merged row is ascending
+}
+
+// The merge of one query (LearnedIndex.py:82-97, replay_merge_kernel's
+// arithmetic) by one thread, its row in registers: the first wn of the stable
+// argsort of hstack(F_q, D_q) (first: F = D_q), written into Fd_out / Fp_out
+// or, with `out` (the last round), straight to the answer (positions mapped to
+// ids).  Returns the merged row's largest kept value (its threshold, :71-72).
+struct MergeRow {
+    int32_t kr, fs, wF, wn, first;
+    const double* Fd;
+    const int32_t* Fp;
+    double* Fd_out;
+    int32_t* Fp_out;
+    const double* dr_d;  // this query's round rows
+    const int32_t* dr_p;
+};
+constexpr int kMergeRegs = 20;  // hstack(F, D) widths a thread holds in registers (k = k_round = 10)
+
+template <bool OUT>
+__device__ inline double merge_row(const MergeRow& m, int q, const int64_t* pos_to_id, int64_t n_total,
+                                   double* dists, uint32_t* anns, int32_t w, int32_t* status) {
+    const int n = m.first ? m.kr : m.wF + m.kr;
+    double v[kMergeRegs];
+    int32_t pv[kMergeRegs];
+#pragma unroll
+    for (int j = 0; j < kMergeRegs; ++j) {
+        const bool inF = !m.first && j < m.wF;
+        const int jd = m.first ? j : j - m.wF;
+        v[j] = j >= n ? 0.0 : inF ? m.Fd[(size_t)q * m.fs + j] : m.dr_d[(size_t)q * m.kr + jd];
+        pv[j] = j >= n ? -1 : inF ? m.Fp[(size_t)q * m.fs + j] : m.dr_p[(size_t)q * m.kr + jd];
+    }
+    double thr = v[0];
+#pragma unroll
+    for (int j = 0; j < kMergeRegs; ++j) {
+        if (j < n) {  // (no break: the row stays in registers only if the loop unrolls)
+        int rank = j;  // (first: the row as it is, :86 -- round 0's D_0)
+        if (!m.first) {
+            rank = 0;
+#pragma unroll
+            for (int i = 0; i < kMergeRegs; ++i)
+                rank += (i < n && (v[i] < v[j] || (v[i] == v[j] && i < j))) ? 1 : 0;
+        }
+        if (rank < m.wn) {
+            if constexpr (OUT) {
+                int64_t id = 0;
+                if (pv[j] >= 0) {
+                    if (pv[j] < n_total) id = pos_to_id[pv[j]];
+                    else atomicOr(status, 4);
+                }
+                dists[(size_t)q * w + rank] = v[j];
+                anns[(size_t)q * w + rank] = (uint32_t)id;
+            } else {
+                m.Fd_out[(size_t)q * m.fs + rank] = v[j];
+                m.Fp_out[(size_t)q * m.fs + rank] = pv[j];
+            }
+        }
+        // round 0's row need not be ascending (the <k quirk): its maximum; a
+        // merged row is ascending: the value placed last
+        if (m.first) thr = fmax(thr, v[j]);
+        else if (rank == m.wn - 1) thr = v[j];
+        }
+    }
+    return thr;
+}
+
+// Rounds r >= 1 in one launch each (C + 1 workgroups, category c of round r;
+// category C holds the queries whose class is out of range): the workgroup
+// first merges round r - 1 for the queries of its own group (a thread per
+// query, merge_row) -- their thresholds, and round r's rows reset to
+// (10000, -1) -- then runs round r's group (replay_group_body), which reads
+// those thresholds; every query is in exactly one group of a round, so the
+// merge of round r - 1 is split over the workgroups of round r.  One launch
+// instead of replay_merge_kernel + replay_group_kernel.
+__global__ __launch_bounds__(kTG) void replay_round_kernel(RoundArgs a, MergeRow m) {
+    const int c = blockIdx.x;
+    const int g0 = a.gb[2 * c], g1 = a.gb[2 * c + 1];
+    double* thr = const_cast<double*>(a.thr);
+    for (int gi = g0 + threadIdx.x; gi < g1; gi += kTG) {
+        const int q = a.groups[gi];
+        thr[q] = merge_row<false>(m, q, nullptr, 0, nullptr, nullptr, 0, nullptr);
+        for (int j = 0; j < a.kr; ++j) {
+            a.dr_d[(size_t)q * a.kr + j] = kFill;
+            a.dr_p[(size_t)q * a.kr + j] = -1;
+        }
+    }
+    __syncthreads();  // (the group's thresholds and reset rows, within the workgroup)
+    if (c < a.C) replay_group_body(a, c);
+}
+
+// The last round's merge and the answer (replay_merge_kernel +
+// replay_out_kernel), a thread per query.
+__global__ __launch_bounds__(kT) void replay_final_kernel(int32_t nq, MergeRow m,
+                                                          const int64_t* __restrict__ pos_to_id,
+                                                          int64_t n_total, double* __restrict__ dists,
+                                                          uint32_t* __restrict__ anns, int32_t w,
+                                                          int32_t* __restrict__ status) {
+    const int q = blockIdx.x * kT + threadIdx.x;
+    if (q >= nq) return;
+    merge_row<true>(m, q, pos_to_id, n_total, dists, anns, w, status);
 }
 
 __global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, int32_t fs,
@@ -737,7 +838,7 @@ int replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32_t k_
                        int32_t n_buckets, const int64_t* pos_to_id, int64_t n_total,
                        int32_t use_threshold, const double* thr_round0, double* dists_out,
                        uint32_t* anns_out, int32_t* status, void* workspace, size_t ws_bytes,
-                       void* stream);
+                       void* stream, int32_t phases = LMI_REPLAY_PHASE_GROUPS | LMI_REPLAY_PHASE_ROUNDS);
 }  // namespace lmi
 
 extern "C" int lmi_replay_device(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
@@ -765,19 +866,33 @@ extern "C" int lmi_replay_device_f64(const int32_t* classes, int32_t nq, int32_t
                                    stream);
 }
 
+extern "C" int lmi_replay_device_phase(int32_t phases, int32_t lists_f64, const int32_t* classes, int32_t nq,
+                                       int32_t R, int32_t k_list, const void* lists_d,
+                                       const int32_t* lists_pos, int32_t k_round, int32_t k_final,
+                                       const int64_t* bucket_size, int32_t n_buckets,
+                                       const int64_t* pos_to_id, int64_t n_total, int32_t use_threshold,
+                                       const double* thr_round0, double* dists_out, uint32_t* anns_out,
+                                       int32_t* status, void* workspace, size_t ws_bytes, void* stream) {
+    return lmi::replay_device_impl(classes, nq, R, k_list, lists_d, lists_f64 ? 1 : 0, lists_pos, k_round,
+                                   k_final, bucket_size, n_buckets, pos_to_id, n_total, use_threshold,
+                                   thr_round0, dists_out, anns_out, status, workspace, ws_bytes, stream,
+                                   phases);
+}
+
 int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32_t k_list,
                             const void* lists_d, int lists_f64, const int32_t* lists_pos,
                             int32_t k_round, int32_t k_final, const int64_t* bucket_size,
                             int32_t n_buckets, const int64_t* pos_to_id, int64_t n_total,
                             int32_t use_threshold, const double* thr_round0, double* dists_out,
                             uint32_t* anns_out, int32_t* status, void* workspace, size_t ws_bytes,
-                            void* stream) {
+                            void* stream, int32_t phases) {
     using namespace lmi;
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && k_round >= 1 && k_final >= 1 && k_list >= 1 && n_buckets >= 1,
                   "lmi_replay_device: bad sizes");
     LMI_CHECK_ARG(k_round <= kMaxKr, "lmi_replay_device: k_round=%d > %d", k_round, kMaxKr);
     LMI_CHECK_ARG(k_final <= kMaxW, "lmi_replay_device: k=%d > %d", k_final, kMaxW);
     LMI_CHECK_ARG(k_list >= k_round, "lmi_replay_device: lists of %d < k_round=%d", k_list, k_round);
+    LMI_CHECK_ARG(phases >= 1 && phases <= 3, "lmi_replay_device: bad phases %d", phases);
     int w = k_round;
     for (int r = 1; r < R; ++r) {
         w = std::min(k_final, w + k_round);
@@ -788,8 +903,10 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         }
     }
     if (nq == 0) return LMI_OK;
-    LMI_CHECK_ARG(classes && lists_d && lists_pos && bucket_size && pos_to_id && dists_out &&
-                  anns_out && status && workspace, "lmi_replay_device: null pointer");
+    const bool do_groups = phases & LMI_REPLAY_PHASE_GROUPS, do_rounds = phases & LMI_REPLAY_PHASE_ROUNDS;
+    LMI_CHECK_ARG(classes && bucket_size && status && workspace, "lmi_replay_device: null pointer");
+    LMI_CHECK_ARG(!do_rounds || (lists_d && lists_pos && pos_to_id && dists_out && anns_out),
+                  "lmi_replay_device: null pointer");
     const ReplayWs s = replay_ws(nq, R, k_list, k_round, w, n_buckets);
     if (ws_bytes < s.total) {
         set_error("workspace %zu B < required %zu B", ws_bytes, s.total);
@@ -802,23 +919,23 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
     int32_t* groups = (int32_t*)(ws + s.groups);
     int32_t* gb = (int32_t*)(ws + s.gb);
     const dim3 qgrid((unsigned)((nq + kT - 1) / kT));
-    // every round's groups in one launch ((C + 1) x R workgroups)
-    hipLaunchKernelGGL(replay_groups_kernel, dim3(C + 1, R), dim3(kTG), 0, st, classes, nq, R, C, groups, gb);
-    LMI_LAUNCH_CHECK("replay_groups_kernel");
-    int cur = 0;  // F lives in buffer cur; the merge writes the other one
-    int wF = 0;
-    for (int r = 0; r < R; ++r) {
-        double* Fd = (double*)(ws + s.Fd[cur]);
-        int32_t* Fp = (int32_t*)(ws + s.Fp[cur]);
-        const bool thresholded = ((r > 0) && use_threshold) || (r == 0 && thr_round0);
-        const int mode = (r == 0 && thr_round0) ? 1 : (thresholded ? 2 : 0);
-        double* drd = (double*)(ws + s.drd[r & 1]);
-        int32_t* drp = (int32_t*)(ws + s.drp[r & 1]);
-        if (r == 0) {  // later rounds: fused into the previous round's merge
-            hipLaunchKernelGGL(replay_thr_kernel, qgrid, dim3(kT), 0, st, nq, k_round, fs, wF, mode,
-                               Fd, thr_round0, (double*)(ws + s.thr), drd, drp);
-            LMI_LAUNCH_CHECK("replay_thr_kernel");
-        }
+    auto thresholded_at = [&](int r) { return ((r > 0) && use_threshold) || (r == 0 && thr_round0); };
+    if (do_groups) {
+        // every round's groups ((C + 1) x R workgroups) and round 0's prologue:
+        // its rows reset, its thresholds (the caller's, or none); the phased
+        // call (GROUPS alone) also zeroes the status word.  They depend on the
+        // classes only: a stream of batches runs them beside the scan.
+        hipLaunchKernelGGL(replay_groups_kernel, dim3(C + 1, R), dim3(kTG), 0, st, classes, nq, R, C, groups, gb);
+        LMI_LAUNCH_CHECK("replay_groups_kernel");
+        const int mode = thr_round0 ? 1 : 0;
+        hipLaunchKernelGGL(replay_thr_kernel, qgrid, dim3(kT), 0, st, nq, k_round, fs, 0, mode,
+                           (const double*)(ws + s.Fd[0]), thr_round0, (double*)(ws + s.thr),
+                           (double*)(ws + s.drd[0]), (int32_t*)(ws + s.drp[0]),
+                           do_rounds ? nullptr : status);
+        LMI_LAUNCH_CHECK("replay_thr_kernel");
+    }
+    if (!do_rounds) return LMI_OK;
+    auto round_args = [&](int r) {
         RoundArgs a{};
         a.classes = classes;
         a.nq = nq;
@@ -833,33 +950,66 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         a.bucket_size = bucket_size;
         a.groups = groups + (size_t)r * nq;
         a.gb = gb + (size_t)r * (C + 1) * 2;
-        a.thresholded = thresholded ? 1 : 0;
+        a.thresholded = thresholded_at(r) ? 1 : 0;
         a.thr = (const double*)(ws + s.thr);
-        a.dr_d = drd;
-        a.dr_p = drp;
+        a.dr_d = (double*)(ws + s.drd[r & 1]);
+        a.dr_p = (int32_t*)(ws + s.drp[r & 1]);
         a.uraw = (int32_t*)(ws + s.uraw);
         a.status = status;
-        hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, a);
-        LMI_LAUNCH_CHECK("replay_group_kernel");
+        return a;
+    };
+    // hstack(F, D) of every merge within a thread's registers: each round r
+    // >= 1 is ONE launch (the merge of r - 1 inside round r's groups) and the
+    // last merge writes the answer (replay_round_kernel, replay_final_kernel);
+    // wider rows take the per-element merge kernels
+    const bool fused = k_round <= kMergeRegs && k_final + k_round <= kMergeRegs;
+    int cur = 0;  // F lives in buffer cur; a merge writes the other one
+    int wF = 0;
+    for (int r = 0; r < R; ++r) {
+        double* Fd = (double*)(ws + s.Fd[cur]);
+        int32_t* Fp = (int32_t*)(ws + s.Fp[cur]);
+        double* drd = (double*)(ws + s.drd[r & 1]);
+        int32_t* drp = (int32_t*)(ws + s.drp[r & 1]);
         const bool last = r + 1 == R;
         const int wn = (r == 0) ? k_round : std::min(k_final, wF + k_round);
-        const int n = (r == 0) ? k_round : wF + k_round;
-        const dim3 mgrid((unsigned)(((int64_t)nq * n + kT - 1) / kT));
-        hipLaunchKernelGGL(replay_merge_kernel, mgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
-                           r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
-                           (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp,
-                           last ? nullptr : (double*)(ws + s.thr),
-                           last ? nullptr : (double*)(ws + s.drd[(r + 1) & 1]),
-                           last ? nullptr : (int32_t*)(ws + s.drp[(r + 1) & 1]));
-        LMI_LAUNCH_CHECK("replay_merge_kernel");
+        if (fused) {
+            if (r == 0) {
+                hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, round_args(0));
+                LMI_LAUNCH_CHECK("replay_group_kernel");
+            }
+            MergeRow m{k_round, fs, wF, wn, r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
+                       (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp};
+            if (last) {
+                hipLaunchKernelGGL(replay_final_kernel, qgrid, dim3(kT), 0, st, nq, m, pos_to_id, n_total,
+                                   dists_out, anns_out, w, status);
+                LMI_LAUNCH_CHECK("replay_final_kernel");
+            } else {
+                hipLaunchKernelGGL(replay_round_kernel, dim3(C + 1), dim3(kTG), 0, st, round_args(r + 1), m);
+                LMI_LAUNCH_CHECK("replay_round_kernel");
+            }
+        } else {
+            hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, round_args(r));
+            LMI_LAUNCH_CHECK("replay_group_kernel");
+            const int n = (r == 0) ? k_round : wF + k_round;
+            const dim3 mgrid((unsigned)(((int64_t)nq * n + kT - 1) / kT));
+            hipLaunchKernelGGL(replay_merge_kernel, mgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
+                               r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
+                               (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp,
+                               last ? nullptr : (double*)(ws + s.thr),
+                               last ? nullptr : (double*)(ws + s.drd[(r + 1) & 1]),
+                               last ? nullptr : (int32_t*)(ws + s.drp[(r + 1) & 1]));
+            LMI_LAUNCH_CHECK("replay_merge_kernel");
+        }
         cur ^= 1;
         wF = wn;
     }
-    const double* Fd = (const double*)(ws + s.Fd[cur]);
-    const int32_t* Fp = (const int32_t*)(ws + s.Fp[cur]);
-    const dim3 ogrid((unsigned)(((int64_t)nq * w + kT - 1) / kT));
-    hipLaunchKernelGGL(replay_out_kernel, ogrid, dim3(kT), 0, st, nq, w, fs, Fd, Fp, pos_to_id, n_total,
-                       dists_out, anns_out, status);
-    LMI_LAUNCH_CHECK("replay_out_kernel");
+    if (!fused) {
+        const double* Fd = (const double*)(ws + s.Fd[cur]);
+        const int32_t* Fp = (const int32_t*)(ws + s.Fp[cur]);
+        const dim3 ogrid((unsigned)(((int64_t)nq * w + kT - 1) / kT));
+        hipLaunchKernelGGL(replay_out_kernel, ogrid, dim3(kT), 0, st, nq, w, fs, Fd, Fp, pos_to_id, n_total,
+                           dists_out, anns_out, status);
+        LMI_LAUNCH_CHECK("replay_out_kernel");
+    }
     return LMI_OK;
 }

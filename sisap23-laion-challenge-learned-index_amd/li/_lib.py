@@ -38,6 +38,8 @@ LMI_Q_SEED_ROUND0 = 0x100
 LMI_Q_PHASE_PLAN = 0x200
 LMI_Q_PHASE_SCAN = 0x400
 LMI_Q_PHASE_MERGE = 0x800
+LMI_REPLAY_PHASE_GROUPS = 1
+LMI_REPLAY_PHASE_ROUNDS = 2
 LMI_MAX_LAYERS = 8
 LMI_MAX_K = 16
 LMI_MAX_K_PASSES = 1024
@@ -59,6 +61,7 @@ EXPORTS = (
     "lmi_bucket_topk_f64q",
     "lmi_refine_fallback_count",
     "lmi_split_eps",
+    "lmi_replay_device_phase",
     "lmi_merge_topk_f64",
     "lmi_packed_rank_words",
     "lmi_merge_topk_packed",
@@ -141,6 +144,8 @@ _SIGNATURES = {
     "lmi_bucket_topk_f64q": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _P, _I32,
                                        _I32, _I32, C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_split_eps": (C.c_double, [_I32]),
+    "lmi_replay_device_phase": (C.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32,
+                                          _P, _I64, _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,
                                             _P]),
     "lmi_merge_topk_f64": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),

@@ -682,21 +682,27 @@ def replay(classes: np.ndarray, lists_d: np.ndarray, lists_pos: np.ndarray, *, k
 def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch.Tensor, *,
                   k_round: int, k_final: int, bucket_size: torch.Tensor, pos_to_id: torch.Tensor,
                   use_threshold: bool, thr_round0: Optional[torch.Tensor] = None, stream=None,
-                  out=None):
-    """A5 on the device (lmi_replay_device, or lmi_replay_device_f64 for
-    float64 lists): same results as `replay`, device tensors in and out:
-    (dists f64 [nq, w], anns uint32-as-int32 [nq, w], status); `out` = such a
-    triple to write into (the status word zeroed by the caller)."""
+                  out=None, phases: int = 3, ws: Optional[torch.Tensor] = None,
+                  k_list: Optional[int] = None):
+    """A5 on the device (lmi_replay_device_phase; float32 or float64 lists):
+    same results as `replay`, device tensors in and out: (dists f64 [nq, w],
+    anns uint32-as-int32 [nq, w], status); `out` = such a triple to write into
+    (the status word zeroed by the caller, or by a GROUPS phase).  `phases`:
+    LMI_REPLAY_PHASE_GROUPS (classes only: lists_d / lists_pos may be None,
+    then give `k_list`, the lists' width, and float32 is assumed for sizing),
+    LMI_REPLAY_PHASE_ROUNDS, or both (3); the calls of one replay share `ws`
+    (a caller-owned uint8 workspace; default: a new one per call)."""
     lib = _lib.load()
-    dev = lists_d.device
+    dev = classes.device if lists_d is None else lists_d.device
     classes = _as_torch(classes, dev, torch.int32)
     if classes.dim() == 1:
         classes = classes[:, None].contiguous()
     nq, R = classes.shape
-    f64 = lists_d.dtype == torch.float64
-    lists_d = _as_torch(lists_d, dev, torch.float64 if f64 else torch.float32).reshape(nq, R, -1).contiguous()
-    lists_pos = _as_torch(lists_pos, dev, torch.int32).reshape(nq, R, -1).contiguous()
-    k_list = lists_d.shape[2]
+    f64 = lists_d is not None and lists_d.dtype == torch.float64
+    if lists_d is not None:
+        lists_d = _as_torch(lists_d, dev, torch.float64 if f64 else torch.float32).reshape(nq, R, -1).contiguous()
+        lists_pos = _as_torch(lists_pos, dev, torch.int32).reshape(nq, R, -1).contiguous()
+        k_list = lists_d.shape[2]
     w = k_round if R == 1 else k_final
     if out is None:
         dists = torch.empty((nq, w), dtype=torch.float64, device=dev)
@@ -706,18 +712,20 @@ def replay_device(classes: torch.Tensor, lists_d: torch.Tensor, lists_pos: torch
         dists, anns, status = out
     n_b = int(bucket_size.numel())
     need = lib.lmi_replay_device_workspace_bytes(nq, R, k_list, k_round, k_final, n_b)
-    ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
+    if ws is None:
+        ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
+    else:
+        _workspace(ws, need, "replay")
     thr = None
     if thr_round0 is not None:
         thr = _as_torch(thr_round0, dev, torch.float64).reshape(-1)
         if thr.numel() != nq:
             raise ValueError("threshold_dist must have one value per query")
     s = stream if stream is not None else _lib.stream_handle(dev)
-    fn = "lmi_replay_device_f64" if f64 else "lmi_replay_device"
-    check(fn, getattr(lib, fn)(
-        ptr(classes), nq, R, k_list, ptr(lists_d), ptr(lists_pos), k_round, k_final,
-        ptr(bucket_size), n_b, ptr(pos_to_id), int(pos_to_id.numel()), int(bool(use_threshold)),
-        ptr(thr), ptr(dists), ptr(anns), ptr(status), ptr(ws), ws.numel(), s))
+    check("lmi_replay_device_phase", lib.lmi_replay_device_phase(
+        int(phases), int(f64), ptr(classes), nq, R, k_list, ptr(lists_d), ptr(lists_pos), k_round,
+        k_final, ptr(bucket_size), n_b, ptr(pos_to_id), int(pos_to_id.numel()),
+        int(bool(use_threshold)), ptr(thr), ptr(dists), ptr(anns), ptr(status), ptr(ws), ws.numel(), s))
     return dists, anns, status
 
 

@@ -135,6 +135,11 @@ class StreamedSearch:
                            torch.empty((nq, R, kl), dtype=torch.int32, device=dev),
                            self.ans[j][3][0:1]) for j in range(NS)]
         bsz, p2id = s._device_tables()
+        # the replay's workspace per slot: its GROUPS phase (every round's
+        # groups, from the classes) runs in the plan stage, beside the scan;
+        # its ROUNDS phase in the finish
+        rwb = int(lib.lmi_replay_device_workspace_bytes(nq, R, kl, k_round, k, int(bsz.numel())))
+        self.rws = [torch.empty(max(rwb, 256), dtype=torch.uint8, device=dev) for _ in range(NS)]
         seed = use_threshold and k <= k_round and _SEED_ROUND0
         scan_fn = bucket_topk_f64 if f64 else bucket_topk
         self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
@@ -179,6 +184,10 @@ class StreamedSearch:
                 self.cls[j].view(G, per, R).copy_(xa[:, self.o_cls:].view(G, per, R))
                 torch.amax(xa[:, self.o_flag:self.o_flag + 1], dim=0, out=st)
             phase(j, _lib.LMI_Q_PHASE_PLAN)
+            _, ad, aa, ast = self.ans[j]
+            replay_device(self.cls[j][:nq], None, None, k_round=k_round, k_final=k, bucket_size=bsz,
+                          pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]),
+                          phases=_lib.LMI_REPLAY_PHASE_GROUPS, ws=self.rws[j], k_list=kl)
 
         def scan(j):
             phase(j, _lib.LMI_Q_PHASE_SCAN)
@@ -190,7 +199,7 @@ class StreamedSearch:
 
         def finish2(j):
             buf, ad, aa, ast = self.ans[j]
-            ast[1:2].zero_()
+            # (the replay status word was zeroed by the plan's GROUPS phase)
             if G > 1:
                 dd = torch.empty((nq * R, kl), dtype=ldt, device=dev) if self._mdd[j] is None \
                     else self._mdd[j]
@@ -204,7 +213,8 @@ class StreamedSearch:
             else:
                 dd, pp = self.lists[j][0], self.lists[j][1]
             replay_device(self.cls[j][:nq], dd, pp, k_round=k_round, k_final=k, bucket_size=bsz,
-                          pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]))
+                          pos_to_id=p2id, use_threshold=use_threshold, out=(ad, aa, ast[1:2]),
+                          phases=_lib.LMI_REPLAY_PHASE_ROUNDS, ws=self.rws[j])
             self.h_ans[j].copy_(buf, non_blocking=True)
 
         def finish(j):

@@ -159,3 +159,31 @@ def test_device_replay_wide_position_range(use_threshold):
     assert int(st.item()) == 0
     np.testing.assert_array_equal(dd_.cpu().numpy(), ref_d)
     np.testing.assert_array_equal(aa.cpu().numpy().view(np.uint32), ref_a)
+
+
+@pytest.mark.parametrize("k_final,R", [(10, 4), (14, 3), (10, 1)])
+def test_phased_replay_equals_one_call(k_final, R):
+    """lmi_replay_device_phase: GROUPS (the classes only; zeroes the status
+    word) then ROUNDS on one workspace = the one-call replay, bit for bit, on
+    the fused rounds (k + k_round <= 20) and on the per-element merges."""
+    from li import _lib
+    classes, d, pos, size, ids = _random_lists(31 + R, nq=500, R=R, C=24, kl=10, tiny=(3,),
+                                               empty=(5,))
+    dev = torch.device("cuda")
+    T = lambda a: torch.from_numpy(a).to(dev)  # noqa: E731
+    kw = dict(k_round=10, k_final=k_final, bucket_size=T(size), pos_to_id=T(ids), use_threshold=True)
+    one = replay_device(T(classes), T(d), T(pos), **kw)
+    ws = torch.empty(1 << 24, dtype=torch.uint8, device=dev)
+    w = 10 if R == 1 else k_final
+    out = (torch.empty((500, w), dtype=torch.float64, device=dev),
+           torch.empty((500, w), dtype=torch.int32, device=dev),
+           torch.full((1,), 0x70, dtype=torch.int32, device=dev))
+    replay_device(T(classes), None, None, out=out, phases=_lib.LMI_REPLAY_PHASE_GROUPS, ws=ws, k_list=10, **kw)
+    torch.cuda.synchronize()
+    assert int(out[2].item()) == 0
+    replay_device(T(classes), T(d), T(pos), out=out, phases=_lib.LMI_REPLAY_PHASE_ROUNDS, ws=ws, **kw)
+    assert torch.equal(out[0], one[0]) and torch.equal(out[1], one[1]) and int(out[2].item()) == 0
+    ref_d, ref_a = replay(classes, d, pos, k_round=10, k_final=k_final, bucket_size=size, pos_to_id=ids,
+                          use_threshold=True)
+    np.testing.assert_array_equal(out[0].cpu().numpy(), ref_d)
+    np.testing.assert_array_equal(out[1].cpu().numpy().view(np.uint32), ref_a)
