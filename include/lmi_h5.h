@@ -42,7 +42,8 @@ int lmi_h5_read_f32(const char* path, const char* name, int64_t row0, int64_t nr
  * returns them (search.py:48-49, :79-87: clip768v2 'emb' stays float16, which
  * decides the reference's float64 arithmetic, utils.py:11): elem_bytes must be
  * the stored element size (2, 4 or 8, from lmi_h5_dataset_info); the bytes
- * are copied unconverted (little-endian IEEE). */
+ * are copied unconverted (little-endian IEEE, or little-endian integers: a
+ * result file's uint32 knns). */
 int lmi_h5_read_stored(const char* path, const char* name, int64_t row0, int64_t nrows,
                        int32_t elem_bytes, void* out);
 

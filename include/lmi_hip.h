@@ -349,10 +349,7 @@ int lmi_replay_device_f64(const int32_t* classes, int32_t nq, int32_t R, int32_t
  * Both = lmi_replay_device / _f64 (the caller zeroes *status then).  Calls of
  * one replay take the same arguments and workspace, GROUPS first (lists_d /
  * lists_pos / pos_to_id / dists_out / anns_out may be NULL in a GROUPS call);
- * lists_f64 selects float64 lists.  With k_round <= 20 and k_final + k_round
- * <= 20 every round r >= 1 is one launch: the merge of round r - 1 runs inside
- * round r's group workgroups, a thread per query, and the last merge writes
- * the answer (the same results, tests/test_gpu_replay.py). */
+ * lists_f64 selects float64 lists. */
 #define LMI_REPLAY_PHASE_GROUPS 1
 #define LMI_REPLAY_PHASE_ROUNDS 2
 int lmi_replay_device_phase(int32_t phases, int32_t lists_f64, const int32_t* classes, int32_t nq,

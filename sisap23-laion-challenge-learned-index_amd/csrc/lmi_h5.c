@@ -121,9 +121,10 @@ int lmi_h5_read_stored(const char* path, const char* name, int64_t row0, int64_t
     hid_t sp = H5Dget_space(d), t = H5Dget_type(d);
     hsize_t dims[2] = {0, 1};
     const int rank = H5Sget_simple_extent_ndims(sp);
-    if (rank < 1 || rank > 2 || H5Tget_class(t) != H5T_FLOAT ||
+    if (rank < 1 || rank > 2 || (H5Tget_class(t) != H5T_FLOAT && H5Tget_class(t) != H5T_INTEGER) ||
         H5Tget_order(t) != H5T_ORDER_LE) {
-        rc = fail(LMI_E_INVALID, "%s/%s: need a rank-1/2 little-endian floating dataset", path, name);
+        rc = fail(LMI_E_INVALID, "%s/%s: need a rank-1/2 little-endian floating or integer dataset",
+                  path, name);
     } else if ((int32_t)H5Tget_size(t) != elem_bytes) {
         rc = fail(LMI_E_INVALID, "%s/%s: stored element is %d bytes, caller expects %d", path, name,
                   (int)H5Tget_size(t), (int)elem_bytes);

@@ -12,18 +12,21 @@
 //     broadcast to the whole group         :192-193
 // and is checked bit for bit against it (tests/test_gpu_replay.py).
 //
-// Before round 0, replay_groups_kernel (C x R workgroups) lays out every
-// round's groups: the queries with classes[q, r] == c in ascending q.
+// Before round 0 (the GROUPS phase: it needs the classes only, so a stream of
+// batches runs it beside the scan), replay_groups_kernel (C x R workgroups)
+// lays out every round's groups: the queries with classes[q, r] == c in
+// ascending q; replay_thr_kernel resets round 0's rows and thresholds.
 // Layout of one round r (R rounds run in order on one stream):
-//   replay_thr_kernel    per query: thr = max of the merged row; D_r <- (FILL, -1)
 //   replay_group_kernel  per category c (one workgroup) over its group of
 //                        round r; thresholded rounds
 //                        need U = sorted unique union of the relevant
 //                        positions, but only its smallest kr + kl members
 //                        matter (fillers and the |U| < kr test), found by
 //                        repeated block-wide minimum selection
-//   replay_merge_kernel  per query: stable insertion sort of hstack(F, D_r)
-// followed by replay_out_kernel (ids through pos_to_id, uint32).
+//   replay_merge_kernel  per element of hstack(F, D_r): its stable rank; it
+//                        also resets the next round's rows and writes its
+//                        thresholds, and the last merge writes the answer
+//                        (ids through pos_to_id, uint32).
 #include "lmi_common.hpp"
 
 #include <type_traits>
@@ -626,7 +629,11 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
                                                           const int32_t* __restrict__ dr_p,
                                                           double* __restrict__ thr_next,
                                                           double* __restrict__ drd_next,
-                                                          int32_t* __restrict__ drp_next) {
+                                                          int32_t* __restrict__ drp_next,
+                                                          const int64_t* __restrict__ pos_to_id,
+                                                          int64_t n_total, double* __restrict__ dists,
+                                                          uint32_t* __restrict__ anns,
+                                                          int32_t* __restrict__ status) {
     // fused prologue of the next round (replay_thr_kernel's mode 2): its row
     // buffers (the other pair) reset to (10000, -1), and its threshold
     // max(F_q) written by the thread that places F's last element
@@ -640,9 +647,24 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
         drd_next[(size_t)q * kr + j] = kFill;
         drp_next[(size_t)q * kr + j] = -1;
     }
+    // the last merge (dists non-null) writes the answer itself: positions ->
+    // ids through pos_to_id, uint32 (one launch less than a separate output pass)
+    auto put = [&](int at, double v, int32_t p) {
+        if (dists) {
+            int64_t id = 0;
+            if (p >= 0) {
+                if (p < n_total) id = pos_to_id[p];
+                else atomicOr(status, 4);
+            }
+            dists[(size_t)q * wn + at] = v;
+            anns[(size_t)q * wn + at] = (uint32_t)id;  // numpy int64 -> uint32 assignment
+        } else {
+            Fd_out[(size_t)q * fs + at] = v;
+            Fp_out[(size_t)q * fs + at] = p;
+        }
+    };
     if (first) {
-        Fd_out[(size_t)q * fs + j] = dd[j];
-        Fp_out[(size_t)q * fs + j] = dr_p[(size_t)q * kr + j];
+        put(j, dd[j], dr_p[(size_t)q * kr + j]);
         if (thr_next && j == 0) {  // round 0's row need not be ascending (the <k quirk)
             double m = dd[0];
             for (int i = 1; i < kr; ++i) m = fmax(m, dd[i]);
@@ -660,135 +682,8 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
         const double di = dd[i];
         rank += (di < dj || (di == dj && wF + i < j)) ? 1 : 0;
     }
-    if (rank < wn) {
-        Fd_out[(size_t)q * fs + rank] = dj;
-        Fp_out[(size_t)q * fs + rank] = j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF];
-    }
+    if (rank < wn) put(rank, dj, j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF]);
     if (thr_next && rank == wn - 1) thr_next[q] = dj;  // the merged row is ascending
-}
-
-// The merge of one query (LearnedIndex.py:82-97, replay_merge_kernel's
-// arithmetic) by one thread, its row in registers: the first wn of the stable
-// argsort of hstack(F_q, D_q) (first: F = D_q), written into Fd_out / Fp_out
-// or, with `out` (the last round), straight to the answer (positions mapped to
-// ids).  Returns the merged row's largest kept value (its threshold, :71-72).
-struct MergeRow {
-    int32_t kr, fs, wF, wn, first;
-    const double* Fd;
-    const int32_t* Fp;
-    double* Fd_out;
-    int32_t* Fp_out;
-    const double* dr_d;  // this query's round rows
-    const int32_t* dr_p;
-};
-constexpr int kMergeRegs = 20;  // hstack(F, D) widths a thread holds in registers (k = k_round = 10)
-
-template <bool OUT>
-__device__ inline double merge_row(const MergeRow& m, int q, const int64_t* pos_to_id, int64_t n_total,
-                                   double* dists, uint32_t* anns, int32_t w, int32_t* status) {
-    const int n = m.first ? m.kr : m.wF + m.kr;
-    double v[kMergeRegs];
-    int32_t pv[kMergeRegs];
-#pragma unroll
-    for (int j = 0; j < kMergeRegs; ++j) {
-        const bool inF = !m.first && j < m.wF;
-        const int jd = m.first ? j : j - m.wF;
-        v[j] = j >= n ? 0.0 : inF ? m.Fd[(size_t)q * m.fs + j] : m.dr_d[(size_t)q * m.kr + jd];
-        pv[j] = j >= n ? -1 : inF ? m.Fp[(size_t)q * m.fs + j] : m.dr_p[(size_t)q * m.kr + jd];
-    }
-    double thr = v[0];
-#pragma unroll
-    for (int j = 0; j < kMergeRegs; ++j) {
-        if (j < n) {  // (no break: the row stays in registers only if the loop unrolls)
-        int rank = j;  // (first: the row as it is, :86 -- round 0's D_0)
-        if (!m.first) {
-            rank = 0;
-#pragma unroll
-            for (int i = 0; i < kMergeRegs; ++i)
-                rank += (i < n && (v[i] < v[j] || (v[i] == v[j] && i < j))) ? 1 : 0;
-        }
-        if (rank < m.wn) {
-            if constexpr (OUT) {
-                int64_t id = 0;
-                if (pv[j] >= 0) {
-                    if (pv[j] < n_total) id = pos_to_id[pv[j]];
-                    else atomicOr(status, 4);
-                }
-                dists[(size_t)q * w + rank] = v[j];
-                anns[(size_t)q * w + rank] = (uint32_t)id;
-            } else {
-                m.Fd_out[(size_t)q * m.fs + rank] = v[j];
-                m.Fp_out[(size_t)q * m.fs + rank] = pv[j];
-            }
-        }
-        // round 0's row need not be ascending (the <k quirk): its maximum; a
-        // merged row is ascending: the value placed last
-        if (m.first) thr = fmax(thr, v[j]);
-        else if (rank == m.wn - 1) thr = v[j];
-        }
-    }
-    return thr;
-}
-
-// Rounds r >= 1 in one launch each (C + 1 workgroups, category c of round r;
-// category C holds the queries whose class is out of range): the workgroup
-// first merges round r - 1 for the queries of its own group (a thread per
-// query, merge_row) -- their thresholds, and round r's rows reset to
-// (10000, -1) -- then runs round r's group (replay_group_body), which reads
-// those thresholds; every query is in exactly one group of a round, so the
-// merge of round r - 1 is split over the workgroups of round r.  One launch
-// instead of replay_merge_kernel + replay_group_kernel.
-__global__ __launch_bounds__(kTG) void replay_round_kernel(RoundArgs a, MergeRow m) {
-    const int c = blockIdx.x;
-    const int g0 = a.gb[2 * c], g1 = a.gb[2 * c + 1];
-    double* thr = const_cast<double*>(a.thr);
-    for (int gi = g0 + threadIdx.x; gi < g1; gi += kTG) {
-        const int q = a.groups[gi];
-        thr[q] = merge_row<false>(m, q, nullptr, 0, nullptr, nullptr, 0, nullptr);
-        for (int j = 0; j < a.kr; ++j) {
-            a.dr_d[(size_t)q * a.kr + j] = kFill;
-            a.dr_p[(size_t)q * a.kr + j] = -1;
-        }
-    }
-    __syncthreads();  // (the group's thresholds and reset rows, within the workgroup)
-    if (c < a.C) replay_group_body(a, c);
-}
-
-// The last round's merge and the answer (replay_merge_kernel +
-// replay_out_kernel), a thread per query.
-__global__ __launch_bounds__(kT) void replay_final_kernel(int32_t nq, MergeRow m,
-                                                          const int64_t* __restrict__ pos_to_id,
-                                                          int64_t n_total, double* __restrict__ dists,
-                                                          uint32_t* __restrict__ anns, int32_t w,
-                                                          int32_t* __restrict__ status) {
-    const int q = blockIdx.x * kT + threadIdx.x;
-    if (q >= nq) return;
-    merge_row<true>(m, q, pos_to_id, n_total, dists, anns, w, status);
-}
-
-__global__ __launch_bounds__(kT) void replay_out_kernel(int32_t nq, int32_t w, int32_t fs,
-                                                        const double* __restrict__ Fd,
-                                                        const int32_t* __restrict__ Fp,
-                                                        const int64_t* __restrict__ pos_to_id,
-                                                        int64_t n_total, double* __restrict__ dists,
-                                                        uint32_t* __restrict__ anns,
-                                                        int32_t* __restrict__ status) {
-    // one thread per output entry (a thread per query walked its w entries
-    // as w dependent load chains: 14 us at 10k x 10)
-    const int64_t t = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (t >= (int64_t)nq * w) return;
-    const int q = (int)(t / w), j = (int)(t - (int64_t)q * w);
-    const int32_t p = Fp[(size_t)q * fs + j];
-    const double dv = Fd[(size_t)q * fs + j];
-    int64_t id = 0;
-    if (p >= 0) {
-        if (p < n_total)
-            id = pos_to_id[p];
-        else
-            atomicOr(status, 4);
-    }
-    dists[t] = dv;
-    anns[t] = (uint32_t)id;  // numpy int64 -> uint32 assignment
 }
 
 struct ReplayWs {
@@ -958,11 +853,6 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         a.status = status;
         return a;
     };
-    // hstack(F, D) of every merge within a thread's registers: each round r
-    // >= 1 is ONE launch (the merge of r - 1 inside round r's groups) and the
-    // last merge writes the answer (replay_round_kernel, replay_final_kernel);
-    // wider rows take the per-element merge kernels
-    const bool fused = k_round <= kMergeRegs && k_final + k_round <= kMergeRegs;
     int cur = 0;  // F lives in buffer cur; a merge writes the other one
     int wF = 0;
     for (int r = 0; r < R; ++r) {
@@ -972,44 +862,21 @@ int lmi::replay_device_impl(const int32_t* classes, int32_t nq, int32_t R, int32
         int32_t* drp = (int32_t*)(ws + s.drp[r & 1]);
         const bool last = r + 1 == R;
         const int wn = (r == 0) ? k_round : std::min(k_final, wF + k_round);
-        if (fused) {
-            if (r == 0) {
-                hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, round_args(0));
-                LMI_LAUNCH_CHECK("replay_group_kernel");
-            }
-            MergeRow m{k_round, fs, wF, wn, r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
-                       (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp};
-            if (last) {
-                hipLaunchKernelGGL(replay_final_kernel, qgrid, dim3(kT), 0, st, nq, m, pos_to_id, n_total,
-                                   dists_out, anns_out, w, status);
-                LMI_LAUNCH_CHECK("replay_final_kernel");
-            } else {
-                hipLaunchKernelGGL(replay_round_kernel, dim3(C + 1), dim3(kTG), 0, st, round_args(r + 1), m);
-                LMI_LAUNCH_CHECK("replay_round_kernel");
-            }
-        } else {
-            hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, round_args(r));
-            LMI_LAUNCH_CHECK("replay_group_kernel");
-            const int n = (r == 0) ? k_round : wF + k_round;
-            const dim3 mgrid((unsigned)(((int64_t)nq * n + kT - 1) / kT));
-            hipLaunchKernelGGL(replay_merge_kernel, mgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
-                               r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
-                               (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp,
-                               last ? nullptr : (double*)(ws + s.thr),
-                               last ? nullptr : (double*)(ws + s.drd[(r + 1) & 1]),
-                               last ? nullptr : (int32_t*)(ws + s.drp[(r + 1) & 1]));
-            LMI_LAUNCH_CHECK("replay_merge_kernel");
-        }
+        hipLaunchKernelGGL(replay_group_kernel, dim3(C), dim3(kTG), 0, st, round_args(r));
+        LMI_LAUNCH_CHECK("replay_group_kernel");
+        const int n = (r == 0) ? k_round : wF + k_round;
+        const dim3 mgrid((unsigned)(((int64_t)nq * n + kT - 1) / kT));
+        // (the last merge writes the answer: w == wn there)
+        hipLaunchKernelGGL(replay_merge_kernel, mgrid, dim3(kT), 0, st, nq, k_round, fs, wF, wn,
+                           r == 0 ? 1 : 0, Fd, Fp, (double*)(ws + s.Fd[cur ^ 1]),
+                           (int32_t*)(ws + s.Fp[cur ^ 1]), drd, drp,
+                           last ? nullptr : (double*)(ws + s.thr),
+                           last ? nullptr : (double*)(ws + s.drd[(r + 1) & 1]),
+                           last ? nullptr : (int32_t*)(ws + s.drp[(r + 1) & 1]), pos_to_id, n_total,
+                           last ? dists_out : nullptr, anns_out, status);
+        LMI_LAUNCH_CHECK("replay_merge_kernel");
         cur ^= 1;
         wF = wn;
-    }
-    if (!fused) {
-        const double* Fd = (const double*)(ws + s.Fd[cur]);
-        const int32_t* Fp = (const int32_t*)(ws + s.Fp[cur]);
-        const dim3 ogrid((unsigned)(((int64_t)nq * w + kT - 1) / kT));
-        hipLaunchKernelGGL(replay_out_kernel, ogrid, dim3(kT), 0, st, nq, w, fs, Fd, Fp, pos_to_id, n_total,
-                           dists_out, anns_out, status);
-        LMI_LAUNCH_CHECK("replay_out_kernel");
     }
     return LMI_OK;
 }

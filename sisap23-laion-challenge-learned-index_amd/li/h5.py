@@ -64,11 +64,12 @@ def dataset_info(path: str, key: str):
     return (int(dims[0]), int(dims[1])), dt.value
 
 
-_STORED = {F16: np.float16, F32: np.float32, F64: np.float64}
+_STORED = {F16: np.float16, F32: np.float32, F64: np.float64, U32: np.uint32, I64: np.int64}
 
 
 def read_dataset(path: str, key: str, row0: int = 0, nrows: int = None, dtype=None) -> np.ndarray:
-    """Rows of a floating dataset [nrows, cols] in its stored type, as
+    """Rows of a dataset [nrows, cols] in its stored type (float16/32/64, or
+    the result files' uint32 knns / int64), as
     np.array(h5py.File(path)[key]) gives them (the fp16 clip768 'emb' stays
     float16: the reference then computes float64 distances, utils.py:11);
     dtype=np.float32 converts through HDF5 instead (fp16 widened exactly)."""

@@ -164,8 +164,8 @@ def test_device_replay_wide_position_range(use_threshold):
 @pytest.mark.parametrize("k_final,R", [(10, 4), (14, 3), (10, 1)])
 def test_phased_replay_equals_one_call(k_final, R):
     """lmi_replay_device_phase: GROUPS (the classes only; zeroes the status
-    word) then ROUNDS on one workspace = the one-call replay, bit for bit, on
-    the fused rounds (k + k_round <= 20) and on the per-element merges."""
+    word) then ROUNDS on one workspace = the one-call replay = the host
+    replay, bit for bit (R = 1, k_final = k_round and k_final > k_round)."""
     from li import _lib
     classes, d, pos, size, ids = _random_lists(31 + R, nq=500, R=R, C=24, kl=10, tiny=(3,),
                                                empty=(5,))

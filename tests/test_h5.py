@@ -128,3 +128,13 @@ def test_cli_synthetic_build_and_search(tmp_path, monkeypatch, semantics):
         d = h5.read_dataset(str(res / f), "dists")
         if "buck=4" in f:  # merged rounds are a stable sort; a search_single row need not be
             assert np.all(np.diff(d, axis=1) >= 0)  # (its <k quirk writes 10000 mid-row)
+
+
+def test_result_knns_read_back_in_their_stored_type(tmp_path):
+    anns = np.arange(60, dtype=np.uint32).reshape(6, 10) * 7
+    dists = np.sort(np.random.default_rng(1).random((6, 10)), axis=1)
+    dst = tmp_path / "r.h5"
+    store_results(str(dst), "Learned-index", "pca96v2", dists, anns, 1.0, 0.5, "x", "10M")
+    got = h5.read_dataset(str(dst), "knns")
+    assert got.dtype == np.uint32
+    np.testing.assert_array_equal(got, anns)
