@@ -1,7 +1,9 @@
 """Device replay (K4) timing on bench-shaped random lists: 10k queries, R=4,
 122 buckets of skewed popularity, k=10; torch events around lmi_replay_device.
 (The round-2 phase study's LMI_REPLAY_ABL stops are no longer in the library;
-profiles/r02_replay_phases.txt keeps its numbers.)"""
+profiles/r02_replay_phases.txt keeps its numbers.)  Times the whole replay and
+its ROUNDS phase alone (the part a batch stream's finish stage runs); an A/B of
+two builds: LMI_LIB_NAME=<other .so>."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "sisap23-laion-challenge-learned-index_amd"))
@@ -58,16 +60,23 @@ else:
     classes, d, pos, size, ids = _random_lists(3, nq=10000, R=4, C=122, kl=10)
     args = [torch.from_numpy(x).to(dev) for x in (classes, d, pos)]
     bsz, p2id = torch.from_numpy(size).to(dev), torch.from_numpy(ids).to(dev)
-for _ in (0,):
-    fn = lambda: replay_device(*args, k_round=10, k_final=10, bucket_size=bsz, pos_to_id=p2id,
-                               use_threshold=True)
+from li import _lib  # noqa: E402
+nq, R = args[0].shape
+w = torch.empty(1 << 26, dtype=torch.uint8, device=dev)
+out = (torch.empty((nq, 10), dtype=torch.float64, device=dev), torch.empty((nq, 10), dtype=torch.int32, device=dev),
+       torch.zeros((1,), dtype=torch.int32, device=dev))
+kw = dict(k_round=10, k_final=10, bucket_size=bsz, pos_to_id=p2id, use_threshold=True, out=out, ws=w)
+replay_device(args[0], None, None, phases=_lib.LMI_REPLAY_PHASE_GROUPS, k_list=args[1].shape[2], **kw)
+for name, fn in (("whole replay (groups + rounds)", lambda: replay_device(*args, **kw)),
+                 ("rounds only (the finish stage's part)",
+                  lambda: replay_device(*args, phases=_lib.LMI_REPLAY_PHASE_ROUNDS, **kw))):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(20):
+    for _ in range(50):
         fn()
     e1.record()
     torch.cuda.synchronize()
-    print(f"replay (per-round launches): {e0.elapsed_time(e1) / 20 * 1e3:8.1f} us", flush=True)
+    print(f"[{_lib.LIB_NAME}] {name}: {e0.elapsed_time(e1) / 50 * 1e3:8.1f} us", flush=True)
