@@ -139,6 +139,11 @@ inline int take_phases(int32_t& qmode) {
 // pair in the outputs (default k); prefill: write (+inf, -1) over all R*ldo
 // entries first (the first pass).  seed_r0: LMI_Q_SEED_ROUND0 (pairs r >= 1
 // start from the bound of pair (q, 0), + seed_margin in distance).
+// out_bound (nullable, [nq*R] float; k <= 15 on scan v3, kl = 15): the float64
+// mode's band lists -- the scan's filter widened by seed_margin (2 eps), every
+// pair's first 15 entries, and out_bound[pair] a distance such that each row
+// of the shard the list does not hold failed the widened filter or has
+// d32 >= it (chunk_merge_band_kernel).
 // The scans of the wide path (k > 16, bucket_topk_wide): mode 1 writes every
 // (pair, chunk part) list as that part's own top-15 (no global bound); mode 2
 // collects every row within the pair's bound bound_ord[pair id] (a distance
@@ -160,7 +165,9 @@ int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int3
                      size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g = nullptr,
                      int32_t ldo = 0, bool prefill = true, bool seed_r0 = false,
                      float seed_margin = 0.0f, int phases = kPhaseAll,
-                     const WideScan* wide = nullptr);
+                     const WideScan* wide = nullptr, float* out_bound = nullptr);
+// scan v3 serves this index and query class (the float64 mode's band lists)
+bool band_capable(const lmi_index_desc* idx, int qmode);
 size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
                             int32_t qmode, bool lo = false);
 // k > LMI_MAX_K: passes_of() passes of kp-entry lists; bucket_topk_passes fills

@@ -56,6 +56,8 @@ struct RefineArgs {
     const float* ld;       // [nq][R][kl] d32 ascending
     const int32_t* lrow;   // [nq][R][kl] local rows (-1 empty)
     const int32_t* lpos;   // [nq][R][kl] global positions
+    const float* lbound;   // [nq*R] band lists: bound of the unlisted rows (null: plain lists)
+    int32_t seeded;        // LMI_Q_SEED_ROUND0 (band lists: rounds r >= 1 need rows under round 0's bound only)
     double* out_d;         // [nq][R][k]
     int32_t* out_pos;
     int32_t* failed;       // [nq*R] queued pairs
@@ -258,7 +260,28 @@ __global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void
     double* od = a.out_d + (size_t)p * k;
     int32_t* op = a.out_pos + (size_t)p * k;
     int m;
-    if (n_valid < kl) {
+    if (a.lbound) {
+        // band lists: an unlisted row failed the scan's filter (d32 past the
+        // pair's k-th + 2 eps) or has d32 >= lbound (+inf: no row was
+        // dropped); the list holds the band unless lbound lies in it
+        const double t = n_valid >= k ? (double)a.ld[li + k - 1] + 2.0 * a.eps : __builtin_inf();
+        // (LMI_Q_SEED_ROUND0, rounds r >= 1: the thresholded replay reads only
+        // entries with d64 below round 0's final threshold D0 <= d32 10th of
+        // pair (q, 0) + eps, i.e. rows with d32 < that + 2 eps; the list must
+        // hold those alone -- the seed's own premise)
+        double lim = t;
+        if (a.seeded && p % a.R != 0)
+            lim = fmin(lim, (double)a.ld[(size_t)(p - p % a.R) * kl + k - 1] + 2.0 * a.eps);
+        const float ub = a.lbound[p];
+        if (ub != __builtin_inff() && (double)ub <= lim) {
+            if (lane == 0) a.failed[atomicAdd(a.n_failed, 1)] = (int32_t)p;
+            return;
+        }
+        m = 0;
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s)
+            m += __popcll(__ballot(64 * s + lane < kl && rj[s] >= 0 && (double)dj[s] <= t));
+    } else if (n_valid < kl) {
         m = n_valid;  // the shard's whole bucket is listed
     } else {
         const double t = (double)a.ld[li + k - 1] + 2.0 * a.eps;
@@ -413,7 +436,7 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
 }
 
 struct RefineWs {
-    size_t scan, ld, lrow, lpos, failed, nfailed, total;
+    size_t scan, ld, lrow, lpos, lbound, failed, nfailed, total;
     int kl;       // scan list length refined (>= k + 5, or 15 for k <= 10)
     int passes;   // 0: one scan of kl entries, else lower-bound passes
 };
@@ -438,6 +461,7 @@ RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     w.ld = take(P * w.kl * 4);
     w.lrow = take(P * w.kl * 4);
     w.lpos = take(P * w.kl * 4);
+    w.lbound = take(P * 4);
     w.failed = take(P * 4);
     w.nfailed = take(256);
     w.scan = take(w.passes ? wide_ws_bytes(idx, nq, R, k + 5, qmode, w.kl)
@@ -844,6 +868,12 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     a.ld = (const float*)(ws + w.ld);
     a.lrow = (const int32_t*)(ws + w.lrow);
     a.lpos = (const int32_t*)(ws + w.lpos);
+    // k <= 10 on scan v3: the band lists (10-entry lane lists, the filter
+    // widened by 2 eps, 15 entries + a bound per pair) instead of 15-entry
+    // lane lists
+    const bool band = !w.passes && band_capable(idx, qmode);
+    a.lbound = band ? (const float*)(ws + w.lbound) : nullptr;
+    a.seeded = seed ? 1 : 0;
     a.out_d = out_d;
     a.out_pos = out_pos;
     a.failed = (int32_t*)(ws + w.failed);
@@ -861,7 +891,7 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
         : bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
                            (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
                            ws + w.scan, w.total - w.scan, s, nullptr, 0, true, seed,
-                           (float)(2.0 * eps), phases);
+                           (float)(2.0 * eps), phases, nullptr, band ? (float*)(ws + w.lbound) : nullptr);
     if (rc != LMI_OK) return rc;
     if (!(phases & kPhaseMerge)) return LMI_OK;
     const int64_t P = (int64_t)nq * R;

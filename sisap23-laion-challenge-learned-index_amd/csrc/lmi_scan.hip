@@ -60,9 +60,9 @@ namespace {
 // launch instead of one per array): array f gets value v[f] in words
 // [row * per_q[f], (row + 1) * per_q[f]) from the wave of query `row`.
 struct PrepFills {
-    uint32_t* p[4];
-    uint32_t v[4];
-    int32_t per_q[4];
+    uint32_t* p[5];
+    uint32_t v[5];
+    int32_t per_q[5];
     int32_t n;
 };
 
@@ -643,6 +643,93 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
     }
 }
 
+// The float64 mode's band lists (scan3_kernel MODE 3): per pair, its parts'
+// 15-entry lists merged to the first 15 by (distance, global position), and
+// out_bound[pair id] = the smallest of the parts' bounds and of the merge's
+// 16th distance: every row of the pair's shard not in its list either failed
+// the scan's widened filter or has d32 >= out_bound (refine_kernel falls back
+// to the whole shard when that bound enters the float64 band).
+__global__ __launch_bounds__(64) void chunk_merge_band_kernel(
+    const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
+    const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
+    const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
+    int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, float* __restrict__ out_bound,
+    int64_t n_rows, int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask, int32_t S) {
+    constexpr int NB = kBandSlot, KB = kBandSlot - 1;
+    const int pp = blockIdx.x * 64 + threadIdx.x;
+    if (pp >= P) return;
+    const int c = pair_bucket[pp];
+    if (c < 0) return;
+    const int nch_c = chunk_first[c + 1] - chunk_first[c];
+    uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
+    const int nch = nch_c + (S - 1) * __popc(sm);
+    const int X = max_chunks / S;
+    int part = S, bit = 0;
+    auto slot_of = [&](int j) {  // (chunk_merge_kernel's order)
+        if (j < nch_c) return j;
+        if (part == S) {
+            bit = __builtin_ctz(sm);
+            sm &= sm - 1u;
+            part = 1;
+        }
+        return (part++) * X + bit;
+    };
+    uint64_t M[NB];
+    int32_t W[NB];
+    list_clear<NB>(M);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) W[i] = -1;
+    uint32_t ub = 0xffffffffu;
+    uint64_t Kn[NB];
+    {
+        const uint64_t* src = partial + (size_t)pp * max_chunks * NB;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) Kn[i] = nch > 0 ? src[i] : kEmptyKey;
+    }
+    for (int j = 0; j < nch; ++j) {
+        uint64_t K[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) K[i] = Kn[i];
+        if (j + 1 < nch) {
+            const uint64_t* src = partial + ((size_t)pp * max_chunks + slot_of(j + 1)) * NB;
+#pragma unroll
+            for (int i = 0; i < NB; ++i) Kn[i] = src[i];
+        }
+        ub = std::min(ub, (uint32_t)(K[KB] >> 32));
+        int32_t g[KB];
+#pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            const uint32_t lp = (uint32_t)K[i];
+            // (entries past the list's 16th distance only raise nothing: the
+            // 16th bounds them)
+            const bool live = K[i] != kEmptyKey && (K[i] >> 32) <= (M[NB - 1] >> 32);
+            const bool ok = lp < (uint32_t)n_rows;
+            if (live && !ok) atomicOr(status, LMI_STATUS_INTERNAL);
+            g[i] = (live && ok) ? gpos[lp] : -1;
+        }
+#pragma unroll
+        for (int i = 0; i < KB; ++i) {
+            if (g[i] < 0) continue;
+            const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
+            if (key < M[NB - 1]) list_insert_pair<NB>(M, W, key, (int32_t)(uint32_t)K[i]);
+        }
+    }
+    ub = std::min(ub, (uint32_t)(M[NB - 1] >> 32));
+    const int pid = pair_q[pp];
+    const size_t o = (size_t)pid * ldo;
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+        if (i < k) {
+            const uint64_t key = M[i];
+            const bool empty = key == kEmptyKey;
+            out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
+            out_pos[o + i] = empty ? -1 : (int32_t)(uint32_t)key;
+            out_row[o + i] = empty ? -1 : W[i];
+        }
+    }
+    out_bound[pid] = ub == 0xffffffffu ? __builtin_inff() : ord2f(ub);
+}
+
 // ---------------------------------------------------------------------------
 // k > 16: lower-bound passes
 // ---------------------------------------------------------------------------
@@ -1051,7 +1138,9 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));
     // (x S: the other parts of tail-split chunks, slot s * max_chunks + j)
-    w.partial = take(P * (size_t)(S * std::max(idx->max_chunks, 1)) * KL * sizeof(uint64_t));
+    // (15-entry lists: room for the float64 mode's band slots, kBandSlot)
+    w.partial = take(P * (size_t)(S * std::max(idx->max_chunks, 1)) * (KL == 15 ? kBandSlot : KL) *
+                     sizeof(uint64_t));
     w.ext_off = take(((size_t)idx->n_buckets + 1 + 2 * S * (size_t)kGroups * kSplitMaxK) * 8);
     w.split_mask = take(P * 4);
     w.thr_g = take(P * sizeof(uint64_t));
@@ -1066,6 +1155,8 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
 }
 
 }  // namespace
+
+bool band_capable(const lmi_index_desc* idx, int qmode) { return v3_capable(idx, qmode); }
 
 int split_parts() {
     return std::max(2, std::min(kSplitMaxParts, env_config().scan_split_parts));
@@ -1227,7 +1318,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                           int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                           size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g, int32_t ldo,
                           bool prefill, bool seed_r0, float seed_margin, int phases,
-                          const WideScan* wide) {
+                          const WideScan* wide, float* out_bound) {
     const bool do_plan = phases & kPhasePlan, do_scan = phases & kPhaseScan,
                do_merge = phases & kPhaseMerge;
     using namespace lmi;
@@ -1264,6 +1355,19 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     // seed), split_mask = 0, the per-pair bounds thr_g = all ones (scan v2/v3)
     PrepFills fills{};
     const bool seed_plan = seed_r0 && w.use_v3 && !(lo_g != nullptr) && R > 1;
+    // the float64 mode's band lists (out_bound: every pair's bound of its
+    // unlisted rows, +inf until the merge writes it)
+    const bool band = out_bound != nullptr;
+    if (band && !(w.use_v3 && KL == 15 && lo_g == nullptr && wide == nullptr)) {
+        set_error("internal: band lists need scan v3 with 15-entry lists");
+        return LMI_E_INVALID;
+    }
+    if (band) {
+        fills.p[fills.n] = reinterpret_cast<uint32_t*>(out_bound);
+        fills.v[fills.n] = 0x7f800000u;
+        fills.per_q[fills.n] = R;
+        ++fills.n;
+    }
     if (idx->n_rows > 0) {
         auto add = [&](void* ptr, uint32_t v, int per_q) {
             fills.p[fills.n] = reinterpret_cast<uint32_t*>(ptr);
@@ -1413,6 +1517,9 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         b.lo_g = lo_g;
         b.pair_pos = seed_pos;
         b.seed_margin = seed_margin;
+        // (MODE 3: 2 eps = the seed margin of the float64 mode, rounded up,
+        // + 2^-22 for the rounding of bound + band, distances being < 4)
+        b.band = band ? seed_margin * (1.0f + 0x1p-20f) + 0x1p-22f : 0.0f;
         b.ng = ng;
         b.lag = std::max(0, std::min(3, env_config().scan_lag));
         // (thr_g was reset by prep)
@@ -1440,6 +1547,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
             }
             rc = launch_scan3_v<15, 0, true>(b, s);
         }
+        else if (w.use_v3 && band)
+            rc = launch_scan3_v<10, 0, false, 3>(b, s);
         else if (w.use_v3)
             rc = (KL == 10) ? launch_scan3<10>(b, s) : launch_scan3<15>(b, s);
         else
@@ -1467,6 +1576,13 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     if (!do_merge) return LMI_OK;
 
     const int grid = (P + 63) / 64;
+    if (band) {
+        hipLaunchKernelGGL(chunk_merge_band_kernel, dim3(grid), dim3(64), 0, s, a.partial, a.max_chunks,
+                           pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo, out_d, out_pos,
+                           out_row, out_bound, idx->n_rows, status, split_mask, w.split_s);
+        LMI_LAUNCH_CHECK("chunk_merge_band_kernel");
+        return LMI_OK;
+    }
 #define LMI_CM(KLV, ROWSV)                                                                         \
     hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
                        a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo,  \

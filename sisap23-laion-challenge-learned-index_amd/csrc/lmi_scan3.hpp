@@ -294,10 +294,16 @@ __device__ __forceinline__ uint32_t opaque_u(uint32_t x) {
 // exchanged or published), the rows behind the wide path's per-pair bound;
 // 2 collect -- every row of a pair within its fixed bound (thr_g, set by the
 // plan) is appended to the pair's candidate buffer (Scan2Args::cand), no lists.
+// MODE 3 (the float64 mode's band lists, KL = 10): the product scan with the
+// filter widened by Scan2Args::band (2 eps) and, per (pair, chunk part), the
+// first 15 of the two lanes' lists plus a bound below which every unlisted
+// row of the part that passed the filter lies (kBandSlot entries, see
+// chunk_merge_band_kernel).
 template <int KL, int ABL = 0, bool LO = false, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     using namespace v3;
     static_assert(MODE == 0 || (ABL == 0 && !LO), "the wide modes are product variants");
+    static_assert(MODE != 3 || KL == 10, "band lists are built from 10-entry lane lists");
     // diagnostic builds only (results wrong for ABL != 0): 1 no insertion,
     // 2 DMA + barriers only, 3 no DMA, 4 no DMA and no insertion, 5 no DMA and
     // no epilogue, 6 = 5 without barriers, 7 event counters, 14 no DMA wait,
@@ -518,7 +524,12 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             const int vr = nrows - eb * 32 - 4 * hh;  // valid rows past this lane's offset
             thr = std::min(thr, xg_carry);
             xg_carry = 0xffffffffu;
-            const float bound = key_dist_bound((uint64_t)thr << 32);
+            // (MODE 3: rows up to 2 eps past the bound pass the filter, so a
+            // row the band lists do not hold lies above the pair's d32 k-th
+            // + 2 eps or at / above the part's bound; the lane lists and the
+            // bounds published stay the plain k-th)
+            float bound = key_dist_bound((uint64_t)thr << 32);
+            if constexpr (MODE == 3) bound += a.band;
             // the filter: a candidate mask, one bit per register, register 0
             // in bit 15 (mask = 2 mask + ok); only the chunk's last block
             // checks the row count
@@ -803,7 +814,38 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
         __syncthreads();  // every wave's DMA drained (the tail waited vmcnt(0))
 
         // ---- merge the two partial lists of each query (lanes col, col+32) ----
-        if (MODE != 2 && h == 0 && live) {
+        if (MODE == 3 && h == 0 && live) {
+            // the union's first 15 by a two-pointer merge over the two LDS
+            // lists (no register list: the kernel has no VGPR to spare) and
+            // the part's bound: every unlisted row that passed the filter was
+            // dropped by its lane (d >= that lane's 10th) or is the union's
+            // 16th or later
+            const uint32_t pb = lbase + 32 * LSTR;
+            uint64_t x = lds_get_u64(lbase), y = lds_get_u64(pb);
+            int ia = 0, ib = 0;
+            uint64_t* out = a.partial + ((size_t)pp * a.max_chunks + tile.chunk) * kBandSlot;
+            uint64_t tenth = kEmptyKey;
+#pragma unroll 1
+            for (int o = 0; o < kBandSlot - 1; ++o) {
+                const bool ta = x <= y;
+                const uint64_t v = ta ? x : y;
+                out[o] = v;
+                if (o == KL - 1) tenth = v;
+                if (ta) {
+                    ++ia;
+                    x = ia < KL ? lds_get_u64(lbase + (uint32_t)ia * ES) : kEmptyKey;
+                } else {
+                    ++ib;
+                    y = ib < KL ? lds_get_u64(pb + (uint32_t)ib * ES) : kEmptyKey;
+                }
+            }
+            const uint32_t l9 = (uint32_t)(lds_get_u64(lbase + (KL - 1) * ES) >> 32);
+            const uint32_t p9 = (uint32_t)(lds_get_u64(pb + (KL - 1) * ES) >> 32);
+            const uint32_t ub = std::min(std::min(l9, p9), (uint32_t)((x <= y ? x : y) >> 32));
+            out[kBandSlot - 1] = ((uint64_t)ub << 32) | 0xffffffffu;
+            if (tenth != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)tenth);
+        }
+        if (MODE != 2 && MODE != 3 && h == 0 && live) {
             uint64_t L[KL], P[KL];
             list_load<KL, 0, ES>(lbase, L);
             list_load<KL, 32 * LSTR, ES>(lbase, P);

@@ -104,6 +104,10 @@ constexpr size_t lds_bytes() {
 }
 }  // namespace v2
 
+// the float64 mode's band lists (scan3_kernel MODE 3): 15 entries + a bound
+// per (pair, chunk part)
+constexpr int kBandSlot = 16;
+
 struct Scan2Args {
     const _Float16* corpus;
     const float* inv_norm;
@@ -125,6 +129,7 @@ struct Scan2Args {
     const unsigned long long* lo_g;  // LO: [nq*R] lower-bound key (d, gpos) per pair id
     const int32_t* pair_pos;    // LMI_Q_SEED_ROUND0: [P] grouped position of the pair's (q, 0), -1 if none; else null
     float seed_margin;          //   (distance added to the seed: 2 eps in the float64 mode)
+    float band;                 // MODE 3 (the float64 mode's band lists): distance added to the filter bound
     unsigned long long* dbg;    // diagnostic counters of the ABL != 0 variants (lmi_scan_abl.hip); null
     // collect mode (k > 16, scan3_kernel MODE 2): every row of a pair within
     // its fixed bound goes to cand[pp * cap + i], i from ccount[pp] (grouped

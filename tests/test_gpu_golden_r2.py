@@ -116,7 +116,9 @@ def test_f64_lists_match_oracle(seed, mode, R):
 
 def test_f64_fallback_path_is_exact():
     """eps so large that every (query, probe) band overflows its list: every
-    pair takes the whole-bucket float64 path, with the same results."""
+    pair takes the whole-bucket float64 path, with the same results.  (The
+    band lists hold 15 entries and a bound of the rows they drop: a pair falls
+    back when its bucket has more than 15 rows, the 16th being in the band.)"""
     from li.index import bucket_topk_f64
     w = workloads.clustered(n=3000, nq=96, C=8, seed=404, label_mode="near")
     ix, cls, classes = _index_and_classes(w, 8, 3)
@@ -124,8 +126,37 @@ def test_f64_fallback_path_is_exact():
     d0, p0, _ = bucket_topk_f64(ix, q, cls, 10)
     d1, p1, st, nfb = bucket_topk_f64(ix, q, cls, 10, eps=0.75, fallback_count=True)
     assert int(st.item()) == 0
-    assert nfb == int((ix.bucket_size[classes] >= 15).sum())  # every pair with a full (15-entry) list
+    assert nfb == int((ix.bucket_size[classes] >= 16).sum())
     assert torch.equal(p0, p1) and torch.equal(d0, d1)
+
+
+@pytest.mark.parametrize("copies", [12, 40])
+def test_f64_band_bound_sends_tied_runs_to_the_fallback(copies):
+    """A run of `copies` identical rows (consecutive in their bucket) next to
+    the queries: with 40 copies each scan lane fills its 10-entry list with
+    them, so the bound of the rows the band lists drop lies in the float64
+    band and those pairs take the whole-bucket path; with 12 the list holds
+    the run.  Either way the lists equal the oracle's."""
+    from li.index import bucket_topk_f64
+    w = workloads.clustered(n=3000, nq=64, C=8, seed=407, label_mode="skewed")
+    x = w["x"].astype(np.float16).copy()
+    lab = w["labels"]
+    big = int(np.bincount(lab, minlength=8).argmax())
+    rows = np.nonzero(lab == big)[0]
+    assert rows.size > copies + 50
+    x[rows[20:20 + copies]] = x[rows[20]]
+    q = w["q"].astype(np.float16).copy()
+    q[:32] = x[rows[20]] + np.float16(0.01)
+    w = dict(w, x=x.astype(np.float32), q=q.astype(np.float32))
+    ix, _, _ = _index_and_classes(w, 8, 1)
+    classes = np.full((q.shape[0], 1), big, np.int64)
+    cls = torch.from_numpy(classes.astype(np.int32)).cuda()
+    d, p, st, nfb = bucket_topk_f64(ix, torch.from_numpy(w["q"]).cuda(), cls, 10, fallback_count=True)
+    assert int(st.item()) == 0
+    ref_d, ref_p = O.bucket_lists(lab, x, q, classes, 1, 10, 8)
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-12, tie=TIE64) == 0
+    if copies == 40:
+        assert nfb >= 32
 
 
 def test_f64_shard_merge_equals_single_gpu():
