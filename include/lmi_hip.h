@@ -217,16 +217,21 @@ int lmi_merge_topk(const float* d_in, const int32_t* pos_in, int32_t G, int64_t 
  * sklearn promotes to float64 (utils.py:11, :19; check_pairwise_arrays) and
  * the threshold test (utils.py:23) and the merges (LearnedIndex.py:86-97) see
  * float64 values.  lmi_bucket_topk_f64 returns those float64 lists:
- *   - the fp32 scan keeps the top-KL (KL >= k + 5: 15 for k <= 10) per (query, probe);
+ *   - the fp32 scan keeps 15 entries per (query, probe) for k <= 10 (round 5,
+ *     fp16 scan: the union of 10-entry lane lists with the filter widened by
+ *     2*eps, plus a bound below which no unlisted row lies; otherwise the
+ *     top-KL, KL >= k + 5);
  *   - every list entry within 2*eps of the fp32 k-th distance is recomputed
  *     in float64 from the stored row (sklearn normalize + dot; exact fp16
- *     inputs; idx->corpus64 when set), sorted by (d64, position); with fewer
- *     than KL entries in that band the result is the exact float64 top-k
- *     whenever eps bounds the fp32 error |d32 - d64| for every row: the host
- *     passes a bound derived from d_pad and the MFMA accumulation depth
+ *     inputs; idx->corpus64 when set), sorted by (d64, position); when no
+ *     unlisted row can lie in that band the result is the exact float64
+ *     top-k whenever eps bounds the fp32 error |d32 - d64| for every row: the
+ *     host passes a bound derived from d_pad and the MFMA accumulation depth
  *     (li.index.refine_eps; 2^-16 for the fp16 path at d 768);
- *   - pairs whose band fills the list are recomputed in float64 over their
- *     whole bucket shard (exact, rare: ties or near-ties of > KL-k objects).
+ *   - other pairs are recomputed in float64 over their whole bucket shard
+ *     (exact, rare: ties or near-ties of many objects).
+ * With LMI_Q_SEED_ROUND0 the lists of rounds r >= 1 are exact below round 0's
+ * threshold only (what the thresholded replay reads; k = k_round lists).
  * Same arguments and layout as lmi_bucket_topk; out_d is float64 [nq][R][k]
  * (+inf past the bucket's size), out_pos global positions (-1 past it).
  * 1 <= k <= LMI_MAX_K_F64, d <= 1024; k > 10 lists come from lower-bound
