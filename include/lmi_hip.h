@@ -149,13 +149,16 @@ typedef struct lmi_index_desc {
      * LMI_F16, inv_norm = 1/||that fp16 row||), and the search is exact in two
      * steps (lmi_bucket_topk, _f64, _f64q, k <= LMI_MAX_K; queries as given,
      * float32, rounded inside the call the same way):
-     *   1. the fp16 scan on the rounded rows and queries gives each (query,
-     *      probe)'s approximate k-th distance d~_k; every row's rounded
-     *      distance lies within eps_x of its exact one, eps_x =
-     *      lmi_split_eps(d) (1.0e-3 at d = 768), so the exact top-k lies
-     *      within d~_k + 2 eps_x;
-     *   2. a collect scan gathers every row under that bound, whose exact
-     *      distances are computed in float64 from these rows (or from
+     *   1. an fp16 scan on the rounded rows and queries gives each (query,
+     *      probe) an upper bound B of its approximate k-th distance d~_k (the
+     *      k-th of a per-bucket sample -- each bucket's first chunk_rows rows
+     *      -- for k <= 10, the 15th of sampled chunk lists for k <= 15, the
+     *      k-th of a whole scan for k = 16); every row's rounded distance
+     *      lies within eps_x of its exact one, eps_x = lmi_split_eps(d)
+     *      (1.0e-3 at d = 768), so the exact top-k lies within d~_k + 2 eps_x;
+     *   2. a collect scan gathers every row under B + 2 eps_x; of those (they
+     *      hold the k smallest d~, hence d~_k), the rows within d~_k + 2 eps_x
+     *      get their exact distances in float64 from these rows (or from
      *      corpus64 when set, for the float64 mode) and the query, sorted by
      *      (distance, position) -- rounded to float32 first for the float32
      *      mode -- and the first k kept; a pair with more candidates than the

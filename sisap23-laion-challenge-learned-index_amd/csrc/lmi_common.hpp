@@ -216,6 +216,10 @@ struct XArgs {
     int32_t* failed;
     int32_t* n_failed;
     int32_t* status;
+    // > 0: the candidates are every row under a sampled bound + two_eps; only
+    // those within the k-th smallest d~ + two_eps are re-scored
+    double two_eps;
+    const int32_t* fix;  // [nq*R] pairs without a sampled bound (whole shard), or null
 };
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);

@@ -601,6 +601,7 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     extern __shared__ double x_lds[];
     double* sd = x_lds;
     int32_t* sr = reinterpret_cast<int32_t*>(x_lds + a.cap);
+    __shared__ uint32_t s_nr;
     const int pp = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (a.pair_bucket[pp] < 0) return;
@@ -608,7 +609,8 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     const int64_t P = (int64_t)a.nq * a.R;
     if (p < 0 || p >= P) return;
     const uint32_t n = a.ccount[pp];
-    if (n > (uint32_t)a.cap) {  // the collect buffer overflowed: the whole shard
+    // the collect buffer overflowed, or the pair had no sampled bound: the whole shard
+    if (n > (uint32_t)a.cap || (a.fix && a.fix[p])) {
         if (tid == 0) a.failed[atomicAdd(a.n_failed, 1)] = p;
         return;
     }
@@ -617,28 +619,65 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     double qh[3][4];
     query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
     const uint64_t* src = a.cand + (size_t)pp * a.cap;
-    for (uint32_t j0 = (uint32_t)w * kB; j0 < n; j0 += (kXT / 64) * kB) {
+    const bool band = a.two_eps > 0.0;
+    uint32_t nr = n;  // candidates re-scored
+    if (band) {
+        // every row under a sampled bound + 2 eps: sort the (d~, row) keys,
+        // keep the rows within the k-th smallest d~ + 2 eps (the candidates
+        // hold the k smallest d~, so that is the pair's own k-th)
+        uint64_t* keys = reinterpret_cast<uint64_t*>(sd);
+        uint32_t m = 1;
+        while (m < n) m <<= 1;
+        for (uint32_t i = tid; i < m; i += kXT) keys[i] = i < n ? src[i] : kEmptyKey;
+        if (tid == 0) s_nr = 0u;
+        __syncthreads();
+        for (uint32_t k2 = 2; k2 <= m; k2 <<= 1) {
+            for (uint32_t j = k2 >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < m; i += kXT) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const uint64_t x = keys[i], y = keys[l];
+                        if ((x > y) == ((i & k2) == 0)) {
+                            keys[i] = y;
+                            keys[l] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        const double t = n >= (uint32_t)a.k ? (double)ord2f((uint32_t)(keys[a.k - 1] >> 32)) + a.two_eps
+                                            : __builtin_inf();
+        uint32_t c = 0;
+        for (uint32_t i = tid; i < n; i += kXT) c += (double)ord2f((uint32_t)(keys[i] >> 32)) <= t ? 1u : 0u;
+        atomicAdd(&s_nr, c);
+        __syncthreads();
+        nr = s_nr;  // (a prefix of the sorted keys)
+        for (uint32_t i = tid; i < nr; i += kXT) sr[i] = (int32_t)(uint32_t)keys[i];
+        __syncthreads();
+    }
+    for (uint32_t j0 = (uint32_t)w * kB; j0 < nr; j0 += (kXT / 64) * kB) {
         int32_t r[kB];
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
-            const int64_t x = j0 + b < n ? (int64_t)(uint32_t)src[j0 + b] : -1;
+            const int64_t x = j0 + b < nr ? (band ? (int64_t)sr[j0 + b] : (int64_t)(uint32_t)src[j0 + b]) : -1;
             r[b] = (x < 0 || x >= a.n_rows) ? -1 : (int32_t)x;
-            if (j0 + b < n && r[b] < 0 && lane == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
+            if (j0 + b < nr && r[b] < 0 && lane == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
         }
         double dv[kB];
         rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
         if (lane == 0) {
 #pragma unroll
             for (int b = 0; b < kB; ++b)
-                if (j0 + b < n) {
+                if (j0 + b < nr) {
                     sd[j0 + b] = r[b] >= 0 ? out_value<OUT64>(dv[b]) : __builtin_inf();
                     sr[j0 + b] = r[b] >= 0 ? r[b] : INT32_MAX;
                 }
         }
     }
     uint32_t m = 1;
-    while (m < n) m <<= 1;
-    for (uint32_t i = n + tid; i < m; i += kXT) {
+    while (m < nr) m <<= 1;
+    for (uint32_t i = nr + tid; i < m; i += kXT) {
         sd[i] = __builtin_inf();
         sr[i] = INT32_MAX;
     }
@@ -665,7 +704,7 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     }
     const size_t o = (size_t)p * a.k;
     for (int i = tid; i < a.k; i += kXT) {
-        const bool has = i < (int)n && sr[i] != INT32_MAX;
+        const bool has = i < (int)nr && sr[i] != INT32_MAX;
         x_store<OUT64>(a, o + i, has ? sd[i] : __builtin_inf(), has ? a.gpos[sr[i]] : -1);
     }
 }

@@ -1062,6 +1062,47 @@ __global__ __launch_bounds__(256) void x_bound_kernel(int64_t P, int32_t k, cons
     bound_ord[p] = f2ord(f) + ((double)f < b ? 1u : 0u);
 }
 
+// The split mode's sampled bound (k <= 15): the kw-th distance ordinal of the
+// pair's sampled lists (kth_bound_kernel) + 2 eps, rounded up; all ones (a
+// bucket collected whole) and 0 (no bound: fix[p], the whole shard exactly)
+// stay as they are.
+__global__ __launch_bounds__(256) void x_margin_kernel(int64_t P, double two_eps, uint32_t* __restrict__ bound_ord) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const uint32_t b = bound_ord[p];
+    if (b == 0u || b == 0xffffffffu) return;
+    const double v = (double)ord2f(b) + two_eps;
+    const float f = (float)v;
+    bound_ord[p] = f2ord(f) + ((double)f < v ? 1u : 0u);
+}
+
+// The split mode's sample (k <= 10): a descriptor of 2C buckets over the same
+// rows -- bucket 2c = the first min(n_c, S) rows of bucket c (one chunk),
+// bucket 2c + 1 = the rest (no chunks, never probed) -- so the product scan
+// gives every pair the k-th of its bucket's sample, an upper bound of its own.
+__global__ __launch_bounds__(64) void x_sample_desc_kernel(const int64_t* __restrict__ bucket_off, int32_t C,
+                                                           int64_t S, const int32_t* __restrict__ classes, int32_t P,
+                                                           int64_t* __restrict__ off2, int32_t* __restrict__ cf2,
+                                                           int32_t* __restrict__ classes2) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int32_t nch = 0;
+        for (int c = 0; c < C; ++c) {
+            const int64_t a = bucket_off[c], n = bucket_off[c + 1] - a;
+            off2[2 * c] = a;
+            off2[2 * c + 1] = a + (n < S ? n : S);
+            cf2[2 * c] = nch;
+            nch += n > 0 ? 1 : 0;
+            cf2[2 * c + 1] = nch;
+        }
+        off2[2 * C] = bucket_off[C];
+        cf2[2 * C] = nch;
+    }
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < P; i += gridDim.x * 64) {
+        const int32_t c = classes[i];
+        classes2[i] = c < 0 ? c : (c < C ? 2 * c : 2 * C);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -1621,9 +1662,29 @@ double split_eps(int d_pad) {
 
 namespace {
 struct XWs {
-    size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, region, region_bytes, total;
+    size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
+        classes2, region, region_bytes, total;
     int32_t cap;
 };
+// k <= 10: the k-th of a per-bucket sample (the product scan over
+// x_sample_desc); the device tables are filled by x_sample_desc_kernel
+inline bool x_sample(int k) { return k <= 10; }
+lmi_index_desc x_sample_desc(const lmi_index_desc* idx, const int64_t* off2, const int32_t* cf2) {
+    lmi_index_desc d = *idx;
+    d.n_buckets = 2 * idx->n_buckets;
+    d.bucket_off = off2;
+    d.chunk_first = cf2;
+    d.max_chunks = 1;
+    d.n_chunks = idx->n_buckets;
+    d.chunk_centroid = nullptr;
+    return d;
+}
+// k <= 15: the k-th comes from a sampled bound scan (the wide path's chunk-list
+// scan over two lists per bucket, each the first quarter of its rows), not a
+// whole first scan
+constexpr int kXLists = 2;
+inline bool x_sampled(int k) { return k <= 15; }
+lmi_index_desc bound_desc(const lmi_index_desc* idx, int lists, const int32_t* sub_first);
 
 XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     XWs w{};
@@ -1640,14 +1701,25 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
         return at;
     };
     w.qr = take((size_t)nq * idx->d_pad * 4);
-    w.ld = take(P * k * 4);
-    w.lpos = take(P * k * 4);
+    w.ld = take(P * std::max(k, 15) * 4);
+    w.lpos = take(P * std::max(k, 15) * 4);
+    w.fix = take(P * 4);
+    w.bins = take(P * 4);
+    w.sub_first = take(((size_t)idx->n_buckets + 1) * 4);
+    w.sub_rows = take((size_t)idx->n_buckets * 4);
+    w.sub_take = take((size_t)idx->n_buckets * 4);
+    w.off2 = take(((size_t)2 * idx->n_buckets + 1) * 8);
+    w.cf2 = take(((size_t)2 * idx->n_buckets + 1) * 4);
+    w.classes2 = take(P * 4);
     w.bound = take(P * 4);
     w.ccount = take(P * 4);
     w.cand = take(P * (size_t)cap * 8);
     w.failed = take(P * 4);
     w.nfailed = take(256);
-    w.region_bytes = std::max(ws_layout(idx, nq, R, k, LMI_Q_F16).total, ws_layout(idx, nq, R, 10, LMI_Q_F16).total);
+    const lmi_index_desc bd = bound_desc(idx, kXLists, nullptr);
+    const lmi_index_desc sd = x_sample_desc(idx, nullptr, nullptr);
+    w.region_bytes = std::max({ws_layout(idx, nq, R, k, LMI_Q_F16).total, ws_layout(idx, nq, R, 10, LMI_Q_F16).total,
+                               ws_layout(&bd, nq, R, 15, LMI_Q_F16).total, ws_layout(&sd, nq, R, k, LMI_Q_F16).total});
     w.region = take(w.region_bytes);
     w.total = off;
     return w;
@@ -1689,13 +1761,65 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
                        0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
     LMI_LAUNCH_CHECK("x_round_queries_kernel");
     LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
-    // 1. the fp16 scan on the rounded vectors: every pair's approximate k-th
-    int rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
+    const double two_eps = 2.0 * split_eps(idx->d_pad);
+    const bool sampled = x_sampled(k);
+    int32_t* fix = (int32_t*)(ws + w.fix);
+    int rc;
+    if (x_sample(k)) {
+        // 1. the k-th of every pair's bucket sample (its first chunk_rows
+        //    rows): the product scan over the 2C-bucket sample descriptor,
+        //    then that k-th + 2 eps as the collect bound
+        auto* off2 = (int64_t*)(ws + w.off2);
+        auto* cf2 = (int32_t*)(ws + w.cf2);
+        auto* classes2 = (int32_t*)(ws + w.classes2);
+        hipLaunchKernelGGL(x_sample_desc_kernel, dim3((unsigned)std::min(1024, (P + 63) / 64)), dim3(64), 0, s,
+                           idx->bucket_off, idx->n_buckets, (int64_t)idx->chunk_rows, classes, P, off2, cf2, classes2);
+        LMI_LAUNCH_CHECK("x_sample_desc_kernel");
+        const lmi_index_desc sd = x_sample_desc(idx, off2, cf2);
+        rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, nullptr, status, region,
+                              w.region_bytes, s);
+        if (rc != LMI_OK) return rc;
+        hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld, two_eps,
+                           bound);
+        LMI_LAUNCH_CHECK("x_bound_kernel");
+    } else if (sampled) {
+        // 1. a bound per pair from a sample: the wide path's chunk-list scan
+        //    (two lists per bucket, each scanning the first quarter of its
+        //    rows, every list its part's own top-15), the 15th smallest entry
+        //    (>= the pair's 15th >= its k-th), + 2 eps
+        hipLaunchKernelGGL(wide_init_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, (int64_t)P, 0,
+                           nullptr, nullptr, nullptr, bound, fix);
+        LMI_LAUNCH_CHECK("wide_init_kernel");
+        auto* sub_first = (int32_t*)(ws + w.sub_first);
+        auto* sub_rows = (int32_t*)(ws + w.sub_rows);
+        auto* sub_take = (int32_t*)(ws + w.sub_take);
+        hipLaunchKernelGGL(bound_lists_kernel, dim3(1), dim3(256), 0, s, idx->bucket_off, idx->n_buckets, kXLists,
+                           sub_first, sub_rows, sub_take);
+        LMI_LAUNCH_CHECK("bound_lists_kernel");
+        const lmi_index_desc bd = bound_desc(idx, kXLists, sub_first);
+        auto* bins = (uint32_t*)(ws + w.bins);
+        LMI_TRY(fill_u32(bins, 0xffffffffu, (size_t)P, s));
+        const WideScan m1{1, nullptr, nullptr, nullptr, 0, bins, 1, sub_rows, sub_take};
+        rc = bucket_topk_impl(&bd, qr, nq, idx->d_pad, classes, R, 15, LMI_Q_F16, ld, lpos, nullptr, status, region,
+                              w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhasePlan | kPhaseScan, &m1);
+        if (rc != LMI_OK) return rc;
+        const WsLayout lb = ws_layout(&bd, nq, R, 15, LMI_Q_F16);
+        hipLaunchKernelGGL(kth_bound_kernel, dim3((unsigned)P), dim3(64), 0, s,
+                           (const uint64_t*)(region + lb.partial), lb.split_s * bd.max_chunks, lb.split_s,
+                           (const int32_t*)(region + lb.pair_q), (const int32_t*)(region + lb.pair_bucket), sub_first,
+                           (const uint32_t*)(region + lb.split_mask), P, 15, idx->bucket_off, w.cap, bound, fix);
+        LMI_LAUNCH_CHECK("kth_bound_kernel");
+        hipLaunchKernelGGL(x_margin_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, two_eps, bound);
+        LMI_LAUNCH_CHECK("x_margin_kernel");
+    } else {
+        // 1. the fp16 scan on the rounded vectors: every pair's approximate k-th
+        rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
                               region, w.region_bytes, s);
-    if (rc != LMI_OK) return rc;
-    hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld,
-                       2.0 * split_eps(idx->d_pad), bound);
-    LMI_LAUNCH_CHECK("x_bound_kernel");
+        if (rc != LMI_OK) return rc;
+        hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld, two_eps,
+                           bound);
+        LMI_LAUNCH_CHECK("x_bound_kernel");
+    }
     // 2. every row under the bound (the collect scan, as the wide path's)
     const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
     rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status, region,
@@ -1734,6 +1858,8 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     a.failed = (int32_t*)(ws + w.failed);
     a.n_failed = (int32_t*)(ws + w.nfailed);
     a.status = status;
+    a.two_eps = sampled ? two_eps : 0.0;
+    a.fix = sampled && !x_sample(k) ? fix : nullptr;
     // (pairs whose class is out of range keep the prefill of step 1's prep:
     // the outputs are prefilled here, by pair id, in step 3's own buffers)
     hipLaunchKernelGGL(x_prefill_kernel, dim3((unsigned)(((int64_t)P * k + 255) / 256)), dim3(256), 0, s,

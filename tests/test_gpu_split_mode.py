@@ -35,8 +35,11 @@ def test_split_eps_bound():
 
 
 @pytest.mark.parametrize("mode,seed", [("near", 601), ("dup", 602), ("skewed", 603)])
-@pytest.mark.parametrize("k", [1, 10, 16])
+@pytest.mark.parametrize("k", [1, 10, 12, 16])
 def test_split_lists_match_oracle(mode, seed, k):
+    """k <= 10: the collect bound from the k-th of each bucket's sample (its
+    first chunk); 11-15: from the sampled chunk lists' 15th; 16: from a whole
+    first scan -- the same exact lists."""
     w, x, q = _x(mode, seed)
     C, R = w["C"], 4
     ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
