@@ -334,7 +334,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     // cooperatively, 16 lanes per list, an entry per lane, four lists per
     // wave instruction.  ABL 65: cooperative at KL = 10 too (slower there).
     constexpr bool kCoop = KL > 10 || ABL == 65;
-    constexpr int LS = kCoop ? list_stride<KL>() : KL;  // entries per lane column
+    // entries per lane column (MODE 3: slot KL holds the smallest distance
+    // ordinal the lane dropped -- evicted, or not inserted -- see below)
+    constexpr int LS = kCoop ? list_stride<KL>() : (MODE == 3 ? KL + 1 : KL);
+    static_assert(LS <= list_stride<KL>(), "lane slots beyond the LDS budget");
     constexpr int ES = kCoop ? 8 : 512;                  // bytes between a list's entries
     constexpr uint32_t LSTR = kCoop ? LS * 8 : 8;        // bytes between lanes' lists
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -502,6 +505,7 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             uint64_t E[KL];
             list_clear<KL>(E);
             list_store<KL, 0, ES>(opaque_u(lbase), E);
+            if constexpr (MODE == 3) lds_put_u64_at<KL * ES>(opaque_u(lbase), kEmptyKey);
         }
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         __syncthreads();
@@ -690,12 +694,20 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                         } else {
                             uint64_t L[KL];
                             list_load<KL>(la, L);
+                            // (MODE 3: the distance this candidate drops, the
+                            // list's old KL-th when it is evicted, else its own)
+                            uint32_t drop = (uint32_t)(key >> 32);
                             if (ABL == 64 ? key < L[KL - 1] : (uint32_t)(key >> 32) < (uint32_t)(L[KL - 1] >> 32)) {
+                                if constexpr (MODE == 3) drop = (uint32_t)(L[KL - 1] >> 32);
                                 if (ABL == 64)
                                     list_insert<KL>(L, key);
                                 else
                                     list_insert_hi<KL>(L, key);
                                 list_store<KL>(la, L);
+                            }
+                            if constexpr (MODE == 3) {
+                                const uint64_t dm = lds_get_u64_at<KL * 512>(la);
+                                if ((uint64_t)drop << 32 < dm) lds_put_u64_at<KL * 512>(la, (uint64_t)drop << 32);
                             }
                             thr = std::min(thr, (uint32_t)(L[KL - 1] >> 32));
                         }
@@ -818,8 +830,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             // the union's first 15 by a two-pointer merge over the two LDS
             // lists (no register list: the kernel has no VGPR to spare) and
             // the part's bound: every unlisted row that passed the filter was
-            // dropped by its lane (d >= that lane's 10th) or is the union's
-            // 16th or later
+            // dropped by its lane (d >= the lane's smallest dropped distance)
+            // or is the union's 16th or later
             const uint32_t pb = lbase + 32 * LSTR;
             uint64_t x = lds_get_u64(lbase), y = lds_get_u64(pb);
             int ia = 0, ib = 0;
@@ -839,8 +851,10 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                     y = ib < KL ? lds_get_u64(pb + (uint32_t)ib * ES) : kEmptyKey;
                 }
             }
-            const uint32_t l9 = (uint32_t)(lds_get_u64(lbase + (KL - 1) * ES) >> 32);
-            const uint32_t p9 = (uint32_t)(lds_get_u64(pb + (KL - 1) * ES) >> 32);
+            // (each lane's smallest dropped distance: its 10 entries are the
+            // lane's best, so every other row it met lies at or above it)
+            const uint32_t l9 = (uint32_t)(lds_get_u64(lbase + KL * ES) >> 32);
+            const uint32_t p9 = (uint32_t)(lds_get_u64(pb + KL * ES) >> 32);
             const uint32_t ub = std::min(std::min(l9, p9), (uint32_t)((x <= y ? x : y) >> 32));
             out[kBandSlot - 1] = ((uint64_t)ub << 32) | 0xffffffffu;
             if (tenth != kEmptyKey) atomicMin(&a.thr_g[pp], (unsigned long long)tenth);
