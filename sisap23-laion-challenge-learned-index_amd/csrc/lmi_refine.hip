@@ -63,6 +63,8 @@ struct RefineArgs {
     int32_t* failed;       // [nq*R] queued pairs
     int32_t* n_failed;
     int32_t* status;
+    double* pd;            // sliced fallback partial lists [kFbSlicedPairs][kFbSlices][k] (null: off)
+    int32_t* pg;
 };
 
 __device__ inline double wave_sum_d(double v) {
@@ -361,6 +363,15 @@ ranked:
 // shard (a wave per row, kFbRows rows in flight); lane 0 of every wave keeps
 // the wave's top-k in LDS, thread 0 merges the waves' lists.
 constexpr int kFbK = 256;
+// The sliced fallback (k <= kFbSliceK): each of the first kFbSlicedPairs
+// failed pairs' bucket shard is cut into kFbSlices row slices, every (pair,
+// slice) a 256-thread workgroup item of a fixed grid (a pair's rows run on
+// kFbSlices CUs instead of one), each writing its slice's top-k; then one
+// merge per pair.
+constexpr int kFbSliceK = 16;
+constexpr int kFbSlices = 32;
+constexpr int kFbSlicedPairs = 512;
+constexpr int kFbSliceT = 256;
 template <typename TC, typename TQ>
 __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
     __shared__ double sd[kFbT / 64][kFbK];
@@ -369,7 +380,10 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
     const int nf = *a.n_failed;
     const int k = a.k;
     const int nps = (a.d + 255) / 256;
-    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+    // (the first kFbSlicedPairs failed pairs of k <= kFbSliceK take the
+    // sliced path: fallback_slice_kernel + fallback_merge_kernel)
+    const int f0 = a.pd ? kFbSlicedPairs : 0;
+    for (int f = f0 + blockIdx.x; f < nf; f += gridDim.x) {
         const int64_t p = a.failed[f];
         const int c = a.classes[p];  // classes is [nq][R]: pair p = q*R + r
         const int64_t b0 = a.bucket_off[c], b1 = a.bucket_off[c + 1];
@@ -435,8 +449,130 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
     }
 }
 
+template <typename TC, typename TQ>
+__global__ __launch_bounds__(kFbSliceT) void fallback_slice_kernel(RefineArgs a) {
+    __shared__ double sd[kFbSliceT / 64][kFbSliceK];
+    __shared__ int32_t sp[kFbSliceT / 64][kFbSliceK];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nf = min(*a.n_failed, kFbSlicedPairs);
+    const int k = a.k;
+    const int nps = (a.d + 255) / 256;
+    for (int item = blockIdx.x; item < nf * kFbSlices; item += gridDim.x) {
+        const int f = item / kFbSlices, sl = item - f * kFbSlices;
+        const int64_t p = a.failed[f];
+        const int c = a.classes[p];
+        const int64_t b0 = a.bucket_off[c], n = a.bucket_off[c + 1] - b0;
+        const int64_t r_lo = b0 + n * sl / kFbSlices, r_hi = b0 + n * (sl + 1) / kFbSlices;
+        double qh[3][4];
+        query_hat<TQ, 3>(query_of<TQ>(a, p / a.R), a.d, nps, qh);
+        double* L = sd[w];
+        int32_t* G = sp[w];
+        if (lane == 0)
+            for (int i = 0; i < k; ++i) {
+                L[i] = __builtin_inf();
+                G[i] = INT32_MAX;
+            }
+        for (int64_t r0 = r_lo + (int64_t)w * kB; r0 < r_hi; r0 += (int64_t)(kFbSliceT / 64) * kB) {
+            int32_t r[kB];
+#pragma unroll
+            for (int b = 0; b < kB; ++b) r[b] = r0 + b < r_hi ? (int32_t)(r0 + b) : -1;
+            double dv[kB];
+            bool done = false;
+            if constexpr (sizeof(TC) == 2) {
+                // (the fp16 rows' loads of kB rows in flight together)
+                if (a.d % 4 == 0) {
+                    rows_dist64_f16<3>(rows_of<TC>(a), (size_t)a.d_pad, r, a.d, nps, qh, dv);
+                    done = true;
+                }
+            }
+            if (!done) {
+#pragma unroll
+                for (int b = 0; b < kB; ++b)
+                    dv[b] = row_dist64<TC, 3>(rows_of<TC>(a) + (size_t)(r[b] >= 0 ? r[b] : r_lo) * a.d_pad, a.d, nps,
+                                              qh);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int b = 0; b < kB; ++b) {
+                    if (r[b] < 0) break;
+                    const double x = dv[b];
+                    const int32_t g = a.gpos[r[b]];
+                    if (!lt_dp(x, g, L[k - 1], G[k - 1])) continue;
+                    int i = k - 1;
+                    while (i > 0 && lt_dp(x, g, L[i - 1], G[i - 1])) {
+                        L[i] = L[i - 1];
+                        G[i] = G[i - 1];
+                        --i;
+                    }
+                    L[i] = x;
+                    G[i] = g;
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int head[kFbSliceT / 64] = {};
+            double* od = a.pd + ((size_t)f * kFbSlices + sl) * kFbSliceK;
+            int32_t* og = a.pg + ((size_t)f * kFbSlices + sl) * kFbSliceK;
+            for (int j = 0; j < k; ++j) {
+                int best = 0;
+                for (int v = 1; v < kFbSliceT / 64; ++v)
+                    if (lt_dp(sd[v][head[v]], sp[v][head[v]], sd[best][head[best]], sp[best][head[best]])) best = v;
+                od[j] = sd[best][head[best]];
+                og[j] = sp[best][head[best]];
+                if (head[best] < k - 1) ++head[best];
+                else sd[best][head[best]] = __builtin_inf(), sp[best][head[best]] = INT32_MAX;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// one wave per sliced failed pair: its kFbSlices slice lists (k each, by
+// (d64, position)) merged to the first k
+__global__ __launch_bounds__(64) void fallback_merge_kernel(RefineArgs a) {
+    const int nf = min(*a.n_failed, kFbSlicedPairs);
+    const int k = a.k;
+    const int lane = threadIdx.x;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        const int64_t p = a.failed[f];
+        const double* pd = a.pd + (size_t)f * kFbSlices * kFbSliceK;
+        const int32_t* pg = a.pg + (size_t)f * kFbSlices * kFbSliceK;
+        // lane s < kFbSlices walks slice s; each round the wave's minimum head
+        // is taken (position breaks distance ties, like every merge here)
+        int h = 0;
+        double* od = a.out_d + (size_t)p * k;
+        int32_t* op = a.out_pos + (size_t)p * k;
+        for (int j = 0; j < k; ++j) {
+            const bool has = lane < kFbSlices && h < k;
+            const double x = has ? pd[lane * kFbSliceK + h] : __builtin_inf();
+            const int32_t g = has ? pg[lane * kFbSliceK + h] : INT32_MAX;
+            double bx = x;
+            int32_t bg = g;
+            int bl = lane;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ox = __shfl_xor(bx, off);
+                const int32_t og = __shfl_xor(bg, off);
+                const int ol = __shfl_xor(bl, off);
+                if (lt_dp(ox, og, bx, bg) || (ox == bx && og == bg && ol < bl)) {
+                    bx = ox;
+                    bg = og;
+                    bl = ol;
+                }
+            }
+            if (lane == bl) ++h;
+            if (lane == 0) {
+                const bool empty = bg == INT32_MAX;
+                od[j] = empty ? __builtin_inf() : bx;
+                op[j] = empty ? -1 : bg;
+            }
+        }
+    }
+}
+
 struct RefineWs {
-    size_t scan, ld, lrow, lpos, lbound, failed, nfailed, total;
+    size_t scan, ld, lrow, lpos, lbound, failed, nfailed, pd, pg, total;
     int kl;       // scan list length refined (>= k + 5, or 15 for k <= 10)
     int passes;   // 0: one scan of kl entries, else lower-bound passes
 };
@@ -464,6 +600,8 @@ RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     w.lbound = take(P * 4);
     w.failed = take(P * 4);
     w.nfailed = take(256);
+    w.pd = take((size_t)kFbSlicedPairs * kFbSlices * kFbSliceK * 8);
+    w.pg = take((size_t)kFbSlicedPairs * kFbSlices * kFbSliceK * 4);
     w.scan = take(w.passes ? wide_ws_bytes(idx, nq, R, k + 5, qmode, w.kl)
                            : scan_workspace_bytes(idx, nq, R, w.kl, qmode));
     w.total = off;
@@ -831,7 +969,13 @@ void launch_refine(const RefineArgs& a, dim3 grid, dim3 fgrid, hipStream_t s) {
     else
         hipLaunchKernelGGL((refine_kernel<TC, TQ, kMaxPieces>), grid, dim3(kRefT), 0, s, a);
     // one workgroup per queued pair (the grid strides over the queue; the
-    // queue length is read on the device, usually 0)
+    // queue length is read on the device, usually 0); k <= kFbSliceK: the
+    // first kFbSlicedPairs pairs in row slices over many workgroups instead
+    if (a.pd) {
+        hipLaunchKernelGGL((fallback_slice_kernel<TC, TQ>), dim3(2 * (unsigned)num_cus_ref()), dim3(kFbSliceT), 0,
+                           s, a);
+        hipLaunchKernelGGL(fallback_merge_kernel, dim3((unsigned)num_cus_ref()), dim3(64), 0, s, a);
+    }
     hipLaunchKernelGGL((fallback_kernel<TC, TQ>), fgrid, dim3(kFbT), 0, s, a);
 }
 template <typename TC>
@@ -918,6 +1062,9 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
     a.failed = (int32_t*)(ws + w.failed);
     a.n_failed = (int32_t*)(ws + w.nfailed);
     a.status = status;
+    const bool sliced = k <= kFbSliceK && idx->d <= 3 * 256;  // (the slices hold 3 pieces of a query per lane)
+    a.pd = sliced ? (double*)(ws + w.pd) : nullptr;
+    a.pg = sliced ? (int32_t*)(ws + w.pg) : nullptr;
     if (w.passes && phases != kPhaseAll) {
         set_error("phase flags need k + 5 <= %d (one scan pass)", LMI_MAX_K);
         return LMI_E_UNSUPPORTED;

@@ -114,13 +114,16 @@ def test_f64_lists_match_oracle(seed, mode, R):
     assert nfb <= 2  # the whole-bucket path is for long runs of ties only
 
 
-def test_f64_fallback_path_is_exact():
+@pytest.mark.parametrize("nq", [96, 256])
+def test_f64_fallback_path_is_exact(nq):
     """eps so large that every (query, probe) band overflows its list: every
     pair takes the whole-bucket float64 path, with the same results.  (The
     band lists hold 15 entries and a bound of the rows they drop: a pair falls
-    back when its bucket has more than 15 rows, the 16th being in the band.)"""
+    back when its bucket has more than 15 rows, the 16th being in the band.)
+    The first 512 failed pairs run in row slices over many workgroups, the
+    rest (nq = 256: ~750 pairs) one workgroup each."""
     from li.index import bucket_topk_f64
-    w = workloads.clustered(n=3000, nq=96, C=8, seed=404, label_mode="near")
+    w = workloads.clustered(n=3000, nq=nq, C=8, seed=404, label_mode="near")
     ix, cls, classes = _index_and_classes(w, 8, 3)
     q = torch.from_numpy(w["q"]).cuda()
     d0, p0, _ = bucket_topk_f64(ix, q, cls, 10)
