@@ -486,19 +486,21 @@ def main():
         return bool(t.item())
 
     def kernel_ms(dist):
-        """The scan kernel's mean duration: HIP events the library records on
-        the launch stream around every timed launch, over K eager steps
-        (events recorded into a graph cannot be timed on ROCm; a kernel runs
-        the same whichever way it is launched)."""
+        """The scan kernel's time per step: HIP events the library records on
+        the launch stream around every timed launch, over K eager steps, summed
+        per step (the split mode launches two scans a step; events recorded into
+        a graph cannot be timed on ROCm; a kernel runs the same whichever way it
+        is launched)."""
         lib.lmi_timing_read(None, 0)
         lib.lmi_timing_enable(1)
         for _ in range(args.steps):
             eager_step(dist)
         torch.cuda.synchronize()
         lib.lmi_timing_enable(0)
-        ms = (_lib.C.c_float * max(args.steps, 1))()
-        n_ev = lib.lmi_timing_read(ms, args.steps)
-        return float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
+        cap = 4 * max(args.steps, 1)
+        ms = (_lib.C.c_float * cap)()
+        n_ev = lib.lmi_timing_read(ms, cap)
+        return float(np.sum(list(ms)[:n_ev])) / args.steps if n_ev > 0 else float("nan")
 
     B = len(host_batches)
     scan_stats = {}
@@ -707,9 +709,16 @@ def main():
             torch.distributed.barrier()
         el = time.perf_counter() - t0
         lib.lmi_timing_enable(0)
-        ms = (_lib.C.c_float * max(args.steps, 1))()
-        n_ev = lib.lmi_timing_read(ms, args.steps)
-        kms = float(np.mean(list(ms)[:n_ev])) if n_ev > 0 else float("nan")
+        # (a step may launch more than one scan -- the split mode's sample /
+        # bound scan and its collect scan --: the scan time per step is the
+        # sum of its launches)
+        cap = 4 * max(args.steps, 1)
+        ms = (_lib.C.c_float * cap)()
+        n_ev = lib.lmi_timing_read(ms, cap)
+        kms = float(np.sum(list(ms)[:n_ev])) / args.steps if n_ev > 0 else float("nan")
+        if n_ev > args.steps:
+            scan_stats[dist] = (f"HIP events around every scan launch over K eager steps (lmi_timing): "
+                                f"{n_ev / args.steps:g} launches per step, summed per step")
         step_mode[dist] = "eager"
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64,
