@@ -797,7 +797,7 @@ def main():
             "traffic_source": traffic_src,
             "kernel": "scan3_kernel (lmi_bucket_topk)", "kernel_ms": round(scan_ms, 4),
             "kernel_ms_source": scan_stats.get(args.dist) or
-                                "HIP events around the scan kernel over K eager steps (lmi_timing)",
+                                "HIP events around every scan launch over K eager steps (lmi_timing), summed per step",
             "arithmetic_intensity_flop_per_byte": round(ai, 1),
             "ridge_flop_per_byte": round(F16_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9), 1),
             "algorithmic_bytes": int(byts), "flops": flops,

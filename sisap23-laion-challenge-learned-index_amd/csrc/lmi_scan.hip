@@ -1077,21 +1077,27 @@ __global__ __launch_bounds__(256) void x_margin_kernel(int64_t P, double two_eps
 }
 
 // The split mode's sample (k <= 10): a descriptor of 2C buckets over the same
-// rows -- bucket 2c = the first min(n_c, S) rows of bucket c (one chunk),
-// bucket 2c + 1 = the rest (no chunks, never probed) -- so the product scan
-// gives every pair the k-th of its bucket's sample, an upper bound of its own.
+// rows -- bucket 2c = the first s_c rows of bucket c, s_c = min(n_c,
+// max(chunk_rows, n_c / kXSampleDiv rounded up to 32 rows)), bucket 2c + 1 =
+// the rest (no chunks, never probed) -- so the product scan gives every pair
+// the k-th of its bucket's sample, an upper bound of its own (and the collect
+// then finds about k n_c / s_c <= k kXSampleDiv rows under it, far inside
+// its buffer at any bucket size).
+constexpr int kXSampleDiv = 16;
 __global__ __launch_bounds__(64) void x_sample_desc_kernel(const int64_t* __restrict__ bucket_off, int32_t C,
-                                                           int64_t S, const int32_t* __restrict__ classes, int32_t P,
-                                                           int64_t* __restrict__ off2, int32_t* __restrict__ cf2,
-                                                           int32_t* __restrict__ classes2) {
+                                                           int64_t chunk_rows, const int32_t* __restrict__ classes,
+                                                           int32_t P, int64_t* __restrict__ off2,
+                                                           int32_t* __restrict__ cf2, int32_t* __restrict__ classes2) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         int32_t nch = 0;
         for (int c = 0; c < C; ++c) {
             const int64_t a = bucket_off[c], n = bucket_off[c + 1] - a;
+            const int64_t want = std::max(chunk_rows, (n / kXSampleDiv + 31) / 32 * 32);
+            const int64_t sc = n < want ? n : want;
             off2[2 * c] = a;
-            off2[2 * c + 1] = a + (n < S ? n : S);
+            off2[2 * c + 1] = a + sc;
             cf2[2 * c] = nch;
-            nch += n > 0 ? 1 : 0;
+            nch += (int32_t)((sc + chunk_rows - 1) / chunk_rows);
             cf2[2 * c + 1] = nch;
         }
         off2[2 * C] = bucket_off[C];
@@ -1674,8 +1680,10 @@ lmi_index_desc x_sample_desc(const lmi_index_desc* idx, const int64_t* off2, con
     d.n_buckets = 2 * idx->n_buckets;
     d.bucket_off = off2;
     d.chunk_first = cf2;
-    d.max_chunks = 1;
-    d.n_chunks = idx->n_buckets;
+    // (host-side bounds for the workspace: a sample of at most n_c / 16 + 32
+    // rows beyond one chunk)
+    d.max_chunks = 2 + std::max(idx->max_chunks, 1) / kXSampleDiv;
+    d.n_chunks = idx->n_buckets * d.max_chunks;
     d.chunk_centroid = nullptr;
     return d;
 }
