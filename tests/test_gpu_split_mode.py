@@ -59,6 +59,31 @@ def test_split_lists_match_oracle(mode, seed, k):
                            tie=1e-12) == 0
 
 
+@pytest.mark.parametrize("dist", ["f32", "f64"])
+def test_split_multi_chunk_sample(dist):
+    """Buckets of ~4500 rows at 128-row chunks: each bucket's sample (n_c / 16
+    rows, rounded up to 32, at least one chunk) spans several chunks of the
+    sample descriptor; the lists equal the oracle's."""
+    w, x, q = _x("router", 641, n=9000, nq=96, C=2)
+    C, R = w["C"], 2
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=128, device="cuda")
+    assert int(np.bincount(w["labels"], minlength=C).max()) // 16 > 2 * 128
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    cls = T(classes.astype(np.int32))
+    if dist == "f32":
+        d, p, st = bucket_topk(ix, T(q), cls, 10)
+        ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, R, 10, C)
+        tol = dict(atol=1e-5, tie=1e-6)
+    else:
+        q64 = q.astype(np.float64)
+        d, p, st, nfb = bucket_topk_f64(ix, T(q64), cls, 10, fallback_count=True)
+        assert nfb == 0
+        ref_d, ref_p = O.bucket_lists(w["labels"], x, q64, classes, R, 10, C)
+        tol = dict(atol=1e-12, tie=1e-12)
+    assert int(st.item()) == 0
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), **tol) == 0
+
+
 def test_split_overflow_takes_the_whole_shard():
     """A bucket of 3000 copies of one vector (relative noise 1e-4: one fp16
     value after normalising and rounding, distinct exact distances): every
