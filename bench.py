@@ -433,7 +433,7 @@ def main():
 
     rank, world, local = init_from_env()
     if args.chunk_rows is None:
-        args.chunk_rows = default_chunk_rows(world)
+        args.chunk_rows = default_chunk_rows(world, SCALES[args.scale])
     if world != args.gpus:
         log(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world} (set by the launcher); "
             f"using {world}")

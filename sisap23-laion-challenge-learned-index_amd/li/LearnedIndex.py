@@ -162,15 +162,14 @@ class LearnedIndex(Logger):
         process group, which must be initialised: li.dist.init_from_env).
         Rank g builds slice g of every bucket; search / search_single return
         the whole answer on every rank.  `chunk_rows`: the scan's chunk of a
-        stripe (default li.index.default_chunk_rows(world))."""
+        stripe (default li.index.default_chunk_rows(world, rows) when the
+        index is built)."""
         import torch.distributed as dist
-        from .index import default_chunk_rows
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("use_process_group: torch.distributed is not initialised "
                                "(li.dist.init_from_env)")
         world = dist.get_world_size(group)
-        self._pg = (group, dist.get_rank(group), world,
-                    int(chunk_rows) if chunk_rows else default_chunk_rows(world))
+        self._pg = (group, dist.get_rank(group), world, int(chunk_rows) if chunk_rows else None)
         self._index = self._searcher = self._cache_key = self._trusted = None
         self._cat_written = None
         return self

@@ -37,11 +37,21 @@ DEFAULT_CHUNK_ROWS = 8192
 SPLIT_D_PAD = 768  # the split mode's (storage "f32x") row width: the fp16 scan's
 
 
-def default_chunk_rows(world: int) -> int:
+def default_chunk_rows(world: int, n_rows: Optional[int] = None) -> int:
     """The scan's chunk (rows) for a shard of a `world`-rank index: 8192 on one
     GPU, 4096 on 2-4, 2048 on more, so a 1/world stripe still cuts into enough
-    tiles to fill 256 CUs (DESIGN.md §5 "Chunk size"; tools/gpu_shards.sh)."""
-    return DEFAULT_CHUNK_ROWS if world <= 1 else 4096 if world <= 4 else 2048
+    tiles to fill 256 CUs (DESIGN.md §5 "Chunk size"; tools/gpu_shards.sh);
+    given the index's rows, halved (down to 1024) while a rank's shard would
+    hold fewer than 64 chunks (configs[1], 300K rows: 4096 -- the scan 0.63
+    instead of 0.75 ms, the float64 line +8%, the stream as fast; smaller
+    chunks speed the scan further but add plan and merge work to a launch
+    the host already bounds, profiles/r05aa_300K_chunk_rows.txt)."""
+    c = DEFAULT_CHUNK_ROWS if world <= 1 else 4096 if world <= 4 else 2048
+    if n_rows is not None:
+        per = n_rows / max(int(world), 1)
+        while c > 1024 and per / c < 64:
+            c //= 2
+    return c
 # LMI_Q_SEED_ROUND0 in the thresholded reference replay (LMI_NO_SEED=1: off,
 # for A/B measurements; results are the same either way)
 _SEED_ROUND0 = os.environ.get("LMI_NO_SEED") != "1"
@@ -206,7 +216,7 @@ class DeviceIndex:
     inv_norm32 = None  # 1/||y|| of corpus32 (the general scan's, k > 16 in f32x)
 
     def __init__(self, data, labels, n_buckets: int, *, ids=None, device=None,
-                 storage: str = "auto", chunk_rows: int = DEFAULT_CHUNK_ROWS,
+                 storage: str = "auto", chunk_rows: Optional[int] = None,
                  rank: int = 0, world: int = 1, subcluster: bool = False):
         _lib.load()
         self.device = torch.device(device if device is not None else "cuda")
@@ -231,7 +241,8 @@ class DeviceIndex:
             self._fill(data, gpos, storage)
         self.gpos = torch.from_numpy(gpos.astype(np.int32)).to(self.device)
         self.n_rows = int(gpos.size)
-        self.chunk_rows = int(chunk_rows)
+        # (default: by the index's size and world, default_chunk_rows)
+        self.chunk_rows = int(chunk_rows) if chunk_rows else default_chunk_rows(world, n)
         cf = np.zeros(n_buckets + 1, np.int32)
         lib = _lib.load()
         mx = lib.lmi_plan_chunks(loc_off.ctypes.data, n_buckets, self.chunk_rows, cf.ctypes.data)

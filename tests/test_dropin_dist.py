@@ -30,7 +30,7 @@ def _worker(rank, world, port, out_dir):
     li = LearnedIndex()
     pg = li._proc_group()                 # entered from WORLD_SIZE > 1
     assert pg is not None and pg[1] == rank and pg[2] == world
-    assert pg[3] == (4096 if world <= 4 else 2048)
+    assert pg[3] is None  # (the stripe's chunk: by the index's size, li.index.default_chunk_rows)
     built = None
     if rank == 0:
         torch.manual_seed(7)

@@ -277,3 +277,17 @@ def test_host_copy():
     assert lib.lmi_host_copy(b.ctypes.data, a.ctypes.data, a.nbytes, 0) == 0
     np.testing.assert_array_equal(a, b)
     assert lib.lmi_host_copy(None, a.ctypes.data, 5, 1) == _lib.LMI_E_INVALID
+
+
+def test_default_chunk_rows_by_world_and_size():
+    """8192 / 4096 / 2048 rows by world, halved (to 1024 at least) while a
+    rank's shard would hold fewer than 64 chunks."""
+    from li.index import default_chunk_rows
+    assert [default_chunk_rows(w) for w in (1, 2, 4, 8)] == [8192, 4096, 4096, 2048]
+    assert default_chunk_rows(1, 10_000_000) == 8192
+    assert default_chunk_rows(8, 10_000_000) == 2048
+    assert default_chunk_rows(1, 100_000_000) == 8192
+    assert default_chunk_rows(1, 1_000_000) == 8192
+    assert default_chunk_rows(1, 300_000) == 4096
+    assert default_chunk_rows(1, 100_000) == 1024
+    assert default_chunk_rows(4, 1_000) == 1024
