@@ -307,9 +307,13 @@ STEP_TEXT = {
                                           "+ K3" if a.gpus > 1 else "") + " + replay + D2H of the "
                          "answer of the batch of three launches before (each a captured graph); every "
                          "batch passes every stage, each timed launch answers one batch"),
-    "graph": lambda a: ("hip-graph replay per step: a new host batch staged, then its H2D (inside the "
-                        "step: the next batch is not known before it is staged) + search + D2H of "
-                        "the answer"),
+    "graph": lambda a: ("hip-graph replay per step (GraphedSearch.stream): each batch staged on the "
+                        "host cores into its slot's pinned buffer and uploaded on a copy stream while "
+                        "the previous batch's step runs, its step (router + search + replay + D2H of "
+                        "the answer) enqueued behind it before the previous answer is read"
+                        if not a.no_pipeline else
+                        "hip-graph replay per step: a new host batch staged, then its H2D (inside the "
+                        "step) + search + D2H of the answer"),
     "eager": lambda a: "eager launches (H2D of the host batch + search + D2H)",
 }
 
@@ -411,8 +415,9 @@ def main():
                          "H2D + plan of batch b+2, the scan of b+1 and the merge/replay/D2H of b per "
                          "launch on four streams; DESIGN.md §5)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="one captured graph instead of two (GraphedSearch(pipeline=False)); with "
-                         "a new batch staged per step either way uploads inside the step")
+                    help="one captured graph instead of two (GraphedSearch(pipeline=False)): each "
+                         "batch staged and uploaded inside its step (the default stages batch i + 1 "
+                         "and uploads it beside batch i's step, GraphedSearch.stream)")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager step (every launch from the host) instead of the "
                          "HIP-graph replay of the captured step")
@@ -571,12 +576,17 @@ def main():
         answers = []
 
         def steps(i0, n, keep):
-            o = None
+            # pipelined (the default): batch i + 1 staged and uploaded while
+            # batch i's step runs (GraphedSearch.stream); single: one batch at a time
+            if gs.pipeline and not single:
+                for j, o in enumerate(gs.stream(hb(i, dist) for i in range(i0, i0 + n))):
+                    if keep:
+                        answers.append(((i0 + j) % B, o))
+                return
             for i in range(i0, i0 + n):
                 o = gs.run(*hb(i, dist))
                 if keep:
                     answers.append((i % B, (o[0].copy(), o[1].copy())))
-            return o
 
         steps(1, args.warmup, False)
         if world > 1:
@@ -731,7 +741,8 @@ def main():
     ms_step = el / args.steps * 1e3
     # submission to answer: a streamed batch is answered by the fourth launch
     # that sees it (route, plan, scan, merge/replay), a graph-step batch by its own
-    lat_ms = ms_step * (4 if step_mode.get(args.dist, "").startswith("stream") else 1)
+    lat_ms = ms_step * (4 if step_mode.get(args.dist, "").startswith("stream") else
+                        2 if step_mode.get(args.dist) == "graph" and not args.no_pipeline else 1)
     value = args.nq / (el / args.steps)
     # the other arithmetic, timed the same way (float64: the reference's on
     # float16 data, e.g. the real clip768 'emb'; float32: on float32 data)
@@ -838,7 +849,8 @@ def main():
                                          "bytes_per_rank": int(h2d[2]),
                                          "queries_staged_as": "f16" if q16_exact else "f32",
                                          "in_step": True,
-                                         "overlapped": step_mode.get(args.dist, "").startswith("stream")},
+                                         "overlapped": step_mode.get(args.dist, "").startswith("stream") or (
+                                             step_mode.get(args.dist) == "graph" and not args.no_pipeline)},
         "dist": args.dist,
         "step": STEP_TEXT[step_mode.get(args.dist, "eager").split(" ")[0]](args) +
                 step_mode.get(args.dist, "eager")[len(step_mode.get(args.dist, "eager").split(" ")[0]):] +

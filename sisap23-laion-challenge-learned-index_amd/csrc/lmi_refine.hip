@@ -642,30 +642,62 @@ template <typename TC, int NPS>
 __device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t (&r)[kB], int d, int nps,
                                      const double (&qh)[NPS][4], double zero_eps, double (&out)[kB]) {
     const int lane = threadIdx.x & 63;
-    double v[kB][NPS][4];
-#pragma unroll
-    for (int b = 0; b < kB; ++b)
-#pragma unroll
-        for (int i = 0; i < NPS; ++i) {
-            if (r[b] >= 0 && i < nps) {
-                load_piece<TC>(base + (size_t)r[b] * d_pad, lane + 64 * i, d, v[b][i]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[b][i][j] = 0.0;
-            }
-        }
     double dot[kB], ss[kB];
+    if constexpr (sizeof(TC) == 4) {
+        // float32 rows stay float32 until used (half the registers of doubles)
+        float v[kB][NPS][4];
 #pragma unroll
-    for (int b = 0; b < kB; ++b) {
-        dot[b] = 0.0;
-        ss[b] = 0.0;
+        for (int b = 0; b < kB; ++b)
 #pragma unroll
-        for (int i = 0; i < NPS; ++i)
+            for (int i = 0; i < NPS; ++i) {
+                const int e0 = 4 * (lane + 64 * i);
+                const TC* row = base + (size_t)(r[b] >= 0 ? r[b] : 0) * d_pad;
+                if (r[b] >= 0 && i < nps && e0 + 4 <= d) {
+                    const float4 f = *reinterpret_cast<const float4*>(row + e0);
+                    v[b][i][0] = f.x; v[b][i][1] = f.y; v[b][i][2] = f.z; v[b][i][3] = f.w;
+                } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                dot[b] = fma(qh[i][j], v[b][i][j], dot[b]);
-                ss[b] = fma(v[b][i][j], v[b][i][j], ss[b]);
+                    for (int j = 0; j < 4; ++j) v[b][i][j] = (r[b] >= 0 && i < nps && e0 + j < d) ? row[e0 + j] : 0.0f;
+                }
             }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            dot[b] = 0.0;
+            ss[b] = 0.0;
+#pragma unroll
+            for (int i = 0; i < NPS; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double x = (double)v[b][i][j];
+                    dot[b] = fma(qh[i][j], x, dot[b]);
+                    ss[b] = fma(x, x, ss[b]);
+                }
+        }
+    } else {
+        double v[kB][NPS][4];
+#pragma unroll
+        for (int b = 0; b < kB; ++b)
+#pragma unroll
+            for (int i = 0; i < NPS; ++i) {
+                if (r[b] >= 0 && i < nps) {
+                    load_piece<TC>(base + (size_t)r[b] * d_pad, lane + 64 * i, d, v[b][i]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) v[b][i][j] = 0.0;
+                }
+            }
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            dot[b] = 0.0;
+            ss[b] = 0.0;
+#pragma unroll
+            for (int i = 0; i < NPS; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    dot[b] = fma(qh[i][j], v[b][i][j], dot[b]);
+                    ss[b] = fma(v[b][i][j], v[b][i][j], ss[b]);
+                }
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
@@ -729,6 +761,15 @@ __device__ inline void x_store(const XArgs& a, size_t o, double v, int32_t pos) 
 }
 
 constexpr int kXT = 256;  // x_select: 4 waves on one pair
+constexpr int kXW = 256;  // x_select_wave: the candidates a wave takes (4 per lane)
+
+// the grouped pairs x_select_wave_kernel answers (a wave each): band
+// candidates (every row under a sampled bound + 2 eps), at most kXW of them;
+// x_select_kernel takes the rest (more candidates, whole-scan candidates) and
+// queues the overflowed and unbounded pairs for the fallback
+__device__ inline bool x_wave_pair(const XArgs& a, uint32_t n, int p) {
+    return a.two_eps > 0.0 && n <= (uint32_t)kXW && n <= (uint32_t)a.cap && !(a.fix && a.fix[p]);
+}
 
 // One workgroup per grouped pair of the collect scan: the exact distance of
 // every candidate (a wave per kB rows), a bitonic sort of (distance, row) in
@@ -747,6 +788,7 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     const int64_t P = (int64_t)a.nq * a.R;
     if (p < 0 || p >= P) return;
     const uint32_t n = a.ccount[pp];
+    if (x_wave_pair(a, n, p)) return;  // (x_select_wave_kernel's)
     // the collect buffer overflowed, or the pair had no sampled bound: the whole shard
     if (n > (uint32_t)a.cap || (a.fix && a.fix[p])) {
         if (tid == 0) a.failed[atomicAdd(a.n_failed, 1)] = p;
@@ -847,6 +889,134 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     }
 }
 
+__device__ inline uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// A wave per grouped pair with at most kXW band candidates (x_wave_pair): the
+// same answer as x_select_kernel without its two LDS sorts and barriers.  The
+// lanes hold the (d~, row) keys (4 each); the k-th smallest is found by k
+// wave minima, the keys within it + 2 eps are compacted into the wave's LDS
+// row list (any order), re-scored kB at a time, and the first k by (exact
+// distance, row) are taken by k wave minima -- the (distance, g.index) order,
+// rows ascending with global position inside a bucket shard.
+template <typename TC, typename TQ, bool OUT64>
+__global__ __launch_bounds__(kXT) void x_select_wave_kernel(XArgs a, int32_t n_pairs) {
+    __shared__ int32_t s_rows[kXT / 64][kXW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int pp = blockIdx.x * (kXT / 64) + w;
+    if (pp >= n_pairs || a.pair_bucket[pp] < 0) return;
+    const int p = a.pair_q[pp];
+    const int64_t P = (int64_t)a.nq * a.R;
+    if (p < 0 || p >= P) return;
+    const uint32_t n = a.ccount[pp];
+    if (!x_wave_pair(a, n, p)) return;
+    const uint64_t* src = a.cand + (size_t)pp * a.cap;
+    uint64_t key[4], work[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const uint32_t i = 64u * s + lane;
+        key[s] = i < n ? src[i] : kEmptyKey;
+        work[s] = key[s];
+    }
+    const double zero_eps = OUT64 ? kEps64 : kEps32;
+    const int nps = (a.d + 255) / 256;
+    double qh[3][4];
+    query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
+    const int k = a.k;
+    // the k-th smallest key (keys are distinct: one per row)
+    uint64_t kth = kEmptyKey;
+    for (int r = 0; r < k; ++r) {
+        const uint64_t m = wave_min_u64(std::min(std::min(work[0], work[1]), std::min(work[2], work[3])));
+        kth = m;
+        if (m == kEmptyKey) break;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) work[s] = work[s] == m ? kEmptyKey : work[s];
+    }
+    const double t = (n >= (uint32_t)k && kth != kEmptyKey)
+                         ? (double)ord2f((uint32_t)(kth >> 32)) + a.two_eps : __builtin_inf();
+    int32_t* rows = s_rows[w];
+    int nr = 0;
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const bool sel = key[s] != kEmptyKey && (double)ord2f((uint32_t)(key[s] >> 32)) <= t;
+        const uint64_t b = __ballot(sel);
+        if (sel) rows[nr + __popcll(b & lt)] = (int32_t)(uint32_t)key[s];
+        nr += __popcll(b);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // entry j (< nr) is kept by lane j % 64, slot j / 64
+    double mine[4];
+    int32_t mrow[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        mine[s] = __builtin_inf();
+        mrow[s] = INT32_MAX;
+    }
+    for (int j0 = 0; j0 < nr; j0 += kB) {
+        int32_t r[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int64_t x = j0 + b < nr ? (int64_t)rows[j0 + b] : -1;
+            r[b] = (x < 0 || x >= a.n_rows) ? -1 : (int32_t)x;
+            if (j0 + b < nr && r[b] < 0 && lane == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
+        }
+        double dv[kB];
+        rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int j = j0 + b;
+            if (j < nr && r[b] >= 0 && lane == (j & 63)) {
+                const int sl = j >> 6;
+                const double v = out_value<OUT64>(dv[b]);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    mine[s] = s == sl ? v : mine[s];
+                    mrow[s] = s == sl ? r[b] : mrow[s];
+                }
+            }
+        }
+    }
+    const size_t o = (size_t)p * k;
+    for (int i = 0; i < k; ++i) {
+        double bd = mine[0];
+        int32_t br = mrow[0];
+#pragma unroll
+        for (int s = 1; s < 4; ++s)
+            if (lt_dp(mine[s], mrow[s], bd, br)) {
+                bd = mine[s];
+                br = mrow[s];
+            }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double od = __shfl_xor(bd, off);
+            const int32_t orw = __shfl_xor(br, off);
+            if (lt_dp(od, orw, bd, br)) {
+                bd = od;
+                br = orw;
+            }
+        }
+        const bool empty = br == INT32_MAX;
+        if (lane == 0) x_store<OUT64>(a, o + i, empty ? __builtin_inf() : bd, empty ? -1 : a.gpos[br]);
+        if (!empty) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                if (mrow[s] == br) {
+                    mine[s] = __builtin_inf();
+                    mrow[s] = INT32_MAX;
+                }
+        }
+    }
+}
+
 // One workgroup per overflowed pair: the exact distance of every row of its
 // bucket shard (a wave per kB rows), lane 0 of each wave keeps the wave's
 // top-k by (distance, row) in LDS, thread 0 merges the waves' lists.
@@ -928,6 +1098,11 @@ int launch_x3(const XArgs& a, int64_t P, hipStream_t s) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     });
     LMI_HIP_TRY(attr_err);
+    if (a.two_eps > 0.0) {
+        hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64>), dim3((unsigned)((P + kXT / 64 - 1) / (kXT / 64))),
+                           dim3(kXT), 0, s, a, (int32_t)P);
+        LMI_LAUNCH_CHECK("x_select_wave_kernel");
+    }
     hipLaunchKernelGGL((x_select_kernel<TC, TQ, OUT64>), dim3((unsigned)P), dim3(kXT), lds, s, a);
     LMI_LAUNCH_CHECK("x_select_kernel");
     const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref()));

@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+from typing import Optional
 
 import numpy as np
 import torch
@@ -95,16 +96,25 @@ class GraphedSearch:
         self.bw = bw = per * dn + per * wq + (per * R if G > 1 else 0)
         pin = torch.cuda.is_available()
         self.bw_all = bw
-        self.h_blk = torch.zeros((G, bw), dtype=torch.int32, pin_memory=pin)
-        if not self.stage(nav, qs):
+        # pipeline: one pinned staging buffer per slot, so the host stages the
+        # next batch while the current one is uploaded and searched (stream())
+        self.pipeline = bool(pipeline) and capture
+        self.h_blks = [torch.zeros((G, bw), dtype=torch.int32, pin_memory=pin)
+                       for _ in range(2 if self.pipeline else 1)]
+        self.h_blk = self.h_blks[0]
+        self._staged = [None] * len(self.h_blks)
+        self._slot = 0
+        if not self.stage(nav, qs, slot=0):
             raise ValueError("staging failed")
+        if self.pipeline:
+            self.h_blks[1].copy_(self.h_blks[0])
+            self._staged[1] = self._staged[0]
         need = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
             C.byref(ix.desc), nq, R, k_round, self.qmode)
         self.ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
         # pipeline: two device copies of the staged block, each with its own
-        # captured graph; run() uploads the next one on a copy stream while
-        # the current graph runs (the upload leaves the graph)
-        self.pipeline = bool(pipeline) and capture
+        # captured graph; the upload of a slot's block runs on a copy stream
+        # beside the other slot's step (the upload leaves the graph)
         self.d_blks = [torch.empty((bw,), dtype=torch.int32, device=dev)
                        for _ in range(2 if self.pipeline else 1)]
         self.d_blk = self.d_blks[0]
@@ -187,7 +197,7 @@ class GraphedSearch:
             self._up_ev = [torch.cuda.Event() for _ in range(2)]
             self._done_ev = [torch.cuda.Event() for _ in range(2)]
             for slot in range(2):
-                self.d_blks[slot].copy_(self.h_blk[g], non_blocking=True)
+                self.d_blks[slot].copy_(self.h_blks[slot][g], non_blocking=True)
             torch.cuda.synchronize(dev)
         slots = (0, 1) if self.pipeline else (0, 0)
         side = torch.cuda.Stream(dev)
@@ -229,9 +239,10 @@ class GraphedSearch:
         self._prefetch = True
         torch.cuda.synchronize(dev)
 
-    def stage(self, q_nav, q_search) -> bool:
+    def stage(self, q_nav, q_search, slot: Optional[int] = None) -> bool:
         """Write a batch (host or device arrays of the captured shape) into the
-        pinned staging buffer.  False if it cannot be staged in the captured
+        pinned staging buffer of `slot` (default: the slot the next run or
+        launch replays).  False if it cannot be staged in the captured
         precision (clip768 values not fp16-representable under an fp16
         capture): run() then answers it on the eager path."""
         nav = host_array(q_nav)
@@ -241,14 +252,17 @@ class GraphedSearch:
             raise ValueError("a staged batch must have the captured shape")
         if not _f32_exact(qs):
             return False  # float64 values float32 would change: the eager path
-        if getattr(self, "pipeline", False):
-            # an upload from the pinned buffer may be in flight (run());
-            # both device copies are stale from now on
-            self._cs.synchronize()
+        if slot is None:
+            slot = self._slot
+        if self.pipeline and getattr(self, "_fresh", None) is not None:
+            # an upload may still read the pinned buffer; both device copies
+            # are stale from now on (a launch runs the last staged batch)
+            for e in self._up_ev:
+                e.synchronize()
             self._fresh = [False, False]
         # every rank block, on the host cores (every rank stages the whole
         # batch, so all ranks decide its precision class alike)
-        blk = self.h_blk.numpy()
+        blk = self.h_blks[slot].numpy()
         ok = True
         for g in range(blk.shape[0]):
             lo, hi = min(nq, g * per), min(nq, (g + 1) * per)
@@ -259,12 +273,15 @@ class GraphedSearch:
             else:
                 stage_rows_f32(sv.view(np.float32).reshape(hi - lo, d), qs[lo:hi])
         if not ok:
-            # not fp16-exact under an fp16 capture: put the last staged batch
-            # back (run() without arguments replays it) and answer eagerly
-            if getattr(self, "_staged", None) is not None:
-                self.stage(*self._staged)
+            # not fp16-exact under an fp16 capture: put the slot's last staged
+            # batch back (run() without arguments replays it) and answer eagerly
+            last = getattr(self, "_last", slot)
+            if self._staged[slot] is not None:
+                self.stage(*self._staged[slot], slot=slot)
+            self._last = last
             return False
-        self._staged = (nav, qs)
+        self._staged[slot] = (nav, qs)
+        self._last = slot
         return True
 
     def upload_bytes(self) -> int:
@@ -297,6 +314,33 @@ class GraphedSearch:
         else:
             torch.cuda.current_stream(dev).synchronize()
         return self._answer(self.h)
+
+    def stream(self, batches):
+        """Answer an iterable of (q_nav, q_search) batches in order, yielding
+        (dists, anns) copies per batch.  pipeline=True: batch i + 1 is staged
+        on the host cores and uploaded on the copy stream while batch i's step
+        runs, and its step is enqueued behind it before batch i's answer is
+        read (two steps in flight); otherwise one run() per batch.  A batch
+        that cannot be staged is answered by Searcher.search, in order."""
+        if not self.pipeline:
+            for b in batches:
+                yield tuple(a.copy() for a in self.run(*b))
+            return
+        self._prefetch = False
+        pending = None
+        for b in batches:
+            if not self.stage(*b):
+                if pending is not None:
+                    yield tuple(a.copy() for a in self.result(pending))
+                    pending = None
+                yield self._eager(*b)
+                continue
+            t = self.launch()
+            if pending is not None:
+                yield tuple(a.copy() for a in self.result(pending))
+            pending = t
+        if pending is not None:
+            yield tuple(a.copy() for a in self.result(pending))
 
     def _answer(self, h):
         hd, ha, st, rst = answer_views(h, self.nq, self.w)
@@ -332,7 +376,7 @@ class GraphedSearch:
         cs = self._cs
         cs.wait_event(self._done_ev[slot])
         with torch.cuda.stream(cs):
-            self.d_blks[slot].copy_(self.h_blk[self.rank_in_group], non_blocking=True)
+            self.d_blks[slot].copy_(self.h_blks[self._last][self.rank_in_group], non_blocking=True)
         self._up_ev[slot].record(cs)
         self._fresh[slot] = True
 

@@ -178,3 +178,33 @@ def test_launch_one_ahead_answers_each_batch(setup):
         d, a = g.result(tk)
         np.testing.assert_array_equal(d, e0)
         np.testing.assert_array_equal(a, b0)
+
+
+@pytest.mark.parametrize("pipeline,dist", [(True, "f32"), (True, "f64"), (False, "f32")])
+def test_graph_stream_answers_each_batch(setup, pipeline, dist):
+    """GraphedSearch.stream: with pipeline=True batch i + 1 is staged into the
+    other slot's pinned buffer and uploaded while batch i's step runs; every
+    answer equals the eager search of its own batch, in order, across a batch
+    the fp16 capture cannot stage (answered eagerly, in its place), and run()
+    without arguments afterwards replays the last staged batch."""
+    w, s = setup
+    T = lambda a: torch.from_numpy(a).cuda()
+    rng = np.random.default_rng(11)
+    batches = []
+    for i in range(7):
+        perm = rng.permutation(w["q"].shape[0])
+        qn, q = w["qn"][perm], w["q"][perm]
+        if i == 4:
+            q = q + np.float32(1e-5)   # not fp16-exact
+        batches.append((qn, q))
+    want = [s.search(T(qn), T(q), 4, k=10, dist=dist) for qn, q in batches]
+    g = s.graph(w["qn"], w["q"], 4, k=10, dist=dist, pipeline=pipeline)
+    got = list(g.stream(iter(batches)))
+    assert len(got) == len(batches)
+    for (d, a), (d0, a0) in zip(got, want):
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+    for _ in range(3):
+        d, a = g.run()
+        np.testing.assert_array_equal(d, want[-1][0])
+        np.testing.assert_array_equal(a, want[-1][1])

@@ -39,7 +39,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
                 agg[r["Kernel_Name"].split("(lmi::")[0].replace("void ", "")].append(float(r["Counter_Value"]))
     for k, v in agg.items():
         out["by_kernel"].setdefault(k, {})[c] = {"launches": len(v), "mean_kb": sum(v) / len(v)}
-        if "<10," in k:
+        if "<10, 0, false, 0>" in k:  # (the f32 product scan; MODE 3 is the float64 band scan)
             out[c] = {"launches": len(v), "mean_kb": sum(v) / len(v), "kernel": k}
 print(json.dumps(out))
 json.dump(out, open("gpurun_out/prof/pmc_traffic.json", "w"), indent=1)
