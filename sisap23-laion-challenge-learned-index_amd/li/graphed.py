@@ -129,7 +129,10 @@ class GraphedSearch:
         # collectives inside a replayed graph are GPU work the process group's
         # watchdog does not track: run() bounds its own wait instead
         self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
-        copy_stream = torch.cuda.Stream(dev)
+        # (on its own hardware queue: a copy stream on the step's queue would
+        # wait for the step it should run beside; li.stream.queue_streams)
+        from .stream import queue_streams
+        copy_stream = queue_streams(dev, 1)[0]
 
         def step(slot=0):
             ans = answer_buffer(nq, self.w, dev)

@@ -16,7 +16,7 @@ MFMA-bound scan between latency-bound chains.  Here every launch runs:
     F  batch t-3: K2's MERGE phase (+ the float64 refinement)
                   [-> all-gather + K3 at G > 1] -> replay (K4) -> D2H
 
-on five streams ordered by per-slot events, and returns the answer of the
+on four streams ordered by per-slot events, and returns the answer of the
 batch it finished; every batch passes every stage (the same kernels as
 Searcher.search), so each answer equals Searcher.search of its batch bit for
 bit.  The persistent scan holds every CU while it runs, so the R, P and F
@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import time
 from typing import Optional
 
 import numpy as np
@@ -43,6 +44,69 @@ from . import _lib
 from ._host import host_array, stage_rows_f16, stage_rows_f32, wait_event_with_deadline
 from .index import _SEED_ROUND0, answer_buffer, answer_views, bucket_topk, bucket_topk_f64, \
     replay_device
+
+
+def _runs_beside(a, b, spin, wait_s):
+    """True if a kernel on stream `b` finishes while a spinning one on stream
+    `a` still runs (the two streams are on different hardware queues)."""
+    ea, eb = torch.cuda.Event(), torch.cuda.Event()
+    with torch.cuda.stream(a):
+        torch.cuda._sleep(spin)
+    ea.record(a)
+    with torch.cuda.stream(b):
+        torch.cuda._sleep(1)
+    eb.record(b)
+    t0 = time.perf_counter()
+    beside = False
+    while time.perf_counter() - t0 < wait_s:
+        if eb.query():
+            beside = not ea.query()
+            break
+    ea.synchronize()
+    eb.synchronize()
+    return beside
+
+
+def _spin_cycles(stream, ms_target: float) -> int:
+    """torch.cuda._sleep's argument (device clock cycles) for a spin of at
+    least `ms_target` ms on `stream`, measured."""
+    spin, ms = 1 << 18, 0.0
+    while ms < ms_target / 2 and spin < (1 << 34):
+        spin *= 4
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(spin)
+        e1.record(stream)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+    return int(spin * max(1.0, ms_target / max(ms, 1e-3)))
+
+
+def queue_streams(dev, n: int):
+    """`n` new streams of `dev` whose work runs beside the current stream's
+    and beside each other's.  HIP maps the streams of a process onto
+    GPU_MAX_HW_QUEUES (4) hardware queues and serialises the streams that
+    share one: a finish stream that lands on the scan's queue waits for the
+    next scan instead of running in its tail (a float64 stream step measured
+    636 µs between scans that way against 196 for float32, whose finish
+    stream had landed elsewhere).  Each candidate stream is
+    tested with a spinning kernel on the others (≈ 10 ms per test); with
+    fewer free queues the rest share.  Every caller gets streams of its own:
+    a stream the graphs of an object still alive (or not yet collected) were
+    launched on is not handed out again on purpose."""
+    dev = torch.device(dev)
+    main = torch.cuda.current_stream(dev)
+    spin, wait_s = _spin_cycles(main, 10.0), 5e-3
+    have, tries = [], 0
+    while len(have) < n and tries < 4 * n + 4:
+        s = torch.cuda.Stream(dev)
+        tries += 1
+        if all(_runs_beside(o, s, spin, wait_s) for o in [main] + have):
+            have.append(s)
+    while len(have) < n:
+        have.append(torch.cuda.Stream(dev))
+    return have
 
 
 class QueryNotF16(RuntimeError):
@@ -224,12 +288,12 @@ class StreamedSearch:
         self._mdd, self._mpp = [None] * NS, [None] * NS
         self._f = dict(U=upload, R=route, X=xgather, P=plan, S=scan, F=finish, F1=finish1,
                        F2=finish2)
-        # five streams: uploads (the copy engine), route, plan, scan (the
-        # caller's stream), finish; per-slot events order them across launches
-        self._cs = torch.cuda.Stream(dev)
-        self._rs = torch.cuda.Stream(dev)
-        self._ps = torch.cuda.Stream(dev)
-        self._fs = torch.cuda.Stream(dev)
+        # four streams: the finish, the plan, the upload + route (the H2D on
+        # the copy engine, then the router), and the scan on the caller's
+        # stream, each on its own hardware queue (queue_streams); per-slot
+        # events order them across launches
+        self._fs, self._ps, self._rs = queue_streams(dev, 3)
+        self._cs = self._rs
         ev = lambda: [torch.cuda.Event() for _ in range(NS)]
         self._up, self._rdone, self._pdone, self._sdone = ev(), ev(), ev(), ev()
         self._gdone, self._fdone = ev(), ev()
@@ -362,7 +426,8 @@ class StreamedSearch:
         it finished (numpy views, valid for the next three launches).  Slot
         t mod 4 is uploaded, routed and planned (stage() before step() streams
         a new batch; without it the slot's previous rows are used again), slot
-        t + 2 scanned and t + 1 finished (mod 4), on five streams:
+        t + 2 scanned and t + 1 finished (mod 4), on four streams (each on its
+        own hardware queue, queue_streams; the upload and the route share one):
 
             copy:   H2D of this rank's block of slot t      (the copy engine)
             route:  wait H2D -> router (slot t)

@@ -163,3 +163,19 @@ def test_stream_of_float16_host_batches(setup):
     for (d, a), (d0, a0) in zip(got, ref):
         np.testing.assert_array_equal(d, d0)
         np.testing.assert_array_equal(a, a0)
+
+
+def test_queue_streams_run_beside_each_other():
+    """li.stream.queue_streams: the streams the batch stream runs its finish,
+    plan and route on take work while the current stream, and each other,
+    are busy (each on its own hardware queue: GPU_MAX_HW_QUEUES is 4 on the
+    box, so the scan's stream and these three fill them)."""
+    from li.stream import _runs_beside, _spin_cycles, queue_streams
+    ss = queue_streams("cuda", 3)
+    assert len({s.cuda_stream for s in ss}) == 3
+    main = torch.cuda.current_stream()
+    spin = _spin_cycles(main, 10.0)
+    for i, s in enumerate(ss):
+        assert _runs_beside(main, s, spin, 5e-3)
+        for o in ss[:i]:
+            assert _runs_beside(o, s, spin, 5e-3)
