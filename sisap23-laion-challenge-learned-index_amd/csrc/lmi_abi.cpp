@@ -43,6 +43,7 @@ EnvConfig read_env() {
     e.wide_no_fixup = env_b("LMI_WIDE_NO_FIXUP");
     e.router_fma = env_b("LMI_ROUTER_FMA");
     e.router_qg = env_i("LMI_ROUTER_QG", 0);
+    e.refine_kb = env_i("LMI_REFINE_KB", 1);
     return e;
 }
 

@@ -158,13 +158,13 @@ __device__ inline double row_dist64(const TC* row, int d, int nps, const double 
 // row's value is computed in exactly row_dist64's order (the same bits)
 // (NPS: pieces per lane known at compile time, 3 for d in (512, 768])
 constexpr int kB = 4;
-template <int NPS>
-__device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const int32_t (&r)[kB], int d,
-                                       int nps, const double (&qh)[NPS][4], double (&out)[kB]) {
+template <int NPS, int KB = kB>
+__device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const int32_t (&r)[KB], int d,
+                                       int nps, const double (&qh)[NPS][4], double (&out)[KB]) {
     const int lane = threadIdx.x & 63;
-    uint2 raw[kB][NPS];
+    uint2 raw[KB][NPS];
 #pragma unroll
-    for (int b = 0; b < kB; ++b)
+    for (int b = 0; b < KB; ++b)
 #pragma unroll
         for (int i = 0; i < NPS; ++i) {
             const int e0 = 4 * (lane + 64 * i);
@@ -172,9 +172,9 @@ __device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const
                             ? *reinterpret_cast<const uint2*>(base + (size_t)r[b] * d_pad + e0)
                             : make_uint2(0u, 0u);
         }
-    double dot[kB], ss[kB];
+    double dot[KB], ss[KB];
 #pragma unroll
-    for (int b = 0; b < kB; ++b) {
+    for (int b = 0; b < KB; ++b) {
         dot[b] = 0.0;
         ss[b] = 0.0;
 #pragma unroll
@@ -194,12 +194,12 @@ __device__ inline void rows_dist64_f16(const _Float16* base, size_t d_pad, const
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
-        for (int b = 0; b < kB; ++b) {
+        for (int b = 0; b < KB; ++b) {
             dot[b] += __shfl_xor(dot[b], off);
             ss[b] += __shfl_xor(ss[b], off);
         }
 #pragma unroll
-    for (int b = 0; b < kB; ++b) {
+    for (int b = 0; b < KB; ++b) {
         double n = sqrt(ss[b]);
         if (n < 10.0 * kEps64) n = 1.0;
         out[b] = 1.0 - dot[b] / n;
@@ -213,10 +213,12 @@ __device__ inline bool lt_dp(double a, int32_t pa, double b, int32_t pb) {
 constexpr int kSlots = 4;  // list entries per lane: lists of <= 256 entries
 
 // the slot-`s` value of lane `l` of a wave-uniform (s, l)
-template <typename T>
-__device__ inline T shfl_slot(const T (&v)[kSlots], int j) {
+template <typename T, int NS>
+__device__ inline T shfl_slot(const T (&v)[NS], int j) {
     const int s = j >> 6, l = j & 63;
-    const T x = s == 0 ? v[0] : s == 1 ? v[1] : s == 2 ? v[2] : v[3];
+    T x = v[0];
+#pragma unroll
+    for (int i = 1; i < NS; ++i) x = s == i ? v[i] : x;
     return __shfl(x, l);
 }
 
@@ -234,8 +236,9 @@ __device__ inline const TQ* query_of(const RefineArgs& a, int64_t q) {
 }
 
 // NP: pieces of 4 per lane held for the query (3: d <= 768; 4: d <= 1024)
-template <typename TC, typename TQ, int NP>
-__global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void refine_kernel(RefineArgs a) {
+template <typename TC, typename TQ, int NP, int KB = kB, int NSL = kSlots>
+__global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(KB >= 4 ? 5 : (KB == 2 ? 6 : 7) + (NSL == 1 ? 1 : 0))))
+void refine_kernel(RefineArgs a) {
     const int lane = threadIdx.x & 63;
     const int64_t p = (int64_t)blockIdx.x * (kRefT / 64) + (threadIdx.x >> 6);
     const int64_t P = (int64_t)a.nq * a.R;
@@ -243,11 +246,11 @@ __global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void
     const int kl = a.kl, k = a.k;
     const size_t li = (size_t)p * kl;
     // lane l, slot s holds list entry 64 s + l
-    float dj[kSlots];
-    int32_t rj[kSlots], gj[kSlots];
+    float dj[NSL];
+    int32_t rj[NSL], gj[NSL];
     int n_valid = 0;
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < NSL; ++s) {
         const int e = 64 * s + lane;
         const bool has = e < kl;
         dj[s] = has ? a.ld[li + e] : __builtin_inff();
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void
         }
         m = 0;
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s)
+        for (int s = 0; s < NSL; ++s)
             m += __popcll(__ballot(64 * s + lane < kl && rj[s] >= 0 && (double)dj[s] <= t));
     } else if (n_valid < kl) {
         m = n_valid;  // the shard's whole bucket is listed
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void
         const double t = (double)a.ld[li + k - 1] + 2.0 * a.eps;
         m = 0;
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s)
+        for (int s = 0; s < NSL; ++s)
             m += __popcll(__ballot(64 * s + lane < kl && (double)dj[s] <= t));
         if (m >= kl) {  // the band may continue past the list: exact fallback
             if (lane == 0) a.failed[atomicAdd(a.n_failed, 1)] = (int32_t)p;
@@ -297,34 +300,32 @@ __global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void
         }
     }
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s)
+    for (int s = 0; s < NSL; ++s)
         if (rj[s] >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);
-    double mine[kSlots];
+    double mine[NSL];
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) mine[s] = __builtin_inf();
+    for (int s = 0; s < NSL; ++s) mine[s] = __builtin_inf();
     auto keep = [&](int j, double dv) {
         if (lane == (j & 63)) {
             const int s = j >> 6;
-            mine[0] = s == 0 ? dv : mine[0];
-            mine[1] = s == 1 ? dv : mine[1];
-            mine[2] = s == 2 ? dv : mine[2];
-            mine[3] = s == 3 ? dv : mine[3];
+#pragma unroll
+            for (int i = 0; i < NSL; ++i) mine[i] = s == i ? dv : mine[i];
         }
     };
     if constexpr (sizeof(TC) == 2) {
         if (a.d % 4 == 0) {
-            // (the stored fp16 rows: kB at a time)
-            for (int j0 = 0; j0 < m; j0 += kB) {
-                int32_t r[kB];
+            // (the stored fp16 rows: KB at a time)
+            for (int j0 = 0; j0 < m; j0 += KB) {
+                int32_t r[KB];
 #pragma unroll
-                for (int b = 0; b < kB; ++b) {
+                for (int b = 0; b < KB; ++b) {
                     const int32_t x = j0 + b < m ? shfl_slot(rj, j0 + b) : -1;
                     r[b] = (x < 0 || x >= a.n_rows) ? -1 : x;
                 }
-                double dv[kB];
-                rows_dist64_f16<NP>(rows_of<TC>(a), (size_t)a.d_pad, r, a.d, nps, qh, dv);
+                double dv[KB];
+                rows_dist64_f16<NP, KB>(rows_of<TC>(a), (size_t)a.d_pad, r, a.d, nps, qh, dv);
 #pragma unroll
-                for (int b = 0; b < kB; ++b)
+                for (int b = 0; b < KB; ++b)
                     if (r[b] >= 0) keep(j0 + b, dv[b]);
             }
             goto ranked;
@@ -338,16 +339,16 @@ __global__ __launch_bounds__(kRefT) __attribute__((amdgpu_waves_per_eu(5))) void
     }
 ranked:
     // rank of every refined entry among the m by (d64, position)
-    int rank[kSlots] = {};
+    int rank[NSL] = {};
     for (int i = 0; i < m; ++i) {
         const double di = shfl_slot(mine, i);
         const int32_t gi = shfl_slot(gj, i);
 #pragma unroll
-        for (int s = 0; s < kSlots; ++s)
+        for (int s = 0; s < NSL; ++s)
             rank[s] += (64 * s + lane != i && lt_dp(di, gi, mine[s], gj[s])) ? 1 : 0;
     }
 #pragma unroll
-    for (int s = 0; s < kSlots; ++s) {
+    for (int s = 0; s < NSL; ++s) {
         if (64 * s + lane < m && rank[s] < k) {
             od[rank[s]] = mine[s];
             op[rank[s]] = gj[s];
@@ -1139,9 +1140,25 @@ namespace {
 template <typename TC, typename TQ>
 void launch_refine(const RefineArgs& a, dim3 grid, dim3 fgrid, hipStream_t s) {
     // (d <= 768: three pieces per lane, the registers of the fourth freed)
-    if (a.d <= 3 * 256)
+    bool done = false;
+    if constexpr (sizeof(TC) == 2) {
+        // (fp16 rows, d <= 768, lists of <= 64 entries: one list slot per
+        // lane, the registers of three freed for more waves per SIMD, and KB
+        // rows in flight per wave, LMI_REFINE_KB)
+        const int kb = env_config().refine_kb;
+        if (a.d <= 3 * 256 && a.kl <= 64) {
+            done = true;
+            if (kb == 1)
+                hipLaunchKernelGGL((refine_kernel<TC, TQ, 3, 1, 1>), grid, dim3(kRefT), 0, s, a);
+            else if (kb == 4)
+                hipLaunchKernelGGL((refine_kernel<TC, TQ, 3, 4, 1>), grid, dim3(kRefT), 0, s, a);
+            else
+                hipLaunchKernelGGL((refine_kernel<TC, TQ, 3, 2, 1>), grid, dim3(kRefT), 0, s, a);
+        }
+    }
+    if (!done && a.d <= 3 * 256)
         hipLaunchKernelGGL((refine_kernel<TC, TQ, 3>), grid, dim3(kRefT), 0, s, a);
-    else
+    else if (!done)
         hipLaunchKernelGGL((refine_kernel<TC, TQ, kMaxPieces>), grid, dim3(kRefT), 0, s, a);
     // one workgroup per queued pair (the grid strides over the queue; the
     // queue length is read on the device, usually 0); k <= kFbSliceK: the
