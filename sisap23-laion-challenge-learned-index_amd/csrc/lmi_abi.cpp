@@ -44,6 +44,7 @@ EnvConfig read_env() {
     e.router_fma = env_b("LMI_ROUTER_FMA");
     e.router_qg = env_i("LMI_ROUTER_QG", 0);
     e.refine_kb = env_i("LMI_REFINE_KB", 1);
+    e.xsel_kb = env_i("LMI_XSEL_KB", 1);
     return e;
 }
 

@@ -639,16 +639,16 @@ constexpr double kEps32 = 1.1920928955078125e-07;
 // 1 - <q^, y/|y|> of kB rows of float32 or float64 values at once (every row's
 // pieces loaded before any is used), in row_dist64's order; sklearn's zero
 // rule with the eps of the output dtype
-template <typename TC, int NPS>
-__device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t (&r)[kB], int d, int nps,
-                                     const double (&qh)[NPS][4], double zero_eps, double (&out)[kB]) {
+template <typename TC, int NPS, int KB = kB>
+__device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t (&r)[KB], int d, int nps,
+                                     const double (&qh)[NPS][4], double zero_eps, double (&out)[KB]) {
     const int lane = threadIdx.x & 63;
-    double dot[kB], ss[kB];
+    double dot[KB], ss[KB];
     if constexpr (sizeof(TC) == 4) {
         // float32 rows stay float32 until used (half the registers of doubles)
-        float v[kB][NPS][4];
+        float v[KB][NPS][4];
 #pragma unroll
-        for (int b = 0; b < kB; ++b)
+        for (int b = 0; b < KB; ++b)
 #pragma unroll
             for (int i = 0; i < NPS; ++i) {
                 const int e0 = 4 * (lane + 64 * i);
@@ -662,7 +662,7 @@ __device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t
                 }
             }
 #pragma unroll
-        for (int b = 0; b < kB; ++b) {
+        for (int b = 0; b < KB; ++b) {
             dot[b] = 0.0;
             ss[b] = 0.0;
 #pragma unroll
@@ -675,9 +675,9 @@ __device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t
                 }
         }
     } else {
-        double v[kB][NPS][4];
+        double v[KB][NPS][4];
 #pragma unroll
-        for (int b = 0; b < kB; ++b)
+        for (int b = 0; b < KB; ++b)
 #pragma unroll
             for (int i = 0; i < NPS; ++i) {
                 if (r[b] >= 0 && i < nps) {
@@ -688,7 +688,7 @@ __device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t
                 }
             }
 #pragma unroll
-        for (int b = 0; b < kB; ++b) {
+        for (int b = 0; b < KB; ++b) {
             dot[b] = 0.0;
             ss[b] = 0.0;
 #pragma unroll
@@ -703,12 +703,12 @@ __device__ inline void rows_dist64_x(const TC* base, size_t d_pad, const int32_t
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1)
 #pragma unroll
-        for (int b = 0; b < kB; ++b) {
+        for (int b = 0; b < KB; ++b) {
             dot[b] += __shfl_xor(dot[b], off);
             ss[b] += __shfl_xor(ss[b], off);
         }
 #pragma unroll
-    for (int b = 0; b < kB; ++b) {
+    for (int b = 0; b < KB; ++b) {
         double n = sqrt(ss[b]);
         if (n < 10.0 * zero_eps) n = 1.0;
         out[b] = 1.0 - dot[b] / n;
@@ -906,8 +906,8 @@ __device__ inline uint64_t wave_min_u64(uint64_t v) {
 // row list (any order), re-scored kB at a time, and the first k by (exact
 // distance, row) are taken by k wave minima -- the (distance, g.index) order,
 // rows ascending with global position inside a bucket shard.
-template <typename TC, typename TQ, bool OUT64>
-__global__ __launch_bounds__(kXT) void x_select_wave_kernel(XArgs a, int32_t n_pairs) {
+template <typename TC, typename TQ, bool OUT64, int KB = kB>
+__global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) == 8 ? 1 : KB >= 4 ? 4 : KB == 2 ? 5 : 7))) void x_select_wave_kernel(XArgs a, int32_t n_pairs) {
     __shared__ int32_t s_rows[kXT / 64][kXW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int pp = blockIdx.x * (kXT / 64) + w;
@@ -962,18 +962,18 @@ __global__ __launch_bounds__(kXT) void x_select_wave_kernel(XArgs a, int32_t n_p
         mine[s] = __builtin_inf();
         mrow[s] = INT32_MAX;
     }
-    for (int j0 = 0; j0 < nr; j0 += kB) {
-        int32_t r[kB];
+    for (int j0 = 0; j0 < nr; j0 += KB) {
+        int32_t r[KB];
 #pragma unroll
-        for (int b = 0; b < kB; ++b) {
+        for (int b = 0; b < KB; ++b) {
             const int64_t x = j0 + b < nr ? (int64_t)rows[j0 + b] : -1;
             r[b] = (x < 0 || x >= a.n_rows) ? -1 : (int32_t)x;
             if (j0 + b < nr && r[b] < 0 && lane == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
         }
-        double dv[kB];
-        rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
+        double dv[KB];
+        rows_dist64_x<TC, 3, KB>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
 #pragma unroll
-        for (int b = 0; b < kB; ++b) {
+        for (int b = 0; b < KB; ++b) {
             const int j = j0 + b;
             if (j < nr && r[b] >= 0 && lane == (j & 63)) {
                 const int sl = j >> 6;
@@ -1100,8 +1100,17 @@ int launch_x3(const XArgs& a, int64_t P, hipStream_t s) {
     });
     LMI_HIP_TRY(attr_err);
     if (a.two_eps > 0.0) {
-        hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64>), dim3((unsigned)((P + kXT / 64 - 1) / (kXT / 64))),
-                           dim3(kXT), 0, s, a, (int32_t)P);
+        const dim3 wg((unsigned)((P + kXT / 64 - 1) / (kXT / 64)));
+        // (float32 rows: LMI_XSEL_KB rows in flight per wave; float64 rows: 4)
+        const int kb = sizeof(TC) == 4 ? env_config().xsel_kb : 4;
+        if constexpr (sizeof(TC) == 4) {
+            if (kb == 1)
+                hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 1>), wg, dim3(kXT), 0, s, a, (int32_t)P);
+            else if (kb == 2)
+                hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 2>), wg, dim3(kXT), 0, s, a, (int32_t)P);
+        }
+        if (kb != 1 && kb != 2)
+            hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 4>), wg, dim3(kXT), 0, s, a, (int32_t)P);
         LMI_LAUNCH_CHECK("x_select_wave_kernel");
     }
     hipLaunchKernelGGL((x_select_kernel<TC, TQ, OUT64>), dim3((unsigned)P), dim3(kXT), lds, s, a);
