@@ -648,23 +648,29 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
         drp_next[(size_t)q * kr + j] = -1;
     }
     // the last merge (dists non-null) writes the answer itself: positions ->
-    // ids through pos_to_id, uint32 (one launch less than a separate output pass)
-    auto put = [&](int at, double v, int32_t p) {
-        if (dists) {
-            int64_t id = 0;
-            if (p >= 0) {
-                if (p < n_total) id = pos_to_id[p];
-                else atomicOr(status, 4);
-            }
-            dists[(size_t)q * wn + at] = v;
-            anns[(size_t)q * wn + at] = (uint32_t)id;  // numpy int64 -> uint32 assignment
-        } else {
-            Fd_out[(size_t)q * fs + at] = v;
-            Fp_out[(size_t)q * fs + at] = p;
-        }
-    };
+    // ids through pos_to_id, uint32 (one launch less than a separate output
+    // pass).  (A lambda capturing by reference kept its captures on the
+    // stack: 40 B of scratch per thread.)
+#define LMI_PUT(AT, V, P)                                                              \
+    do {                                                                               \
+        const int at_ = (AT);                                                          \
+        const double v_ = (V);                                                         \
+        const int32_t p_ = (P);                                                        \
+        if (dists) {                                                                   \
+            int64_t id = 0;                                                            \
+            if (p_ >= 0) {                                                             \
+                if (p_ < n_total) id = pos_to_id[p_];                                  \
+                else atomicOr(status, 4);                                              \
+            }                                                                          \
+            dists[(size_t)q * wn + at_] = v_;                                          \
+            anns[(size_t)q * wn + at_] = (uint32_t)id; /* numpy int64 -> uint32 */     \
+        } else {                                                                       \
+            Fd_out[(size_t)q * fs + at_] = v_;                                         \
+            Fp_out[(size_t)q * fs + at_] = p_;                                         \
+        }                                                                              \
+    } while (0)
     if (first) {
-        put(j, dd[j], dr_p[(size_t)q * kr + j]);
+        LMI_PUT(j, dd[j], dr_p[(size_t)q * kr + j]);
         if (thr_next && j == 0) {  // round 0's row need not be ascending (the <k quirk)
             double m = dd[0];
             for (int i = 1; i < kr; ++i) m = fmax(m, dd[i]);
@@ -682,8 +688,9 @@ __global__ __launch_bounds__(kT) void replay_merge_kernel(int32_t nq, int32_t kr
         const double di = dd[i];
         rank += (di < dj || (di == dj && wF + i < j)) ? 1 : 0;
     }
-    if (rank < wn) put(rank, dj, j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF]);
+    if (rank < wn) LMI_PUT(rank, dj, j < wF ? Fp[(size_t)q * fs + j] : dr_p[(size_t)q * kr + j - wF]);
     if (thr_next && rank == wn - 1) thr_next[q] = dj;  // the merged row is ascending
+#undef LMI_PUT
 }
 
 struct ReplayWs {
