@@ -304,7 +304,8 @@ STEP_TEXT = {
                          "pinned memory, then on five streams -- the H2D of that batch (copy engine) "
                          "and its router and plan, the scan of the batch of two launches before, the "
                          "chunk merge" + (" + one all-gather (lists + the next batch's query blocks) "
-                                          "+ K3" if a.gpus > 1 else "") + " + replay + D2H of the "
+                                          "+ K3" if (a.gpus > 1 or os.environ.get("LMI_FORCE_EXCHANGE") == "1")
+                                          else "") + " + replay + D2H of the "
                          "answer of the batch of three launches before (each a captured graph); every "
                          "batch passes every stage, each timed launch answers one batch"),
     "graph": lambda a: ("hip-graph replay per step (GraphedSearch.stream): each batch staged on the "
@@ -560,6 +561,8 @@ def main():
         if not agree(ok):
             if not graph_failed:
                 graph_failed.append("capture failed on another rank")
+            if gs is not None:
+                gs.close()
             del gs
             return None if single else timed_eager(dist)
         g_d, g_a = (a.copy() for a in gs.run())
@@ -570,6 +573,7 @@ def main():
         if not same:
             log(f"[bench] graph replay differs from the eager step ({dist}); timing eager launches")
             graph_failed.append("first replay differs from the eager step")
+            gs.close()
             del gs
             return None if single else timed_eager(dist)
         h2d = h2d_ms(gs.h_blk[gs.rank_in_group], gs.d_blk) + (gs.upload_bytes(),)
@@ -600,6 +604,7 @@ def main():
             torch.distributed.barrier()
         el = time.perf_counter() - t0
         marker_pop()
+        gs.close()
         del gs
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=device)
@@ -636,6 +641,8 @@ def main():
         if not agree(ok):
             if not stream_failed:
                 stream_failed.append("stream set-up failed on another rank")
+            if ss is not None:
+                ss.close()
             del ss
             return timed_graph(dist) if use_graph else timed_eager(dist)
         staged = []   # batch index staged at launch t (all slots hold batch 0 at set-up)
@@ -654,6 +661,7 @@ def main():
         if not same:
             log(f"[bench] batch stream differs from the eager step ({dist}); timing the step graph")
             stream_failed.append("stream answer differs from the eager step")
+            ss.close()
             del ss
             return timed_graph(dist) if use_graph else timed_eager(dist)
         h2d = h2d_ms(ss.h_stage[0][:ss.staged_words], ss.d_blk[0][:ss.staged_words]) + \
@@ -676,6 +684,7 @@ def main():
         el = time.perf_counter() - t0
         marker_pop()
         scans = ss.scan_ms()
+        ss.close()
         del ss
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=device if capture else "cpu")
@@ -852,6 +861,10 @@ def main():
                                          "overlapped": step_mode.get(args.dist, "").startswith("stream") or (
                                              step_mode.get(args.dist) == "graph" and not args.no_pipeline)},
         "dist": args.dist,
+        "list_exchange": ("RCCL all-gather of the packed lists + K3 over a "
+                          f"{world}-rank group" + (" (LMI_FORCE_EXCHANGE=1: the G > 1 branch on "
+                                                   "one GPU)" if world == 1 else "")
+                          if searcher.exchange else None),
         "step": STEP_TEXT[step_mode.get(args.dist, "eager").split(" ")[0]](args) +
                 step_mode.get(args.dist, "eager")[len(step_mode.get(args.dist, "eager").split(" ")[0]):] +
                 (f" (batch stream not used: {stream_failed[0]})" if stream_failed and use_stream else "") +

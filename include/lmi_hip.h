@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 9
+#define LMI_ABI_VERSION 10
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -76,6 +76,9 @@ extern "C" {
 #define LMI_Q_PHASE_PLAN 0x200
 #define LMI_Q_PHASE_SCAN 0x400
 #define LMI_Q_PHASE_MERGE 0x800
+/* ABI 10 (lmi_bucket_topk_f64g only): the float64 refinement as a phase of
+ * its own, after the ranks' k-th distances were exchanged. */
+#define LMI_Q_PHASE_REFINE 0x1000
 
 #define LMI_MAX_LAYERS 8
 #define LMI_MAX_K 16          /* largest k of one scan pass (and of K3 / the float32 ABI 1 lists) */
@@ -256,6 +259,35 @@ int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, int32_t nq, 
                          const double* q64, int32_t ldq64, const int32_t* classes, int32_t R,
                          int32_t k, int32_t qmode, double eps, double* out_d, int32_t* out_pos,
                          int32_t* status, void* workspace, size_t ws_bytes, void* stream);
+/* ABI 10: lmi_bucket_topk_f64q for a stripe of a G-rank index, with the band
+ * decided over every rank's lists (replaces, for the striped
+ * float64 search, the per-rank refinement of the same reference lines:
+ * utils.py:10-11 in float64 and LearnedIndex.py:170-172).  The float64 top-k
+ * of a pair lies in d32 <= T + 2 eps with T the k-th smallest d32 over ALL
+ * ranks' rows; T is never above a rank's own k-th, so a rank that knows T
+ * refines only its own rows of that merged band (about 1/G of them) instead
+ * of the band of its own list.  Phases:
+ *   PLAN, SCAN   as lmi_bucket_topk_f64q;
+ *   MERGE        the chunk merge, then kth_send (device [nq*R][k] f32) = each
+ *                pair's k smallest d32 of this rank (+inf past its list);
+ *   (the caller all-gathers kth_send: block g of G at kth_all + g * kth_stride)
+ *   REFINE       per pair T from the G blocks, then the refinement of this
+ *                rank's listed rows with d32 <= T + 2 eps (and the whole-shard
+ *                fallback of a pair whose band may hold unlisted rows): out_d
+ *                / out_pos hold this rank's part of the pair's float64 top-k,
+ *                ascending by (d64, position), (+inf, -1) past it.
+ * No phase flag = all four on one rank (kth_all == kth_send, G == 1).  K3
+ * (lmi_merge_topk_f64 / _packed) over the ranks' outputs then gives exactly
+ * the one-GPU float64 lists.  Needs the band lists (k <= 10 on the fp16
+ * scan): lmi_f64_global_band returns 1 when a call of these arguments has
+ * them, 0 otherwise (then lmi_bucket_topk_f64q per rank). */
+int lmi_f64_global_band(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k, int32_t qmode);
+int lmi_bucket_topk_f64g(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                         const double* q64, int32_t ldq64, const int32_t* classes, int32_t R,
+                         int32_t k, int32_t qmode, double eps, float* kth_send,
+                         const float* kth_all, int32_t G, int64_t kth_stride, double* out_d,
+                         int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes,
+                         void* stream);
 /* ABI 9: the split mode's bound eps_x on |d~ - d| (lmi_index_desc.corpus32),
  * for rows of d_pad elements; a host function (≈ 9.9e-4 at d_pad = 768).  In the
  * split mode the eps argument of lmi_bucket_topk_f64* is ignored (this one

@@ -65,7 +65,39 @@ struct RefineArgs {
     int32_t* status;
     double* pd;            // sliced fallback partial lists [kFbSlicedPairs][kFbSlices][k] (null: off)
     int32_t* pg;
+    // ABI 10 (band lists, a stripe of a G-rank index): the k smallest d32 of
+    // every rank's band list of every pair, gathered: block g at kth_all +
+    // g * kth_stride, [nq*R][k] ascending (+inf past the list); the band is
+    // then decided by the pair's k-th over all ranks (null: its own list's)
+    const float* kth_all;
+    int32_t kth_G;
+    int64_t kth_stride;
 };
+
+// the k-th smallest of G ascending lists of k values (lane g < G holds list g
+// in registers): k steps of a wave minimum, the winning lane (lowest on ties)
+// shifting its list; +inf when the lists hold fewer than k finite values
+__device__ inline float global_kth(const float* kth_all, int G, int64_t stride, int64_t p, int k) {
+    const int lane = threadIdx.x & 63;
+    float v[LMI_MAX_K];
+    const float* L = kth_all + (size_t)(lane < G ? lane : 0) * stride + (size_t)p * k;
+#pragma unroll
+    for (int i = 0; i < LMI_MAX_K; ++i) v[i] = (lane < G && i < k) ? L[i] : __builtin_inff();
+    float m = __builtin_inff();
+    for (int step = 0; step < k; ++step) {
+        float mn = v[0];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+        m = mn;
+        const uint64_t b = __ballot(v[0] == mn);
+        if (lane == (int)__builtin_ctzll(b)) {
+#pragma unroll
+            for (int i = 0; i + 1 < LMI_MAX_K; ++i) v[i] = v[i + 1];
+            v[LMI_MAX_K - 1] = __builtin_inff();
+        }
+    }
+    return m;
+}
 
 __device__ inline double wave_sum_d(double v) {
 #pragma unroll
@@ -258,6 +290,14 @@ void refine_kernel(RefineArgs a) {
         gj[s] = has ? a.lpos[li + e] : -1;
         n_valid += __popcll(__ballot(rj[s] >= 0));
     }
+    // ABI 10: the k-th over every rank's list -- never above this rank's own
+    // -- decides the band, so each rank refines only its rows of the merged
+    // pair's band; computed before the query's registers are live
+    float tg = 0.0f, tg0 = 0.0f;
+    if (a.lbound && a.kth_all) {
+        tg = global_kth(a.kth_all, a.kth_G, a.kth_stride, p, k);
+        if (a.seeded && p % a.R != 0) tg0 = global_kth(a.kth_all, a.kth_G, a.kth_stride, p - p % a.R, k);
+    }
     // (the query's loads go out beside the list's)
     const int nps = (a.d + 255) / 256;
     double qh[NP][4];
@@ -269,14 +309,18 @@ void refine_kernel(RefineArgs a) {
         // band lists: an unlisted row failed the scan's filter (d32 past the
         // pair's k-th + 2 eps) or has d32 >= lbound (+inf: no row was
         // dropped); the list holds the band unless lbound lies in it
-        const double t = n_valid >= k ? (double)a.ld[li + k - 1] + 2.0 * a.eps : __builtin_inf();
+        double t = n_valid >= k ? (double)a.ld[li + k - 1] + 2.0 * a.eps : __builtin_inf();
+        if (a.kth_all)
+            t = tg == __builtin_inff() ? __builtin_inf() : (double)tg + 2.0 * a.eps;
         // (LMI_Q_SEED_ROUND0, rounds r >= 1: the thresholded replay reads only
         // entries with d64 below round 0's final threshold D0 <= d32 10th of
         // pair (q, 0) + eps, i.e. rows with d32 < that + 2 eps; the list must
         // hold those alone -- the seed's own premise)
         double lim = t;
-        if (a.seeded && p % a.R != 0)
-            lim = fmin(lim, (double)a.ld[(size_t)(p - p % a.R) * kl + k - 1] + 2.0 * a.eps);
+        if (a.seeded && p % a.R != 0) {
+            const float t0 = a.kth_all ? tg0 : a.ld[(size_t)(p - p % a.R) * kl + k - 1];
+            lim = fmin(lim, (double)t0 + 2.0 * a.eps);
+        }
         const float ub = a.lbound[p];
         if (ub != __builtin_inff() && (double)ub <= lim) {
             if (lane == 0) a.failed[atomicAdd(a.n_failed, 1)] = (int32_t)p;
@@ -1196,15 +1240,46 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
                                 out_pos, status, workspace, ws_bytes, stream);
 }
 
-extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, int32_t nq,
-                                    int32_t ldq, const double* q64, int32_t ldq64,
-                                    const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
-                                    double eps, double* out_d, int32_t* out_pos, int32_t* status,
-                                    void* workspace, size_t ws_bytes, void* stream) {
-    using namespace lmi;
+namespace lmi {
+namespace {
+__global__ void kth_send_kernel(const float* ld, int kl, int k, int64_t P, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P * k) return;
+    const int64_t p = i / k;
+    out[i] = ld[(size_t)p * kl + (i - p * k)];
+}
+
+// lmi_bucket_topk_f64q, and with `global` (ABI 10, lmi_bucket_topk_f64g) the
+// band decided over every rank's lists: the MERGE phase writes each pair's k
+// smallest d32 to kth_send, the REFINE phase reads the gathered kth_all
+int bucket_topk_f64_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
+                         const double* q64, int32_t ldq64, const int32_t* classes, int32_t R,
+                         int32_t k, int32_t qmode, double eps, double* out_d, int32_t* out_pos,
+                         int32_t* status, void* workspace, size_t ws_bytes, void* stream,
+                         bool global, float* kth_send, const float* kth_all, int32_t kth_G,
+                         int64_t kth_stride) {
     const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
     qmode &= ~LMI_Q_SEED_ROUND0;
-    const int phases = take_phases(qmode);
+    int phases;
+    bool do_refine;
+    if (global) {
+        // PLAN / SCAN / MERGE (the chunk merge, then kth_send) and REFINE;
+        // none = all four (one rank: kth_all == kth_send)
+        const bool ref = (qmode & LMI_Q_PHASE_REFINE) != 0;
+        qmode &= ~LMI_Q_PHASE_REFINE;
+        const bool any = ((qmode >> 9) & 7) != 0;
+        phases = take_phases(qmode);
+        if (!any && ref) phases = 0;
+        do_refine = ref || !any;
+        LMI_CHECK_ARG(any || ref || (kth_all == kth_send && kth_G == 1),
+                      "one call of every phase needs kth_all == kth_send and G == 1");
+        LMI_CHECK_ARG(!(phases & kPhaseMerge) || kth_send, "the MERGE phase needs kth_send");
+        LMI_CHECK_ARG(!do_refine || (kth_all && kth_G >= 1 && kth_G <= 64 && kth_stride >= (int64_t)nq * R * k),
+                      "the REFINE phase needs kth_all, 1 <= G <= 64, stride >= nq*R*k");
+    } else {
+        phases = take_phases(qmode);
+        do_refine = (phases & kPhaseMerge) != 0;
+    }
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(k >= 1 && k <= LMI_MAX_K_F64, "k=%d outside [1, %d]", k, LMI_MAX_K_F64);
     LMI_CHECK_ARG(nq >= 0 && R >= 1 && (int64_t)nq * R < INT32_MAX, "bad nq/R");
@@ -1270,8 +1345,18 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
         set_error("phase flags need k + 5 <= %d (one scan pass)", LMI_MAX_K);
         return LMI_E_UNSUPPORTED;
     }
+    if (global && !band) {
+        set_error("the global band needs the band lists (k <= 10 on the fp16 scan; "
+                  "lmi_f64_global_band)");
+        return LMI_E_UNSUPPORTED;
+    }
+    if (global) {
+        a.kth_all = kth_all;
+        a.kth_G = kth_G;
+        a.kth_stride = kth_stride;
+    }
     if (phases & kPhasePlan) LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
-    int rc = w.passes
+    int rc = phases == 0 ? LMI_OK : w.passes
         ? bucket_topk_wide(idx, q, nq, ldq, classes, R, k + 5, qmode, (float*)(ws + w.ld),
                              (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), kl, status,
                              ws + w.scan, w.total - w.scan, s)
@@ -1280,8 +1365,14 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
                            ws + w.scan, w.total - w.scan, s, nullptr, 0, true, seed,
                            (float)(2.0 * eps), phases, nullptr, band ? (float*)(ws + w.lbound) : nullptr);
     if (rc != LMI_OK) return rc;
-    if (!(phases & kPhaseMerge)) return LMI_OK;
     const int64_t P = (int64_t)nq * R;
+    if (global && (phases & kPhaseMerge) && P > 0) {
+        const int64_t n = P * k;
+        hipLaunchKernelGGL(kth_send_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           (const float*)(ws + w.ld), kl, k, P, kth_send);
+        LMI_LAUNCH_CHECK("kth_send_kernel");
+    }
+    if (!do_refine) return LMI_OK;
     const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));
     const dim3 fgrid((unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref())));
     if (idx->corpus64)
@@ -1292,6 +1383,39 @@ extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, i
         launch_refine_q<float>(a, grid, fgrid, s);
     LMI_LAUNCH_CHECK("refine_kernel / fallback_kernel");
     return LMI_OK;
+}
+}  // namespace
+}  // namespace lmi
+
+extern "C" int lmi_bucket_topk_f64q(const lmi_index_desc* idx, const float* q, int32_t nq,
+                                    int32_t ldq, const double* q64, int32_t ldq64,
+                                    const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
+                                    double eps, double* out_d, int32_t* out_pos, int32_t* status,
+                                    void* workspace, size_t ws_bytes, void* stream) {
+    return lmi::bucket_topk_f64_impl(idx, q, nq, ldq, q64, ldq64, classes, R, k, qmode, eps, out_d,
+                                     out_pos, status, workspace, ws_bytes, stream, false, nullptr,
+                                     nullptr, 0, 0);
+}
+
+extern "C" int lmi_f64_global_band(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,
+                                   int32_t qmode) {
+    using namespace lmi;
+    qmode &= ~(LMI_Q_SEED_ROUND0 | LMI_Q_PHASE_REFINE);
+    take_phases(qmode);
+    if (!idx || idx->corpus32 || nq < 0 || R < 1 || k < 1 || k > LMI_MAX_K_F64) return 0;
+    return (!refine_ws(idx, nq, R, k, qmode).passes && band_capable(idx, qmode)) ? 1 : 0;
+}
+
+extern "C" int lmi_bucket_topk_f64g(const lmi_index_desc* idx, const float* q, int32_t nq,
+                                    int32_t ldq, const double* q64, int32_t ldq64,
+                                    const int32_t* classes, int32_t R, int32_t k, int32_t qmode,
+                                    double eps, float* kth_send, const float* kth_all, int32_t G,
+                                    int64_t kth_stride, double* out_d, int32_t* out_pos,
+                                    int32_t* status, void* workspace, size_t ws_bytes, void* stream) {
+    LMI_CHECK_ARG(idx != nullptr && !idx->corpus32, "the global band needs an index without corpus32");
+    return lmi::bucket_topk_f64_impl(idx, q, nq, ldq, q64, ldq64, classes, R, k, qmode, eps, out_d,
+                                     out_pos, status, workspace, ws_bytes, stream, true, kth_send,
+                                     kth_all, G, kth_stride);
 }
 
 extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx,

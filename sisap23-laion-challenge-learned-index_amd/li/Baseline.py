@@ -35,7 +35,7 @@ class Baseline(Logger):
         q = _upload_queries(queries, ix.device)
         classes = torch.zeros((q.shape[0], 1), dtype=torch.int32, device=ix.device)
         dist = dist_dtype(data, queries)
-        _, d, pos, st = Searcher(ix, None).lists(None, q, 1, k, classes=classes, dist=dist)
+        _, d, pos, st = Searcher(ix, None, exchange=False).lists(None, q, 1, k, classes=classes, dist=dist)
         if int(st.item()) & _lib.LMI_STATUS_INTERNAL:
             raise RuntimeError(f"Baseline.search: scan status {int(st.item())}")
         dists = d[:, 0].cpu().numpy()  # float32 or float64, as 1 - cosine_similarity

@@ -152,7 +152,7 @@ class LearnedIndex(Logger):
         the model; the HBM index and its caches stay out of the file."""
         st = dict(self.__dict__)
         for key in ("_index", "_cache_key", "_trusted", "_searcher", "_attached_labels", "_cat_written",
-                    "_pg"):
+                    "_pg", "_n_builds"):
             st.pop(key, None)
         return st
 
@@ -359,22 +359,54 @@ class LearnedIndex(Logger):
         s = time.time()
         pg = self._proc_group()
         if pg is None or pg[1] == 0:
-            _, labels = self.cluster(data, n_categories)
-            dataset = LIDataset(data, labels)
-            train_loader = torch.utils.data.DataLoader(
-                dataset, batch_size=256,
-                sampler=torch.utils.data.SubsetRandomSampler(data.index.values.tolist()))
-            nn = NeuralNetwork(input_dim=data.shape[1], output_dim=n_categories, lr=lr,
-                               model_type=model_type)
-            nn.train_batch(train_loader, epochs=epochs, logger=self.logger)
-            self.model = nn
-            pred = nn.predict(data_X_to_torch(data))
+            try:
+                _, labels = self.cluster(data, n_categories)
+                dataset = LIDataset(data, labels)
+                train_loader = torch.utils.data.DataLoader(
+                    dataset, batch_size=256,
+                    sampler=torch.utils.data.SubsetRandomSampler(data.index.values.tolist()))
+                nn = NeuralNetwork(input_dim=data.shape[1], output_dim=n_categories, lr=lr,
+                                   model_type=model_type)
+                nn.train_batch(train_loader, epochs=epochs, logger=self.logger)
+                self.model = nn
+                pred = nn.predict(data_X_to_torch(data))
+            except BaseException as e:
+                if pg is not None:
+                    self._build_done(pg, repr(e)[:500])
+                raise
         if pg is not None:
+            # the other ranks wait for rank 0's build on the rendezvous store,
+            # outside any collective: the build (k-means + 100 epochs of
+            # training) may take far longer than the process group's timeout
+            # (LMI_DIST_TIMEOUT_S), which then bounds only the broadcast
+            self._build_done(pg, None)
             # every rank must index the same buckets: rank 0's router and
             # labels, broadcast (GPU training is not promised bit-reproducible)
             pred = self._share_build(pg, None if pg[1] else (self.model, pred),
                                      data.shape[1], n_categories, lr, model_type)
         return pred, time.time() - s
+
+    def _build_done(self, pg, error):
+        """Rank 0: publish that the build ended (`error`: its message, or None).
+        Other ranks: wait for that key on the default group's store, polling,
+        for at most LMI_BUILD_TIMEOUT_S (default 86400 s), and raise rank 0's
+        error if it failed.  A store key per build call (builds are called in
+        the same order on every rank)."""
+        import torch.distributed as dist
+        store = dist.distributed_c10d._get_default_store()
+        self._n_builds = getattr(self, "_n_builds", 0) + 1
+        key = f"lmi_build_{self._n_builds}"
+        if pg[1] == 0:
+            store.set(key, "ok" if error is None else "ERR " + error)
+            return
+        deadline = time.monotonic() + float(os.environ.get("LMI_BUILD_TIMEOUT_S", "86400"))
+        while not store.check([key]):
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"rank {pg[1]}: rank 0's build did not finish in time")
+            time.sleep(0.2)
+        got = store.get(key).decode()
+        if got != "ok":
+            raise RuntimeError(f"rank 0's build failed: {got[4:]}")
 
     def _share_build(self, pg, built, input_dim, n_categories, lr, model_type):
         """Broadcast rank 0's trained router (state_dict) and object labels to

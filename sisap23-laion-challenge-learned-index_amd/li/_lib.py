@@ -38,6 +38,7 @@ LMI_Q_SEED_ROUND0 = 0x100
 LMI_Q_PHASE_PLAN = 0x200
 LMI_Q_PHASE_SCAN = 0x400
 LMI_Q_PHASE_MERGE = 0x800
+LMI_Q_PHASE_REFINE = 0x1000
 LMI_REPLAY_PHASE_GROUPS = 1
 LMI_REPLAY_PHASE_ROUNDS = 2
 LMI_MAX_LAYERS = 8
@@ -59,6 +60,8 @@ EXPORTS = (
     "lmi_scan_f64_workspace_bytes",
     "lmi_bucket_topk_f64",
     "lmi_bucket_topk_f64q",
+    "lmi_f64_global_band",
+    "lmi_bucket_topk_f64g",
     "lmi_refine_fallback_count",
     "lmi_split_eps",
     "lmi_replay_device_phase",
@@ -103,7 +106,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class IndexDesc(C.Structure):
@@ -143,6 +146,10 @@ _SIGNATURES = {
                                       C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_bucket_topk_f64q": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _P, _I32,
                                        _I32, _I32, C.c_double, _P, _P, _P, _P, C.c_size_t, _P]),
+    "lmi_f64_global_band": (C.c_int, [C.POINTER(IndexDesc), _I32, _I32, _I32, _I32]),
+    "lmi_bucket_topk_f64g": (C.c_int, [C.POINTER(IndexDesc), _P, _I32, _I32, _P, _I32, _P, _I32,
+                                       _I32, _I32, C.c_double, _P, _P, _I32, _I64, _P, _P, _P, _P,
+                                       C.c_size_t, _P]),
     "lmi_split_eps": (C.c_double, [_I32]),
     "lmi_replay_device_phase": (C.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32,
                                           _P, _I64, _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),

@@ -25,14 +25,31 @@ import torch
 import torch.distributed as dist
 
 
+def force_exchange() -> bool:
+    """LMI_FORCE_EXCHANGE=1: every step form takes its G > 1 branch even in a
+    one-rank process group -- the striped layout's packed lists, the captured
+    all-gather (RCCL over one rank), lmi_merge_topk_packed, the sharded
+    router's block exchange -- so the exchange runs on a one-GPU box exactly
+    as it does on eight (init_from_env then creates the one-rank group)."""
+    return os.environ.get("LMI_FORCE_EXCHANGE") == "1"
+
+
 def init_from_env(backend: Optional[str] = None):
-    """torchrun-style init (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); 127.0.0.1."""
+    """torchrun-style init (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*); 127.0.0.1.
+    One rank: no process group, unless LMI_FORCE_EXCHANGE=1 (a one-rank
+    group, backend nccl = RCCL on a GPU)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1:
+    if world == 1 and not force_exchange():
         return rank, world, local
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if world == 1 and "MASTER_PORT" not in os.environ:
+        import socket
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+        sk.close()
     os.environ.setdefault("MASTER_PORT", "29517")
     if backend is None:
         # LMI_DIST_BACKEND=gloo: control-flow rehearsal of several ranks on one
@@ -102,10 +119,15 @@ def launch_ranks(n: int, argv, script: str, relay_stdout: bool = True) -> int:
     port = sk.getsockname()[1]
     sk.close()
     procs = []
+    # rank 0's stdout goes to an unlinked temporary file, read back when the
+    # ranks end: a pipe read only then would block a rank 0 that writes more
+    # than the pipe buffer
+    import tempfile
+    out0 = tempfile.TemporaryFile() if relay_stdout else None
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r % ndev), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        out = (subprocess.PIPE if r == 0 else subprocess.DEVNULL) if relay_stdout else None
+        out = (out0 if r == 0 else subprocess.DEVNULL) if relay_stdout else None
         procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env, stdout=out))
     rc = 0
     live = set(range(n))
@@ -121,8 +143,10 @@ def launch_ranks(n: int, argv, script: str, relay_stdout: bool = True) -> int:
                     procs[o].terminate()
         time.sleep(0.05)
     if relay_stdout:
-        sys.stdout.write(procs[0].stdout.read().decode())
+        out0.seek(0)
+        sys.stdout.write(out0.read().decode(errors="replace"))
         sys.stdout.flush()
+        out0.close()
     return rc
 
 

@@ -63,9 +63,10 @@ class GraphedSearch:
         lib = _lib.load()
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
         self.use_threshold, self.dist = use_threshold, dist
-        G = ix.world
-        grouped = G > 1 and torch.distributed.is_initialized()
-        if k_round > _lib.LMI_MAX_K or (capture and grouped and
+        # X: the exchange branch (Searcher.exchange: G > 1 ranks, or a one-rank
+        # group under LMI_FORCE_EXCHANGE=1)
+        X = s.exchange
+        if k_round > _lib.LMI_MAX_K or (capture and X and
                                        torch.distributed.get_backend(s.group) != "nccl"):
             raise ValueError("graph capture needs k_round <= 16 and RCCL collectives "
                              "(capture=False runs the same step eagerly, e.g. over gloo)")
@@ -88,12 +89,11 @@ class GraphedSearch:
         # the batch is shared over the ranks of the process group (the index's
         # world is the stripe count; they differ only in a one-process
         # rehearsal of one stripe, tools/shard_step.py)
-        Gi = G if grouped else 1
-        G = torch.distributed.get_world_size(s.group) if Gi > 1 else 1
-        g = torch.distributed.get_rank(s.group) if Gi > 1 else 0
+        G = torch.distributed.get_world_size(s.group) if X else 1
+        g = torch.distributed.get_rank(s.group) if X else 0
         self.per = per = -(-nq // G)
         self.wq = wq = d // 2 if self.f16_up else d          # int32 words per staged row
-        self.bw = bw = per * dn + per * wq + (per * R if G > 1 else 0)
+        self.bw = bw = per * dn + per * wq + (per * R if X else 0)
         pin = torch.cuda.is_available()
         self.bw_all = bw
         # pipeline: one pinned staging buffer per slot, so the host stages the
@@ -110,7 +110,7 @@ class GraphedSearch:
             self.h_blks[1].copy_(self.h_blks[0])
             self._staged[1] = self._staged[0]
         need = (lib.lmi_scan_f64_workspace_bytes if f64 else lib.lmi_scan_workspace_bytes)(
-            C.byref(ix.desc), nq, R, k_round, self.qmode)
+            C.byref(ix.desc_for(k_round)), nq, R, k_round, self.qmode)
         self.ws = torch.empty(max(int(need), 256), dtype=torch.uint8, device=dev)
         # pipeline: two device copies of the staged block, each with its own
         # captured graph; the upload of a slot's block runs on a copy stream
@@ -118,14 +118,14 @@ class GraphedSearch:
         self.d_blks = [torch.empty((bw,), dtype=torch.int32, device=dev)
                        for _ in range(2 if self.pipeline else 1)]
         self.d_blk = self.d_blks[0]
-        self.d_all = torch.empty((G, bw), dtype=torch.int32, device=dev) if G > 1 else None
+        self.d_all = torch.empty((G, bw), dtype=torch.int32, device=dev) if X else None
         self.q32 = torch.empty((G * per, d), dtype=torch.float32, device=dev) \
-            if (self.f16_up or G > 1) else None
-        self.cls = torch.empty((G * per, R), dtype=torch.int32, device=dev) if G > 1 else None
+            if (self.f16_up or X) else None
+        self.cls = torch.empty((G * per, R), dtype=torch.int32, device=dev) if X else None
         bsz, p2id = s._device_tables()
         self.w = k_round if R == 1 else k
         self.rank_in_group = g
-        self.G = G
+        self.G, self.X = G, X
         # collectives inside a replayed graph are GPU work the process group's
         # watchdog does not track: run() bounds its own wait instead
         self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
@@ -138,7 +138,7 @@ class GraphedSearch:
             ans = answer_buffer(nq, self.w, dev)
             main = torch.cuda.current_stream(dev)
             d_blk = self.d_blks[slot]
-            if G == 1:
+            if not X:
                 if not self.pipeline:
                     # pca96 rows first; the clip768 rows come in on a second
                     # stream while the router runs
@@ -214,7 +214,7 @@ class GraphedSearch:
             torch.cuda.synchronize(dev)
         except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
             err = e
-        if Gi > 1:
+        if X:
             ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
             torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
             if int(ok.item()) == 0:
@@ -241,6 +241,26 @@ class GraphedSearch:
         # replayed again, run() without arguments); off once run() stages
         self._prefetch = True
         torch.cuda.synchronize(dev)
+
+    def close(self):
+        """Wait for this object's launches and uploads still in flight
+        (pipeline=True: launch() returns before its step ends), then release
+        the captured graphs and their memory pools (li.stream.StreamedSearch.
+        close: a graph destroyed while queued leaves the GPU reading freed
+        kernel arguments).  Idempotent."""
+        if getattr(self, "graphs", None) is None:
+            return
+        for name in ("_done_ev", "_up_ev"):
+            for e in getattr(self, name, ()):
+                e.synchronize()
+        self._cs.synchronize()
+        self.graphs, self.graph = None, None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown: torch may be gone)
+            pass
 
     def stage(self, q_nav, q_search, slot: Optional[int] = None) -> bool:
         """Write a batch (host or device arrays of the captured shape) into the
@@ -297,6 +317,8 @@ class GraphedSearch:
         [nq, w], anns uint32 [nq, w])."""
         s = self.searcher
         dev = s.index.device
+        if self.graph is None and self._step is None:
+            raise RuntimeError("GraphedSearch: run() after close()")
         if q_nav is not None or q_search is not None:
             if q_nav is None or q_search is None:
                 raise ValueError("stage both q_nav and q_search")
@@ -312,7 +334,7 @@ class GraphedSearch:
             self.graph.replay()
         else:
             self.h.copy_(self._step(), non_blocking=True)
-        if self.G > 1 and self.graph is not None:
+        if self.X and self.graph is not None:
             wait_with_deadline(dev, self.timeout_s)
         else:
             torch.cuda.current_stream(dev).synchronize()
@@ -367,7 +389,7 @@ class GraphedSearch:
         """Wait for the step of `ticket` (from launch()) -> (dists f64 [nq, w],
         anns uint32 [nq, w]): numpy views of that step's pinned answer."""
         ev = self._done_ev[ticket]
-        if self.G > 1:
+        if self.X:
             wait_event_with_deadline(ev, self.timeout_s)
         else:
             ev.synchronize()

@@ -401,6 +401,12 @@ class DeviceIndex:
                 self.corpus[a:b] = self.corpus[a:b][order]
                 self.inv_norm[a:b] = self.inv_norm[a:b][order]
                 self.gpos[a:b] = self.gpos[a:b][order]
+                # the row arrays that share corpus's local row index (the
+                # split mode's float32 rows, the float64 rows) move with it
+                for name in ("corpus32", "inv_norm32", "corpus64"):
+                    t = getattr(self, name)
+                    if t is not None:
+                        t[a:b] = t[a:b][order]
             for j in range(nch):
                 ra, rb = a + j * cr, min(b, a + (j + 1) * cr)
                 v = (self.corpus[ra:rb, :d].float() * self.inv_norm[ra:rb, None]).sum(dim=0)
@@ -586,13 +592,16 @@ def bucket_topk(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: i
 def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, k: int,
                     qmode: Optional[int] = None, eps: Optional[float] = None, stream=None,
                     fallback_count: bool = False, out=None, ws=None, seed_round0: bool = False,
-                    phases: int = 0):
+                    phases: int = 0, band_x=None):
     """K2 with float64 distances (lmi_bucket_topk_f64): the reference's
     arithmetic when either operand is not float32 (utils.py:11, :19).  Returns
     (d f64 [nq,R,k], pos [nq,R,k] int32, status int32 tensor[, n_fallback]);
     `out` and `ws` as bucket_topk.  Float64 queries whose float32 rounding
     changes them are kept for the float64 recomputation (lmi_bucket_topk_f64q;
-    the scan reads them rounded)."""
+    the scan reads them rounded).  `band_x` = (kth_send, kth_all, G): the
+    band decided over G ranks (lmi_bucket_topk_f64g, ABI 10; kth_send f32
+    [nq*R*k] written by the MERGE phase, kth_all f32 [G, nq*R*k] read by the
+    REFINE phase, LMI_Q_PHASE_REFINE in `phases`)."""
     lib = _lib.load()
     q64 = None
     if isinstance(q, torch.Tensor) and q.dtype == torch.float64 or \
@@ -630,16 +639,33 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     if index.storage == "f32x":
         seed_round0 = False  # (the split mode scans every pair whole)
     flags = (_lib.LMI_Q_SEED_ROUND0 if seed_round0 else 0) | phases
-    check("lmi_bucket_topk_f64q", lib.lmi_bucket_topk_f64q(
-        C.byref(desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
-        ptr(classes), R, k, qmode | flags, float(eps), ptr(out_d), ptr(out_pos), ptr(status),
-        ptr(ws), ws.numel(), s))
+    if band_x is not None:
+        kth_send, kth_all, G = band_x
+        check("lmi_bucket_topk_f64g", lib.lmi_bucket_topk_f64g(
+            C.byref(desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
+            ptr(classes), R, k, qmode | flags, float(eps), ptr(kth_send), ptr(kth_all), int(G),
+            nq * R * k, ptr(out_d), ptr(out_pos), ptr(status), ptr(ws), ws.numel(), s))
+    else:
+        check("lmi_bucket_topk_f64q", lib.lmi_bucket_topk_f64q(
+            C.byref(desc), ptr(q), nq, q.stride(0), ptr(q64), 0 if q64 is None else q64.stride(0),
+            ptr(classes), R, k, qmode | flags, float(eps), ptr(out_d), ptr(out_pos), ptr(status),
+            ptr(ws), ws.numel(), s))
     if not fallback_count:
         return out_d, out_pos, status
     n = C.c_int32(0)
     check("lmi_refine_fallback_count", lib.lmi_refine_fallback_count(
         ptr(ws), C.byref(desc), nq, R, k, qmode, C.byref(n), s))
     return out_d, out_pos, status, int(n.value)
+
+
+def global_band(index: DeviceIndex, nq: int, R: int, k: int, qmode: int) -> bool:
+    """True when the float64 search of a striped index can decide its band
+    over every rank's lists (lmi_f64_global_band: the band lists, k <= 10 on
+    the fp16 scan, no split mode); LMI_F64_LOCAL_BAND=1 turns it off (every
+    rank refines the band of its own list, the round-5 form)."""
+    if os.environ.get("LMI_F64_LOCAL_BAND") == "1":
+        return False
+    return bool(_lib.load().lmi_f64_global_band(C.byref(index.desc_for(k)), nq, R, k, qmode))
 
 
 def merge_topk(d_in: torch.Tensor, pos_in: torch.Tensor, k: int, stream=None):
@@ -766,10 +792,27 @@ class Searcher:
 
     ``search`` times like search.py:116-141 (router + scan + merge + replay)."""
 
-    def __init__(self, index: DeviceIndex, router: DeviceRouter, group=None):
+    def __init__(self, index: DeviceIndex, router: DeviceRouter, group=None,
+                 exchange: Optional[bool] = None):
+        """`exchange`: run the list exchange (route_sharded, K2 into the packed
+        send buffer, the all-gather, lmi_merge_topk_packed) over the process
+        group.  None (default): when a group is initialised and the index is
+        a stripe of a G > 1 index, the group has G > 1 ranks, or
+        LMI_FORCE_EXCHANGE=1 (li.dist.force_exchange: a one-rank RCCL group
+        then takes the G > 1 branch of every step form, so the exchange runs
+        on one GPU exactly as on eight)."""
+        import torch.distributed as tdist
+        from .dist import force_exchange
         self.index = index
         self.router = router
         self.group = group
+        grouped = tdist.is_available() and tdist.is_initialized()
+        if exchange is None:
+            exchange = grouped and (index.world > 1 or tdist.get_world_size(group) > 1
+                                    or force_exchange())
+        if exchange and not grouped:
+            raise ValueError("the list exchange needs an initialised process group")
+        self.exchange = bool(exchange)
         self._pinned = {}
         self._qcheck = None
 
@@ -809,20 +852,36 @@ class Searcher:
         `status_out` (a zeroed device int32 word): the status lands there.
         `ws`: a caller-owned scan workspace (GraphedSearch's)."""
         out = None
-        if self.index.world == 1 and status_out is not None:
+        if not self.exchange and status_out is not None:
             nq, R = classes.shape
             dev = self.index.device
             out = (torch.empty((nq, R, k_list), dtype=torch.float64 if f64 else torch.float32,
                                device=dev),
                    torch.empty((nq, R, k_list), dtype=torch.int32, device=dev), status_out)
-        if self.index.world > 1:
+        if self.exchange:
             # the lists and the status word land in this rank's slice of the
             # all-gather's packed send buffer (li.dist.packed_lists)
             from .dist import packed_lists
             nq, R = classes.shape
             buf, dv, pv, sv = packed_lists(nq * R, k_list, f64, self.index.device)
             out = (dv.view(nq, R, k_list), pv.view(nq, R, k_list), sv)
-        if f64:
+        if f64 and self.exchange and global_band(self.index, nq, R, k_list, qmode):
+            # the band decided over every rank's lists (ABI 10): the ranks'
+            # k smallest d32 per pair are all-gathered between the chunk merge
+            # and the float64 refinement, so each rank refines only its own
+            # rows of the merged band (DESIGN.md §6)
+            from .dist import _all_gather
+            G = torch.distributed.get_world_size(self.group)
+            kth = torch.empty((nq * R * k_list,), dtype=torch.float32, device=q_search.device)
+            kall = torch.empty((G, nq * R * k_list), dtype=torch.float32, device=q_search.device)
+            ph = _lib.LMI_Q_PHASE_PLAN | _lib.LMI_Q_PHASE_SCAN | _lib.LMI_Q_PHASE_MERGE
+            bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode, out=out, ws=ws,
+                            seed_round0=seed_round0, phases=ph, band_x=(kth, None, G))
+            _all_gather(kall.view(-1), kth, self.group)
+            d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode,
+                                             out=out, ws=ws, seed_round0=seed_round0,
+                                             phases=_lib.LMI_Q_PHASE_REFINE, band_x=(None, kall, G))
+        elif f64:
             d, pos, status = bucket_topk_f64(self.index, q_search, classes, k_list, qmode=qmode,
                                              out=out, ws=ws, seed_round0=seed_round0)
         else:
@@ -830,7 +889,7 @@ class Searcher:
                                          ws=ws, seed_round0=seed_round0)
         if lap:
             lap("scan")
-        if self.index.world > 1:
+        if self.exchange:
             from .dist import gather_merge_packed
             d, pos, status = gather_merge_packed(buf, nq * R, k_list, f64, self.group,
                                                  status_out=status_out)
@@ -851,7 +910,7 @@ class Searcher:
     def route(self, q_nav, R: int) -> torch.Tensor:
         """K1 classes [nq, R]; with G > 1 ranks each routes nq/G queries and
         the classes are all-gathered (li.dist.route_sharded)."""
-        if self.index.world > 1:
+        if self.exchange:
             from .dist import route_sharded
             return route_sharded(self.router, _rows_f32(q_nav, self.index.device), R, self.group)
         return self.router.topr(q_nav, R)[0]

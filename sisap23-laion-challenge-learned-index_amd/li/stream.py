@@ -43,7 +43,7 @@ import torch
 from . import _lib
 from ._host import host_array, stage_rows_f16, stage_rows_f32, wait_event_with_deadline
 from .index import _SEED_ROUND0, answer_buffer, answer_views, bucket_topk, bucket_topk_f64, \
-    replay_device
+    global_band, replay_device
 
 
 def _runs_beside(a, b, spin, wait_s):
@@ -129,21 +129,23 @@ class StreamedSearch:
 
     def __init__(self, searcher, q_nav, q_search, R: int, k: int = 10, *,
                  k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True, lookahead: bool = True):
+                 capture: bool = True, lookahead: bool = True, kth_peers=None):
         s = searcher
         ix = s.index
         dev = ix.device
         lib = _lib.load()
         self.searcher, self.R, self.k, self.k_round = s, R, k, k_round
         self.use_threshold, self.dist = use_threshold, dist
-        grouped = ix.world > 1 and torch.distributed.is_initialized()
-        # the list exchange spans the process group's ranks (a stripe of a
-        # G-way index in a process without a group: the rank's own lists)
-        self.G = G = torch.distributed.get_world_size(s.group) if grouped else 1
-        self.g = g = torch.distributed.get_rank(s.group) if grouped else 0
+        # the list exchange spans the process group's ranks (Searcher.exchange;
+        # a stripe of a G-way index in a process without a group: the rank's
+        # own lists).  X: the exchange branch -- G > 1, or a one-rank group
+        # under LMI_FORCE_EXCHANGE=1 (the same graphs, RCCL over one rank)
+        self.X = X = s.exchange
+        self.G = G = torch.distributed.get_world_size(s.group) if X else 1
+        self.g = g = torch.distributed.get_rank(s.group) if X else 0
         if k_round > _lib.LMI_MAX_K:
             raise ValueError("the phased scan needs k_round <= 16")
-        if capture and G > 1 and torch.distributed.get_backend(s.group) != "nccl":
+        if capture and X and torch.distributed.get_backend(s.group) != "nccl":
             raise ValueError("graph capture needs RCCL collectives (capture=False runs the "
                              "stages eagerly, e.g. over gloo)")
         if lookahead not in (True, False):
@@ -158,7 +160,7 @@ class StreamedSearch:
         f64 = dist == "f64"
         self.w = k_round if R == 1 else k
         kl = k_round
-        NS = self.NS
+        NS, X = self.NS, self.X
         self.per = per = -(-nq // G)                 # rows of a rank's block
         self.lo, self.hi = min(nq, g * per), min(nq, (g + 1) * per)
         wq = d // 2                                  # int32 words per fp16 row
@@ -167,7 +169,7 @@ class StreamedSearch:
         # H2D moves everything before the classes
         self.o_q, self.o_flag = per * dn, per * (dn + wq)
         self.o_cls = self.staged_words = self.o_flag + 2
-        self.bw = self.o_cls + (per * R if G > 1 else 0)
+        self.bw = self.o_cls + (per * R if X else 0)
         pin = torch.cuda.is_available()
         self.h_stage = [torch.zeros((self.bw,), dtype=torch.int32, pin_memory=pin) for _ in range(NS)]
         self.q32 = [torch.empty((G * per, d), dtype=torch.float32, device=dev) for _ in range(NS)]
@@ -179,7 +181,7 @@ class StreamedSearch:
         self.h_ans = [torch.empty((3 * nq * self.w + 2,), dtype=torch.int32, pin_memory=pin)
                       for _ in range(NS)]
         ldt = torch.float64 if f64 else torch.float32
-        if G > 1:
+        if X:
             # exchange buffer j: [packed lists of slot j (lmi_packed_rank_words)
             # | the block of slot j-1]; gathered into xall[j] by F1 of slot j
             wl = int(lib.lmi_packed_rank_words(nq * R, kl, int(f64)))
@@ -209,10 +211,33 @@ class StreamedSearch:
         self.timeout_s = float(os.environ.get("LMI_DIST_TIMEOUT_S", "300"))
         NF = _lib.LMI_STATUS_QUERY_NOT_F16
 
-        def phase(j, ph):
+        # float64 at G > 1 (ABI 10): the band decided over every rank's lists
+        # -- the MERGE phase writes the pairs' k smallest d32 (kth), F1
+        # all-gathers them (kall) before the REFINE phase, so each rank
+        # refines only its rows of the merged band (Searcher._scan's form)
+        # (`kth_peers`, measurement only: a one-rank rehearsal of one stripe
+        # of a G'-rank index, tools/stream_steps.py -- the other stripes' kth
+        # blocks of the batch, [G' - 1, nq*R*k], held beside the gathered one,
+        # so the REFINE phase sees the G'-rank band)
+        self.gband = gband = f64 and X and global_band(ix, nq, R, kl, _lib.LMI_Q_F16)
+        Gk = G
+        if gband:
+            nk = nq * R * kl
+            if kth_peers is not None:
+                if G != 1 or tuple(kth_peers.shape[1:]) != (nk,):
+                    raise ValueError("kth_peers needs a one-rank group and [G' - 1, nq*R*k] blocks")
+                Gk = 1 + int(kth_peers.shape[0])
+            self.kth = [torch.empty((nk,), dtype=torch.float32, device=dev) for _ in range(NS)]
+            self.kall = [torch.empty((Gk * nk,), dtype=torch.float32, device=dev) for _ in range(NS)]
+            if kth_peers is not None:
+                for kall in self.kall:
+                    kall[nk:].copy_(kth_peers.reshape(-1))
+
+        def phase(j, ph, band_x=None):
             dl, pl, st = self.lists[j]
+            kw = {} if band_x is None else {"band_x": band_x}
             scan_fn(ix, self.q32[j][:nq], self.cls[j][:nq], kl, qmode=_lib.LMI_Q_F16,
-                    out=(dl, pl, st), ws=self.ws[j], seed_round0=seed, phases=ph)
+                    out=(dl, pl, st), ws=self.ws[j], seed_round0=seed, phases=ph, **kw)
 
         def upload(j):
             self.d_blk[j][:self.staged_words].copy_(self.h_stage[j][:self.staged_words],
@@ -224,7 +249,7 @@ class StreamedSearch:
             # into the block (gathered with it)
             blk = self.d_blk[j]
             nav_d = blk[:self.o_q].view(torch.float32).view(per, dn)
-            if G == 1:
+            if not X:
                 s.router.topr(nav_d, R, out=self.cls[j])
             else:
                 s.router.topr(nav_d, R, out=blk[self.o_cls:self.o_cls + per * R])
@@ -235,7 +260,7 @@ class StreamedSearch:
 
         def plan(j):
             st = self.lists[j][2]
-            if G == 1:
+            if not X:
                 blk = self.d_blk[j]
                 self.q32[j].copy_(blk[self.o_q:self.o_flag].view(torch.float16).view(nq, d))
                 # the scan's status word starts with the staged block's
@@ -257,14 +282,20 @@ class StreamedSearch:
             phase(j, _lib.LMI_Q_PHASE_SCAN)
 
         def finish1(j):
-            phase(j, _lib.LMI_Q_PHASE_MERGE)
-            if G > 1:
+            if gband:
+                from .dist import _all_gather
+                phase(j, _lib.LMI_Q_PHASE_MERGE, band_x=(self.kth[j], None, G))
+                _all_gather(self.kall[j][:G * self.kth[j].numel()], self.kth[j], s.group)
+                phase(j, _lib.LMI_Q_PHASE_REFINE, band_x=(None, self.kall[j], Gk))
+            else:
+                phase(j, _lib.LMI_Q_PHASE_MERGE)
+            if X:
                 xgather(j)
 
         def finish2(j):
             buf, ad, aa, ast = self.ans[j]
             # (the replay status word was zeroed by the plan's GROUPS phase)
-            if G > 1:
+            if X:
                 dd = torch.empty((nq * R, kl), dtype=ldt, device=dev) if self._mdd[j] is None \
                     else self._mdd[j]
                 pp = torch.empty((nq * R, kl), dtype=torch.int32, device=dev) if self._mpp[j] is None \
@@ -298,6 +329,7 @@ class StreamedSearch:
         self._up, self._rdone, self._pdone, self._sdone = ev(), ev(), ev(), ev()
         self._gdone, self._fdone = ev(), ev()
         self.graphs = None
+        self._closed = False
         self._t = None  # launch counter once primed
         self.launches = 0  # step() calls so far (all primes)
         # measurement only: HIP events on the scan's stream around every scan
@@ -323,7 +355,7 @@ class StreamedSearch:
             torch.cuda.synchronize(dev)
         except Exception as e:  # noqa: BLE001 (re-raised below on every rank)
             err = e
-        if G > 1:
+        if X:
             ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
             torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.MIN, group=s.group)
             if int(ok.item()) == 0:
@@ -332,7 +364,7 @@ class StreamedSearch:
             raise err
         if capture:
             # one graph per (stage, slot); F is F1 + F2 at G > 1
-            names = ("R", "P", "S") + (("F1", "F2") if G > 1 else ("F",))
+            names = ("R", "P", "S") + (("F1", "F2") if X else ("F",))
             self.graphs = {}
             for name in names:
                 for j in range(NS):
@@ -341,6 +373,47 @@ class StreamedSearch:
                         self._f[name](j)
                     self.graphs[name, j] = gr
             torch.cuda.synchronize(dev)
+
+    # -- lifetime ------------------------------------------------------------
+    def drain(self):
+        """Wait for every piece of work this object enqueued: its finish, plan
+        and route streams, and the scans it launched on the caller's stream
+        (with `lookahead` the next launch's scan is still in flight when
+        step() returns)."""
+        if getattr(self, "_closed", True):
+            return
+        for evs in (self._up, self._rdone, self._pdone, self._sdone, self._gdone, self._fdone):
+            for e in evs:
+                e.synchronize()
+        for st in (self._fs, self._ps, self._rs):
+            st.synchronize()
+
+    def close(self):
+        """drain(), then release the captured graphs (and with them their
+        private memory pools and kernel-argument buffers).  The cause of
+        round 5's abort (STUDIES.md, "stream objects"): a StreamedSearch
+        dropped right after step() had its graphs destroyed while its
+        lookahead scan graph was still queued on the device; the destroyed
+        executable's kernel arguments and the graph pool's blocks (returned
+        to the caching allocator and handed to the next object) were then
+        still in use by the GPU.  Idempotent; step() after close() raises."""
+        if getattr(self, "_closed", True):
+            return
+        self.drain()
+        self.graphs = None
+        self._closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown: torch may be gone)
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     # -- staging -------------------------------------------------------------
     def stage(self, q_nav, q_search, slot: Optional[int] = None) -> bool:
@@ -373,7 +446,7 @@ class StreamedSearch:
     # -- launches --------------------------------------------------------------
     def _fill(self, j, upto):
         """Slot j's stages eagerly, in order, up to `upto` (fill and drain)."""
-        order = ("U", "R") + (("X",) if self.G > 1 else ()) + ("P", "S", "F")
+        order = ("U", "R") + (("X",) if self.X else ()) + ("P", "S", "F")
         for name in order:
             if name == "X":
                 self._f["X"]((j + 1) % self.NS)  # the exchange buffer holding slot j's block
@@ -438,10 +511,12 @@ class StreamedSearch:
 
         With `lookahead` the next launch's scan (slot t+3, planned a launch
         earlier) is enqueued too, behind this launch's finish on the device."""
+        if self._closed:
+            raise RuntimeError("StreamedSearch: step() after close()")
         if self._t is None:
             self.prime()
         dev = self.searcher.index.device
-        NS, G = self.NS, self.G
+        NS, X = self.NS, self.X
         t = self._t % NS
         jr, js, jf = t, (t + 2) % NS, (t + 1) % NS
         main = torch.cuda.current_stream(dev)
@@ -458,13 +533,13 @@ class StreamedSearch:
         with torch.cuda.stream(self._rs):
             self._run("R", jr)
         self._rdone[jr].record(self._rs)
-        if G == 1:
+        if not X:
             self._ps.wait_event(self._rdone[jr])
             with torch.cuda.stream(self._ps):
                 self._run("P", jr)
             self._pdone[jr].record(self._ps)
         self._fs.wait_event(self._sdone[jf])
-        if G == 1:
+        if not X:
             with torch.cuda.stream(self._fs):
                 self._run("F", jf)
         else:
@@ -488,7 +563,7 @@ class StreamedSearch:
         self._s_ahead = bool(self.lookahead)
         self._t += 1
         self.launches += 1
-        if G > 1 and self.graphs is not None:
+        if X and self.graphs is not None:
             wait_event_with_deadline(self._fdone[jf], self.timeout_s)
         else:
             self._fdone[jf].synchronize()
@@ -525,7 +600,7 @@ class StreamedSearch:
         one launch per batch, then the last three finish eagerly.  A batch
         that is not fp16-exact is answered by Searcher.search instead."""
         dev = self.searcher.index.device
-        NS = self.NS
+        NS, X = self.NS, self.X
         sync = lambda: torch.cuda.current_stream(dev).synchronize()
         it = iter(batches)
         held = {}
@@ -570,6 +645,7 @@ class StreamedSearch:
         self._f["S"](j3)
         self._f["F"](j3)
         sync()
+        self.drain()
         yield self._take(j3, held[j3])
         self._t = None
         self._s_ahead = False

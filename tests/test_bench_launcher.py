@@ -23,6 +23,9 @@ RANK_SCRIPT = textwrap.dedent("""
     dist.init_process_group("gloo", rank=rank, world_size=world)
     t = torch.tensor([float(rank + 1)])
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0 and "--big" in sys.argv:
+        print("x" * 300000)   # more than a pipe buffer, before the collective
+    dist.barrier()
     if rank == 0:
         print(json.dumps({"n_gpus": world, "max": float(t), "local": os.environ["LOCAL_RANK"]}))
     dist.barrier()
@@ -55,3 +58,16 @@ def test_launcher_fails_when_a_rank_fails(script, monkeypatch):
     monkeypatch.setenv("LMI_DIST_BACKEND", "gloo")
     rc = bench.launch_ranks(2, ["--fail"], script=script)
     assert rc == 3
+
+
+def test_launcher_relays_more_than_a_pipe_buffer(script, capfd, monkeypatch):
+    """Rank 0 writes 300 KB to stdout before a collective: the relay does not
+    block it (an unread pipe would, leaving the other rank at the barrier)."""
+    import bench
+    monkeypatch.setenv("LMI_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("LMI_DIST_TIMEOUT_S", "60")
+    rc = bench.launch_ranks(2, ["--big"], script=script)
+    assert rc == 0
+    out = capfd.readouterr().out.strip().splitlines()
+    assert len(out[-2]) == 300000
+    assert json.loads(out[-1])["n_gpus"] == 2

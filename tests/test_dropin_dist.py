@@ -79,3 +79,46 @@ def test_gpus_arg():
     assert gpus_arg(["--size", "10M", "--gpus", "8"]) == 8
     assert gpus_arg(["--gpus=2"]) == 2
     assert gpus_arg(["-bp", "4"]) == 1
+
+
+def _slow_build_worker(rank, world, port, out_dir):
+    """Rank 0 builds for longer than the process group's timeout (3 s here):
+    the other ranks wait on the store (LearnedIndex._build_done), so the
+    broadcast after it does not time out; a second build that
+    fails on rank 0 raises on every rank."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", LMI_DIST_TIMEOUT_S="3")
+    from li.LearnedIndex import LearnedIndex
+    from li.model import NeuralNetwork
+    li = LearnedIndex()
+    pg = li._proc_group()
+    built = None
+    if rank == 0:
+        time.sleep(6.0)
+        torch.manual_seed(7)
+        li.model = NeuralNetwork(input_dim=96, output_dim=16, lr=0.01, model_type="MLP")
+        built = (li.model, np.arange(50) % 16)
+    li._build_done(pg, None)
+    labels = li._share_build(pg, built, 96, 16, 0.01, "MLP")
+    failed = ""
+    try:
+        if rank == 0:
+            li._build_done(pg, "ValueError('boom')")
+        else:
+            li._build_done(pg, None)
+    except RuntimeError as e:
+        failed = str(e)
+    with open(os.path.join(out_dir, f"r{rank}.txt"), "w") as f:
+        f.write(f"{int(np.asarray(labels).sum())}|{failed}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_slow_rank0_build_does_not_time_out_the_other_ranks(tmp_path):
+    world = 3
+    mp.spawn(_slow_build_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = [(tmp_path / f"r{r}.txt").read_text().split("|") for r in range(world)]
+    assert all(g[0] == got[0][0] for g in got)
+    assert got[0][1] == ""
+    assert all("boom" in g[1] for g in got[1:])

@@ -198,3 +198,28 @@ def test_split_dropin_baseline_matches_reference(name):
     dists, nns, _ = Baseline().search(q32, x32, k=k)
     ref_d, ref_n = G5[f"base_{name}__dists"], G5[f"base_{name}__nns"]
     assert O.compare_lists(ref_d, ref_n, dists, nns, atol=1e-5, tie=1e-6) == 0
+
+
+@pytest.mark.parametrize("k", [10, 30])
+def test_split_subcluster_layout_moves_the_float32_rows(k):
+    """subcluster=True reorders the rows inside each bucket; the split mode's
+    float32 rows (the exact re-score's and the k > 16 scan's input) and their
+    norms move with them: the lists equal the oracle's and the
+    plain layout's."""
+    w, x, q = _x("near", 651, n=6000)
+    C, R = w["C"], 2
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    cls = T(classes.astype(np.int32))
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=256, device="cuda", subcluster=True)
+    assert ix.storage == "f32x" and ix.chunk_centroid is not None
+    d, p, st = bucket_topk(ix, T(q), cls, k)
+    assert int(st.item()) == 0
+    ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, R, k, C)
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-5, tie=1e-6) == 0
+    if k <= 16:
+        q64 = q.astype(np.float64)
+        d64, p64, st64 = bucket_topk_f64(ix, T(q64), cls, k)
+        ref_d64, ref_p64 = O.bucket_lists(w["labels"], x, q64, classes, R, k, C)
+        assert O.compare_lists(ref_d64, ref_p64, d64.cpu().numpy(), p64.cpu().numpy(), atol=1e-12,
+                               tie=1e-12) == 0
+

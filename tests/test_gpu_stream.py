@@ -179,3 +179,45 @@ def test_queue_streams_run_beside_each_other():
         assert _runs_beside(main, s, spin, 5e-3)
         for o in ss[:i]:
             assert _runs_beside(o, s, spin, 5e-3)
+
+
+def test_stream_objects_dropped_with_work_in_flight(setup):
+    """a StreamedSearch dropped right after step() (its
+    lookahead scan still queued) and a new one on the very same streams: the
+    old object's __del__ -> close() waits for its work before its graphs and
+    their pools are released, so the new object's answers are bitwise those
+    of Searcher.search.  Twice, back to back."""
+    import gc
+    w, s = setup
+    bs = _batches(w, 5, seed=77)
+    ref = [s.search(T(a), T(b), 4, k=10) for a, b in bs]
+    saved = None
+    for rep in range(2):
+        st = s.streamed(w["qn"], w["q"], 4, k=10, lookahead=True)
+        if saved is not None:
+            st._fs, st._ps, st._rs = saved   # the streams deliberately shared
+            st._cs = st._rs
+        got = list(st.stream(bs))
+        for (d, a), (d0, a0) in zip(got, ref):
+            np.testing.assert_array_equal(d, d0)
+            np.testing.assert_array_equal(a, a0)
+        assert st.launches == len(bs) - 3
+        st.stage(*bs[0])
+        st.step()                            # leaves its lookahead scan in flight
+        saved = (st._fs, st._ps, st._rs)
+        del st
+        gc.collect()                         # (the stage closures hold a cycle)
+
+
+def test_close_is_idempotent_and_final(setup):
+    w, s = setup
+    st = s.streamed(w["qn"], w["q"], 4, k=10)
+    st.step()
+    st.close()
+    st.close()
+    assert st.graphs is None
+    with pytest.raises(RuntimeError):
+        st.step()
+    with s.streamed(w["qn"], w["q"], 4, k=10) as st2:
+        st2.step()
+    assert st2.graphs is None
