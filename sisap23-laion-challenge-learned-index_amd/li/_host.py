@@ -93,3 +93,58 @@ def wait_with_deadline(dev, timeout_s: float) -> None:
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(dev))
     wait_event_with_deadline(ev, timeout_s)
+
+
+# ---- graph lifetime ---------------------------------------------------------
+# The round-5 abort, root-caused in round 6 (DESIGN.md §5 "Graph lifetime"):
+# a StreamedSearch holds its stage closures, which hold the object -- a
+# reference cycle -- so a dropped object is freed by the cyclic garbage
+# collector, at whatever allocation triggers it.  When that allocation sat
+# inside ANOTHER object's graph capture, the collector ran the old object's
+# finalisers there: destroying a graph executable and releasing its private
+# memory pool (or synchronising an event) while a stream capture is underway
+# aborts the process.  So: (1) captures run with the collector off
+# (`no_gc_capture`), and (2) a finaliser that runs while a capture is
+# underway anyway (another library's capture) parks the graphs instead of
+# destroying them (`release_later`); they are destroyed at the next safe
+# point (`flush_released`, after a device synchronisation).
+_PARKED = []
+
+
+def capture_underway() -> bool:
+    """True while the current stream is capturing a graph."""
+    try:
+        return bool(torch.cuda.is_available() and torch.cuda.is_current_stream_capturing())
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def release_later(*objs) -> None:
+    """Keep `objs` (graphs, their buffers) alive until flush_released()."""
+    _PARKED.append(objs)
+
+
+def flush_released() -> None:
+    """Destroy the parked graphs once no capture is underway (after a device
+    synchronisation: their last replays may still be queued)."""
+    if _PARKED and not capture_underway():
+        torch.cuda.synchronize()
+        _PARKED.clear()
+
+
+class no_gc_capture:
+    """Context manager around a block of graph captures: the cyclic garbage
+    collector is off inside (torch.cuda.graph itself collects before each
+    capture begins), so no finaliser runs mid-capture."""
+
+    def __enter__(self):
+        import gc
+        flush_released()
+        self._was = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        import gc
+        if self._was:
+            gc.enable()

@@ -11,8 +11,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._host import host_array, np_fp16_exact, stage_rows_f16, stage_rows_f32, \
-    wait_event_with_deadline, wait_with_deadline
+from ._host import capture_underway, host_array, no_gc_capture, np_fp16_exact, release_later, \
+    stage_rows_f16, stage_rows_f32, wait_event_with_deadline, wait_with_deadline
 from .index import _SEED_ROUND0, _as_torch, answer_buffer, answer_views, replay_device
 
 
@@ -227,13 +227,14 @@ class GraphedSearch:
                    for _ in range(2 if self.pipeline else 1)]
         self.h = self.hs[0]
         self.graphs, self._keep = [], []
-        for slot in range(2 if self.pipeline else 1):
-            gr = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gr):
-                buf = step(slot)
-                self.hs[slot].copy_(buf, non_blocking=True)
-            self.graphs.append(gr)
-            self._keep.append(buf)
+        with no_gc_capture():   # (li._host "graph lifetime")
+            for slot in range(2 if self.pipeline else 1):
+                gr = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gr):
+                    buf = step(slot)
+                    self.hs[slot].copy_(buf, non_blocking=True)
+                self.graphs.append(gr)
+                self._keep.append(buf)
         self.graph = self.graphs[0]
         self._slot = 0
         self._fresh = [True, True]   # d_blks[slot] holds the staged batch
@@ -250,10 +251,13 @@ class GraphedSearch:
         kernel arguments).  Idempotent."""
         if getattr(self, "graphs", None) is None:
             return
-        for name in ("_done_ev", "_up_ev"):
-            for e in getattr(self, name, ()):
-                e.synchronize()
-        self._cs.synchronize()
+        if capture_underway():
+            release_later(self.graphs, self._keep, self.ws)
+        else:
+            for name in ("_done_ev", "_up_ev"):
+                for e in getattr(self, name, ()):
+                    e.synchronize()
+            self._cs.synchronize()
         self.graphs, self.graph = None, None
 
     def __del__(self):

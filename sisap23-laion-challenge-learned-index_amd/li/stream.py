@@ -41,7 +41,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._host import host_array, stage_rows_f16, stage_rows_f32, wait_event_with_deadline
+from ._host import capture_underway, host_array, no_gc_capture, release_later, stage_rows_f16, \
+    stage_rows_f32, wait_event_with_deadline
 from .index import _SEED_ROUND0, answer_buffer, answer_views, bucket_topk, bucket_topk_f64, \
     global_band, replay_device
 
@@ -363,15 +364,17 @@ class StreamedSearch:
         elif err is not None:
             raise err
         if capture:
-            # one graph per (stage, slot); F is F1 + F2 at G > 1
+            # one graph per (stage, slot); F is F1 + F2 at G > 1 (the garbage
+            # collector off meanwhile: li._host "graph lifetime")
             names = ("R", "P", "S") + (("F1", "F2") if X else ("F",))
             self.graphs = {}
-            for name in names:
-                for j in range(NS):
-                    gr = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(gr):
-                        self._f[name](j)
-                    self.graphs[name, j] = gr
+            with no_gc_capture():
+                for name in names:
+                    for j in range(NS):
+                        gr = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(gr):
+                            self._f[name](j)
+                        self.graphs[name, j] = gr
             torch.cuda.synchronize(dev)
 
     # -- lifetime ------------------------------------------------------------
@@ -380,7 +383,7 @@ class StreamedSearch:
         and route streams, and the scans it launched on the caller's stream
         (with `lookahead` the next launch's scan is still in flight when
         step() returns)."""
-        if getattr(self, "_closed", True):
+        if getattr(self, "_closed", True) or capture_underway():
             return
         for evs in (self._up, self._rdone, self._pdone, self._sdone, self._gdone, self._fdone):
             for e in evs:
@@ -390,16 +393,21 @@ class StreamedSearch:
 
     def close(self):
         """drain(), then release the captured graphs (and with them their
-        private memory pools and kernel-argument buffers).  The cause of
-        round 5's abort (STUDIES.md, "stream objects"): a StreamedSearch
-        dropped right after step() had its graphs destroyed while its
-        lookahead scan graph was still queued on the device; the destroyed
-        executable's kernel arguments and the graph pool's blocks (returned
-        to the caching allocator and handed to the next object) were then
-        still in use by the GPU.  Idempotent; step() after close() raises."""
+        private memory pools and kernel-argument buffers): a StreamedSearch
+        dropped right after step() still has its lookahead scan graph queued
+        on the device, and destroying that executable and handing its pool's
+        blocks to the caching allocator while the GPU still uses them is
+        unsafe.  Inside another object's capture nothing is synchronised or
+        destroyed: the graphs are parked (li._host "graph lifetime", the
+        root cause of round 5's abort).  Idempotent; step() after close()
+        raises."""
         if getattr(self, "_closed", True):
             return
-        self.drain()
+        if capture_underway():
+            # (a finaliser inside another capture: park the graphs, li._host)
+            release_later(self.graphs, self.ws, self.rws, self.lists, self.xall)
+        else:
+            self.drain()
         self.graphs = None
         self._closed = True
 

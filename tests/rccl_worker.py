@@ -65,10 +65,14 @@ def main():
         assert len(got) == len(batches) and ss.launches == len(batches) - 3
         for o, r in zip(got, ref):
             eq(o, r)
-        # step() per launch on one staged batch, the bench's use
+        ss.close()
+        # step() per launch on one staged batch, the bench's use (a new
+        # object: after stream() the slots hold the stream's last batches)
         r0 = s0.search(qn, q, 4, k=10, dist=dd)
+        ss = sx.streamed(w["qn"], w["q"], 4, k=10, dist=dd)
         for _ in range(5):
             eq(ss.step(), r0)
+        assert ss.launches == 5
         ss.close()
         checks.append(f"graph/pipelined graph/stream {dd}")
     dist.barrier()

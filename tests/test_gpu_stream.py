@@ -221,3 +221,35 @@ def test_close_is_idempotent_and_final(setup):
     with s.streamed(w["qn"], w["q"], 4, k=10) as st2:
         st2.step()
     assert st2.graphs is None
+
+
+def test_object_finalised_inside_another_capture_is_parked(setup):
+    """The round-5 abort's cause, reproduced on purpose: a StreamedSearch
+    becomes cyclic garbage and the collector finalises it while another graph
+    is being captured.  Destroying its graphs (or synchronising its events)
+    there would abort the process; close() parks them instead (li._host
+    "graph lifetime"), the capture completes and replays, and the parked
+    graphs are released at the next safe point."""
+    import gc
+    from li import _host
+    w, s = setup
+    st = s.streamed(w["qn"], w["q"], 4, k=10)
+    st.step()
+    holder = [st]
+    del st
+    x = torch.zeros(4, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        holder.clear()          # the last reference: the object is now cyclic garbage
+        gc.collect()            # its finaliser runs mid-capture
+        x += 1
+    assert len(_host._PARKED) == 1
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(x.sum()) == 4
+    _host.flush_released()
+    assert not _host._PARKED
+    d0, a0 = s.search(T(w["qn"]), T(w["q"]), 4, k=10)
+    d, a = s.streamed(w["qn"], w["q"], 4, k=10).step()
+    np.testing.assert_array_equal(d, d0)
+    np.testing.assert_array_equal(a, a0)
