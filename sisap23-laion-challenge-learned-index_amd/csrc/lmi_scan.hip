@@ -1180,7 +1180,11 @@ WsLayout ws_layout(const lmi_index_desc* idx, int nq, int R, int k, int qmode, b
     const bool nearest_first = w.use_v3 && idx->chunk_centroid && !env_config().scan_no_pref;
     const bool split_on = w.use_v3 && !nearest_first && env_config().scan_split >= 0;
     w.split_s = split_on ? split_parts() : 1;
-    const size_t S = (size_t)w.split_s;
+    // (the buffers are sized for split_parts() on scan v3 whether the split
+    // is on or not, so the total and every offset do not depend on the
+    // LMI_SCAN_SPLIT / LMI_SCAN_NO_PREF knobs or on the index's centroids:
+    // a workspace sized once fits every call)
+    const size_t S = w.use_v3 ? (size_t)split_parts() : 1;
     w.tiles = take(((size_t)w.max_tiles + (size_t)kGroups * kSplitMaxK * (S - 1)) * sizeof(Tile));
     w.ntiles = take(4 * (3 * kGroups + 1));
     w.work = take(4 * (kGroups + 1));

@@ -1,8 +1,7 @@
 """Device replay (K4) timing on bench-shaped random lists: 10k queries, R=4,
-122 buckets of skewed popularity, k=10; torch events around lmi_replay_device.
-(The round-2 phase study's LMI_REPLAY_ABL stops are no longer in the library;
-profiles/r02_replay_phases.txt keeps its numbers.)  Times the whole replay and
-its ROUNDS phase alone (the part a batch stream's finish stage runs); an A/B of
+122 buckets of skewed popularity, k=10; torch events around lmi_replay_device
+(round 2's phase study and its numbers: profiles/r02_replay_phases.txt).
+Times the whole replay and its ROUNDS phase alone (the part a batch stream's finish stage runs); an A/B of
 two builds: LMI_LIB_NAME=<other .so>."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_rccl.py tests/test_gpu_f64_global.py tests/test_gpu_stream.py tests/test_gpu_dist.py \
-  tests/test_gpu_split_mode.py > gpurun_out/r6b_tests.log 2>&1
+  tests/test_gpu_split_mode.py tests/test_gpu_graph.py > gpurun_out/r6b_tests.log 2>&1
 rc=$?; tail -5 gpurun_out/r6b_tests.log; [ $rc -ne 0 ] && exit $rc
 LMI_FORCE_EXCHANGE=1 timeout -k 10 400 python bench.py --steps 10 --warmup 3 --no-cpu-baseline \
   > gpurun_out/r6b_bench_fx.json 2> gpurun_out/r6b_bench_fx.err
