@@ -298,10 +298,7 @@ void refine_kernel(RefineArgs a) {
         tg = global_kth(a.kth_all, a.kth_G, a.kth_stride, p, k);
         if (a.seeded && p % a.R != 0) tg0 = global_kth(a.kth_all, a.kth_G, a.kth_stride, p - p % a.R, k);
     }
-    // (the query's loads go out beside the list's)
     const int nps = (a.d + 255) / 256;
-    double qh[NP][4];
-    query_hat<TQ, NP>(query_of<TQ>(a, p / a.R), a.d, nps, qh);
     double* od = a.out_d + (size_t)p * k;
     int32_t* op = a.out_pos + (size_t)p * k;
     int m;
@@ -343,6 +340,19 @@ void refine_kernel(RefineArgs a) {
             return;
         }
     }
+    if (m == 0) {
+        // (no listed row in the band: the global band of a stripe holding
+        // none of the pair's merged band -- most pairs of most stripes at
+        // G = 8 -- needs no query; the list is all padding)
+        for (int j = lane; j < k; j += 64) {
+            od[j] = __builtin_inf();
+            op[j] = -1;
+        }
+        return;
+    }
+    // (the query, once the pair has rows to refine)
+    double qh[NP][4];
+    query_hat<TQ, NP>(query_of<TQ>(a, p / a.R), a.d, nps, qh);
 #pragma unroll
     for (int s = 0; s < NSL; ++s)
         if (rj[s] >= (int64_t)a.n_rows) atomicOr(a.status, LMI_STATUS_INTERNAL);

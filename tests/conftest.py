@@ -40,7 +40,21 @@ def pytest_collection_modifyitems(config, items):
 # written as JSON
 # ---------------------------------------------------------------------------
 _TIES = {}
+_BYMODE = {}
 _CURRENT = ["<collection>"]
+
+
+def _mode_key(nodeid: str, tie: float):
+    """(side, arithmetic, checked against) of one compare_lists call:
+    side "product" for the GPU tests, "oracle" for the CPU oracle-vs-reference
+    tests; arithmetic "split" for float32 data that is not fp16-exact (the
+    split mode, r5 fixtures), else "float64" (tie 1e-12) or "float32"; the
+    reference's own fixtures (golden tests) or the oracle."""
+    side = "product" if "test_gpu_" in nodeid else "oracle"
+    split = "split" in nodeid or "golden_r5" in nodeid or "[x_" in nodeid
+    arith = ("split-" if split else "") + ("float64" if tie <= 1e-12 else "float32")
+    against = "reference fixtures" if ("golden" in nodeid or "reference" in nodeid) else "oracle"
+    return side, arith, against
 
 
 def _install_tie_accounting():
@@ -60,6 +74,12 @@ def _install_tie_accounting():
         for key in ("rows", "mismatched", "tie_rows", "exact_tie_rows"):
             acc[key] += st[key]
         acc["tie"].add(st["tie"])
+        if "sharp" in _CURRENT[0]:
+            return bad  # (the sharpness tests count disagreements on purpose)
+        mk = _mode_key(_CURRENT[0], st["tie"])
+        bm = _BYMODE.setdefault(mk, {"rows": 0, "tie_rows": 0, "exact_tie_rows": 0})
+        for key in ("rows", "tie_rows", "exact_tie_rows"):
+            bm[key] += st[key]
         return bad
 
     compare_lists._counted = True
@@ -84,8 +104,14 @@ def pytest_terminal_summary(terminalreporter):
         if v["tie_rows"]:
             terminalreporter.write_line(f"  {name}: {v['tie_rows']}/{v['rows']} rows "
                                         f"({v['exact_tie_rows']} exact ties), tie={sorted(v['tie'])}")
+    terminalreporter.write_line("  by (side, arithmetic, checked against): rows / tie-window rows "
+                                "(exact ties, non-exact)")
+    for mk, v in sorted(_BYMODE.items()):
+        terminalreporter.write_line(f"    {' / '.join(mk)}: {v['rows']} / {v['tie_rows']} "
+                                    f"({v['exact_tie_rows']}, {v['tie_rows'] - v['exact_tie_rows']})")
     path = os.environ.get("LMI_TIE_REPORT")
     if path:
         out = {k: {**v, "tie": sorted(v["tie"])} for k, v in _TIES.items()}
+        out["_by_mode"] = {" / ".join(mk): v for mk, v in sorted(_BYMODE.items())}
         with open(path, "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)
