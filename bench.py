@@ -137,8 +137,16 @@ def algorithmic_bytes(index, classes, nq):
     probed = np.unique(classes)
     loc = index.bucket_off_local.cpu().numpy()
     rows = int(sum(loc[c + 1] - loc[c] for c in probed))
+    if index.storage == "f32x":
+        # the split mode's two scans (lmi_scan.hip bucket_topk_x): the sample
+        # scan over each probed bucket's first max(chunk_rows, n_c / 16) rows,
+        # then the collect scan over all its rows, both streaming the fp16
+        # rounding
+        n_c = np.array([loc[c + 1] - loc[c] for c in probed], dtype=np.int64)
+        want = np.maximum(index.chunk_rows, (n_c // 16 + 31) // 32 * 32)
+        rows += int(np.minimum(n_c, want).sum())
     s = 4 if index.storage == "f32" else 2   # (f32x: its scans stream the fp16 rounding)
-    byts = rows * (index.d_pad * s + 4) + nq * index.d_pad * s
+    byts = rows * (index.d_pad * s + 4) + nq * index.d_pad * s * (2 if index.storage == "f32x" else 1)
     sizes = np.diff(loc)
     flops = 2.0 * index.d * float(sizes[classes].sum())
     return byts, flops, rows
@@ -319,13 +327,16 @@ STEP_TEXT = {
 }
 
 
-def pmc_traffic(kernel_ms):
+def pmc_traffic(kernel_ms, split=False):
     """HBM-side bytes per scan launch from the committed rocprofv3 PMC passes
-    (tools/gpu_profile.sh -> profiles/*pmc_traffic.json): FETCH_SIZE x 2 (gfx950
-    reports half of wide streaming reads, MI355X_MICROARCH.md HBM section) +
-    WRITE_SIZE, in bytes; None when no summary is committed."""
+    (tools/gpu_profile.sh -> profiles/*pmc_traffic.json; the split mode's two
+    scans per step: tools/pmc_split.sh -> profiles/*split_pmc_traffic.json):
+    FETCH_SIZE x 2 (gfx950 reports half of wide streaming reads,
+    MI355X_MICROARCH.md HBM section) + WRITE_SIZE, in bytes; None when no
+    summary is committed."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))
+                   if ("split_pmc" in os.path.basename(f)) == split)
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -797,7 +808,8 @@ def main():
     achieved = byts / (scan_ms * 1e-3) / 1e9
     tflops = flops / (scan_ms * 1e-3) / 1e12
     # the committed PMC passes profile the default (10M, 1 GPU) command only
-    traffic, traffic_src = pmc_traffic(scan_ms) if (args.scale == "10M" and world == 1) else (None, None)
+    traffic, traffic_src = pmc_traffic(scan_ms, split=index.storage == "f32x") \
+        if (args.scale == "10M" and world == 1) else (None, None)
     # `bound` is the roof the kernel's arithmetic intensity selects: flops /
     # algorithmic bytes (401 flop/B at configs[2]) above the dense-fp16 ridge
     # (2.5 PF / 8 TB/s = 312 flop/B) means MFMA-bound, and achieved / peak /

@@ -549,91 +549,136 @@ namespace {
 // ---------------------------------------------------------------------------
 // chunk merge
 // ---------------------------------------------------------------------------
+// kMergeLanes lanes per pair (round 6; was one thread per pair): lane s of a
+// pair merges the pair's chunk lists j = s, s + kMergeLanes, ... into a
+// register list (each list read with all its loads in flight, then its global
+// positions gathered the same way; the next list's keys load while this
+// one's positions are gathered), then the lanes' lists are merged by a
+// butterfly of shuffles (log2 kMergeLanes rounds: insert the partner lane's
+// entries).  Every lane ends with the same list: the KL smallest keys of the
+// union, exactly the one-thread merge's.  At 40,000 pairs one thread per pair
+// was 625 waves for 1,024 SIMDs -- latency-bound, ~41 us at W = 8 (58 at
+// W = 1) on the finish chain's critical path.
+constexpr int kMergeLanes = 8;
+constexpr int kMergeBlock = 256;
+
+// slot of the pair's j-th list: chunks 0 .. nch_c - 1, then the other parts
+// (1 .. S-1) of the tail-split chunks in ascending chunk order (bit b of the
+// pair's mask: chunk b was split; part p lives at slot p * X + b)
+__device__ inline int chunk_slot(int j, int nch_c, uint32_t sm, int S, int X) {
+    if (j < nch_c) return j;
+    const int idx = j - nch_c;
+    int n = idx / (S - 1);
+    const int part = 1 + idx % (S - 1);
+    while (n-- > 0) sm &= sm - 1u;
+    return part * X + __builtin_ctz(sm);
+}
+
+// (the pair's list keys are (distance, local row) in the partial lists and
+// (distance, global position) in M; rows inside a chunk ascend in global
+// position, so mapping keeps each list ordered and the merge is by the
+// reference's (distance, g.index) order)
+template <int KL, int NE>
+__device__ inline void merge_chunk_list(const uint64_t (&K)[NE], uint64_t (&M)[KL], int32_t (&W)[KL],
+                                        const int32_t* __restrict__ gpos, int64_t n_rows,
+                                        int32_t* __restrict__ status) {
+    int32_t g[NE];
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+        const uint32_t lp = (uint32_t)K[i];
+        // (pre-filter on the distance part: past this lane's KL-th, an entry
+        // is past the union's too)
+        const bool live = K[i] != kEmptyKey && (K[i] >> 32) <= (M[KL - 1] >> 32);
+        const bool ok = lp < (uint32_t)n_rows;
+        if (live && !ok) atomicOr(status, LMI_STATUS_INTERNAL);  // never for a sound scan
+        g[i] = (live && ok) ? gpos[lp] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+        if (g[i] < 0) continue;
+        const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
+        if (key < M[KL - 1]) list_insert_pair<KL>(M, W, key, (int32_t)(uint32_t)K[i]);
+    }
+}
+
+// The lanes of a pair merge their lists (xor butterfly inside the pair's
+// kMergeLanes-lane group): after the rounds every lane holds the union's
+// KL smallest keys
+template <int KL>
+__device__ inline void merge_lanes(uint64_t (&M)[KL], int32_t (&W)[KL]) {
+#pragma unroll
+    for (int off = 1; off < kMergeLanes; off <<= 1) {
+        uint64_t o[KL];
+        int32_t ow[KL];
+#pragma unroll
+        for (int i = 0; i < KL; ++i) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)M[i], off);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(M[i] >> 32), off);
+            o[i] = ((uint64_t)hi << 32) | lo;
+            ow[i] = __shfl_xor(W[i], off);
+        }
+#pragma unroll
+        for (int i = 0; i < KL; ++i)
+            if (o[i] < M[KL - 1]) list_insert_pair<KL>(M, W, o[i], ow[i]);
+    }
+}
+
+// one pair's lists -> the merged list in M/W (every lane of the pair's group);
+// NE entries read per list (KL, or the band lists' kBandSlot - 1), the
+// list's slot stride LS; BAND: *ub = the smallest of the lists' bound slots
+template <int KL, int NE, int LS, bool BAND>
+__device__ inline void merge_pair(const uint64_t* __restrict__ partial, int32_t max_chunks, int pp, int nch_c,
+                                  uint32_t sm, int S, const int32_t* __restrict__ gpos, int64_t n_rows,
+                                  int32_t* __restrict__ status, int sub, uint64_t (&M)[KL], int32_t (&W)[KL],
+                                  uint32_t* ub) {
+    const int nch = nch_c + (S - 1) * __popc(sm);
+    const int X = max_chunks / S;
+    list_clear<KL>(M);
+#pragma unroll
+    for (int i = 0; i < KL; ++i) W[i] = -1;
+    uint64_t Kn[NE];
+    uint32_t ubn = 0xffffffffu;
+    auto load = [&](int j) {
+        const uint64_t* src = partial + ((size_t)pp * max_chunks + chunk_slot(j, nch_c, sm, S, X)) * LS;
+#pragma unroll
+        for (int i = 0; i < NE; ++i) Kn[i] = src[i];
+        if constexpr (BAND) ubn = (uint32_t)(src[LS - 1] >> 32);
+    };
+    if (sub < nch) load(sub);
+    for (int j = sub; j < nch; j += kMergeLanes) {
+        uint64_t K[NE];
+#pragma unroll
+        for (int i = 0; i < NE; ++i) K[i] = Kn[i];
+        if constexpr (BAND) *ub = std::min(*ub, ubn);
+        if (j + kMergeLanes < nch) load(j + kMergeLanes);
+        merge_chunk_list<KL, NE>(K, M, W, gpos, n_rows, status);
+    }
+    merge_lanes<KL>(M, W);
+}
+
 template <int KL, bool ROWS>
-__global__ __launch_bounds__(64) void chunk_merge_kernel(
+__global__ __launch_bounds__(kMergeBlock) void chunk_merge_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, int64_t n_rows,
     int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask, int32_t S) {
-    // one thread per pair, 64-thread blocks (spread over every CU); each
-    // chunk list is read with all its loads in flight, then its global
-    // positions gathered the same way, then merged into a register list
-    // (ROWS: the local row of every entry travels beside its key)
-    const int pp = blockIdx.x * 64 + threadIdx.x;
+    const int gt = blockIdx.x * kMergeBlock + threadIdx.x;
+    const int pp = gt / kMergeLanes, sub = gt % kMergeLanes;
+    // (a pair's lanes are one aligned group of a wave: they return together)
     if (pp >= P) return;
     const int c = pair_bucket[pp];
     if (c < 0) return;
     const int nch_c = chunk_first[c + 1] - chunk_first[c];
-    // (+ the other parts of tail-split chunks: slots s*X + j, s = 1..S-1, for
-    // bit j of the pair's mask, X = max_chunks / S, the stride being S*X)
-    uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
-    const int nch = nch_c + (S - 1) * __popc(sm);
-    const int X = max_chunks / S;
-    int part = S;  // part of the current split chunk (S: take the next bit)
-    int bit = 0;
-    auto slot_of = [&](int j) {
-        if (j < nch_c) return j;
-        if (part == S) {
-            bit = __builtin_ctz(sm);  // split chunks in ascending order, parts 1..S-1
-            sm &= sm - 1u;
-            part = 1;
-        }
-        return (part++) * X + bit;
-    };
+    const uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
     uint64_t M[KL];
     int32_t W[KL];
-    list_clear<KL>(M);
-#pragma unroll
-    for (int i = 0; i < KL; ++i) W[i] = -1;
-    // A chunk list is ordered by (distance, row); rows inside a chunk are in
-    // ascending global position (the index layout guarantees it), so mapping
-    // each key to (distance, global position) keeps the list ordered, and the
-    // merge across chunks is by the reference's (distance, g.index) order.
-    // (software-pipelined: chunk j+1's keys load while chunk j's positions
-    // are gathered, one memory latency per chunk instead of two)
-    uint64_t Kn[KL];
-    {
-        const uint64_t* src = partial + (size_t)pp * max_chunks * KL;
-#pragma unroll
-        for (int i = 0; i < KL; ++i) Kn[i] = nch > 0 ? src[i] : kEmptyKey;
-    }
-    for (int j = 0; j < nch; ++j) {
-        uint64_t K[KL];
-#pragma unroll
-        for (int i = 0; i < KL; ++i) K[i] = Kn[i];
-        if (j + 1 < nch) {
-            const uint64_t* src = partial + ((size_t)pp * max_chunks + slot_of(j + 1)) * KL;
-#pragma unroll
-            for (int i = 0; i < KL; ++i) Kn[i] = src[i];
-        }
-        int32_t g[KL];
-#pragma unroll
-        for (int i = 0; i < KL; ++i) {
-            const uint32_t lp = (uint32_t)K[i];
-            // (pre-filter on the distance part only: the low halves are rows
-            // here and global positions in M)
-            const bool live = K[i] != kEmptyKey && (K[i] >> 32) <= (M[KL - 1] >> 32);
-            const bool ok = lp < (uint32_t)n_rows;
-            if (live && !ok) atomicOr(status, LMI_STATUS_INTERNAL);  // never for a sound scan
-            g[i] = (live && ok) ? gpos[lp] : -1;
-        }
-#pragma unroll
-        for (int i = 0; i < KL; ++i) {
-            if (g[i] < 0) continue;
-            const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
-            if (key < M[KL - 1]) {
-                if constexpr (ROWS)
-                    list_insert_pair<KL>(M, W, key, (int32_t)(uint32_t)K[i]);
-                else
-                    list_insert<KL>(M, key);
-            }
-        }
-    }
+    merge_pair<KL, KL, KL, false>(partial, max_chunks, pp, nch_c, sm, S, gpos, n_rows, status, sub, M, W,
+                                  nullptr);
     const size_t o = (size_t)pair_q[pp] * ldo;
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
-        if (i < k) {
+        if (i < k && i % kMergeLanes == sub) {
             const uint64_t key = M[i];
             const bool empty = key == kEmptyKey;
             out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
@@ -649,77 +694,32 @@ __global__ __launch_bounds__(64) void chunk_merge_kernel(
 // 16th distance: every row of the pair's shard not in its list either failed
 // the scan's widened filter or has d32 >= out_bound (refine_kernel falls back
 // to the whole shard when that bound enters the float64 band).
-__global__ __launch_bounds__(64) void chunk_merge_band_kernel(
+__global__ __launch_bounds__(kMergeBlock) void chunk_merge_band_kernel(
     const uint64_t* __restrict__ partial, int32_t max_chunks, const int32_t* __restrict__ pair_q,
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, float* __restrict__ out_bound,
     int64_t n_rows, int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask, int32_t S) {
     constexpr int NB = kBandSlot, KB = kBandSlot - 1;
-    const int pp = blockIdx.x * 64 + threadIdx.x;
+    const int gt = blockIdx.x * kMergeBlock + threadIdx.x;
+    const int pp = gt / kMergeLanes, sub = gt % kMergeLanes;
     if (pp >= P) return;
     const int c = pair_bucket[pp];
     if (c < 0) return;
     const int nch_c = chunk_first[c + 1] - chunk_first[c];
-    uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
-    const int nch = nch_c + (S - 1) * __popc(sm);
-    const int X = max_chunks / S;
-    int part = S, bit = 0;
-    auto slot_of = [&](int j) {  // (chunk_merge_kernel's order)
-        if (j < nch_c) return j;
-        if (part == S) {
-            bit = __builtin_ctz(sm);
-            sm &= sm - 1u;
-            part = 1;
-        }
-        return (part++) * X + bit;
-    };
+    const uint32_t sm = split_mask != nullptr ? split_mask[pp] : 0u;
     uint64_t M[NB];
     int32_t W[NB];
-    list_clear<NB>(M);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) W[i] = -1;
     uint32_t ub = 0xffffffffu;
-    uint64_t Kn[NB];
-    {
-        const uint64_t* src = partial + (size_t)pp * max_chunks * NB;
+    merge_pair<NB, KB, NB, true>(partial, max_chunks, pp, nch_c, sm, S, gpos, n_rows, status, sub, M, W, &ub);
 #pragma unroll
-        for (int i = 0; i < NB; ++i) Kn[i] = nch > 0 ? src[i] : kEmptyKey;
-    }
-    for (int j = 0; j < nch; ++j) {
-        uint64_t K[NB];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) K[i] = Kn[i];
-        if (j + 1 < nch) {
-            const uint64_t* src = partial + ((size_t)pp * max_chunks + slot_of(j + 1)) * NB;
-#pragma unroll
-            for (int i = 0; i < NB; ++i) Kn[i] = src[i];
-        }
-        ub = std::min(ub, (uint32_t)(K[KB] >> 32));
-        int32_t g[KB];
-#pragma unroll
-        for (int i = 0; i < KB; ++i) {
-            const uint32_t lp = (uint32_t)K[i];
-            // (entries past the list's 16th distance only raise nothing: the
-            // 16th bounds them)
-            const bool live = K[i] != kEmptyKey && (K[i] >> 32) <= (M[NB - 1] >> 32);
-            const bool ok = lp < (uint32_t)n_rows;
-            if (live && !ok) atomicOr(status, LMI_STATUS_INTERNAL);
-            g[i] = (live && ok) ? gpos[lp] : -1;
-        }
-#pragma unroll
-        for (int i = 0; i < KB; ++i) {
-            if (g[i] < 0) continue;
-            const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
-            if (key < M[NB - 1]) list_insert_pair<NB>(M, W, key, (int32_t)(uint32_t)K[i]);
-        }
-    }
+    for (int off = 1; off < kMergeLanes; off <<= 1) ub = std::min(ub, (uint32_t)__shfl_xor((int)ub, off));
     ub = std::min(ub, (uint32_t)(M[NB - 1] >> 32));
     const int pid = pair_q[pp];
     const size_t o = (size_t)pid * ldo;
 #pragma unroll
     for (int i = 0; i < KB; ++i) {
-        if (i < k) {
+        if (i < k && i % kMergeLanes == sub) {
             const uint64_t key = M[i];
             const bool empty = key == kEmptyKey;
             out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(64) void chunk_merge_band_kernel(
             out_row[o + i] = empty ? -1 : W[i];
         }
     }
-    out_bound[pid] = ub == 0xffffffffu ? __builtin_inff() : ord2f(ub);
+    if (sub == 0) out_bound[pid] = ub == 0xffffffffu ? __builtin_inff() : ord2f(ub);
 }
 
 // ---------------------------------------------------------------------------
@@ -1626,16 +1626,16 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     if (rc != LMI_OK) return rc;
     if (!do_merge) return LMI_OK;
 
-    const int grid = (P + 63) / 64;
+    const int grid = (int)(((int64_t)P * kMergeLanes + kMergeBlock - 1) / kMergeBlock);
     if (band) {
-        hipLaunchKernelGGL(chunk_merge_band_kernel, dim3(grid), dim3(64), 0, s, a.partial, a.max_chunks,
+        hipLaunchKernelGGL(chunk_merge_band_kernel, dim3(grid), dim3(kMergeBlock), 0, s, a.partial, a.max_chunks,
                            pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo, out_d, out_pos,
                            out_row, out_bound, idx->n_rows, status, split_mask, w.split_s);
         LMI_LAUNCH_CHECK("chunk_merge_band_kernel");
         return LMI_OK;
     }
 #define LMI_CM(KLV, ROWSV)                                                                         \
-    hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(64), 0, s, a.partial,    \
+    hipLaunchKernelGGL((chunk_merge_kernel<KLV, ROWSV>), dim3(grid), dim3(kMergeBlock), 0, s, a.partial, \
                        a.max_chunks, pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo,  \
                        out_d, out_pos, out_row, idx->n_rows, status, split_mask, w.split_s)
     if (KL == 10) {

@@ -135,7 +135,13 @@ def flush_released() -> None:
 class no_gc_capture:
     """Context manager around a block of graph captures: the cyclic garbage
     collector is off inside (torch.cuda.graph itself collects before each
-    capture begins), so no finaliser runs mid-capture."""
+    capture begins), so no finaliser runs mid-capture.  The captures
+    themselves use capture_error_mode="thread_local": with an RCCL process
+    group the watchdog thread queries its collectives' events at any moment,
+    and in the default global mode such a query from another thread during a
+    capture invalidates it and kills the watchdog, which aborts the process
+    (round 6: tools/stream_steps.py aborted building its eighth stream object
+    that way, gpurun_out r6d)."""
 
     def __enter__(self):
         import gc

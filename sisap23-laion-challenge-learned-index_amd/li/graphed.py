@@ -230,7 +230,7 @@ class GraphedSearch:
         with no_gc_capture():   # (li._host "graph lifetime")
             for slot in range(2 if self.pipeline else 1):
                 gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr):
+                with torch.cuda.graph(gr, capture_error_mode="thread_local"):
                     buf = step(slot)
                     self.hs[slot].copy_(buf, non_blocking=True)
                 self.graphs.append(gr)

@@ -372,7 +372,7 @@ class StreamedSearch:
                 for name in names:
                     for j in range(NS):
                         gr = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(gr):
+                        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
                             self._f[name](j)
                         self.graphs[name, j] = gr
             torch.cuda.synchronize(dev)
