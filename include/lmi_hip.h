@@ -166,8 +166,21 @@ typedef struct lmi_index_desc {
      *      (distance, position) -- rounded to float32 first for the float32
      *      mode -- and the first k kept; a pair with more candidates than the
      *      collect buffer holds is scanned whole in float64.
-     * Needs d_pad == 768 (the fp16 scan's width) and no phase flags. */
+     * Needs d_pad == 768 (the fp16 scan's width) and no phase flags.
+     * ABI 10: the float32 arithmetic re-scores in the reference's own float32
+     * operation order -- sklearn's normalize (numpy einsum row norms, a
+     * division) and OpenBLAS sgemm's summation order for the (round, bucket)
+     * group's shape (oracle blas32_*: numpy 2.2 / OpenBLAS 0.3.29 SkylakeX,
+     * the libraries the reference runs on in the build container) -- so its
+     * float32 distances are the reference's bit for bit; shapes whose BLAS
+     * path is not restated (a group of one query or one row, groups of at
+     * most 3 x 3) and the whole-shard fallback keep the exact value rounded
+     * to float32. */
     const float* corpus32;
+    /* ABI 10: optional (NULL = this shard's own) device [n_buckets] int64: the
+     * rows of every bucket in the whole index (a G-GPU index's shards hold
+     * slices): the shape of the reference's per-bucket product. */
+    const int64_t* bucket_rows;
 } lmi_index_desc;
 
 /* Host helper: fills chunk_first_out[C+1] from host bucket offsets and returns

@@ -12,6 +12,8 @@ Every function restates a piece of TerkaSlan/sisap23-laion-challenge-learned-ind
                        utils.py:10-11 (cosine_similarity) and search.py:50-52
   pairwise_cosine      utils.py:10-11
   pairwise_cosine_threshold  utils.py:14-43
+  blas32_*             utils.py:10-11's float32 arithmetic operation by
+                       operation (numpy einsum + OpenBLAS sgemm orders, round 6)
   mlp_forward / predict_proba / predict   model.py:15-83, :201-229
   search_single_direct / search_direct   LearnedIndex.py:22-195, restated
                        line by line (full distance matrices, no shortcut)
@@ -71,6 +73,105 @@ def pairwise_cosine_threshold(x, y, threshold, cat_idxs, k=10):
     to_be_added = result[relevant_dists[0], relevant_dists[1]]
     output_arr[relevant_dists[0], output_arr_2nd_dim] = to_be_added
     return output_arr, relevant_object_ids, 0.0
+
+
+# ---------------------------------------------------------------------------
+# the reference's float32 arithmetic, operation by operation (round 6)
+# ---------------------------------------------------------------------------
+# utils.py:10-11 in float32 is sklearn's normalize (row norms by
+# np.einsum('ij,ij->i'), then an in-place division) and a float32 GEMM
+# (numpy.matmul -> OpenBLAS sgemm), then 1 - S.  The summation orders below
+# restate the third-party code the reference runs on in this container --
+# numpy 2.2's einsum sum-of-products loop (SSE baseline: four float32 lanes,
+# the four vectors of each 16-element group multiplied and added in reverse
+# order, no FMA, lanes summed (0+1)+(2+3)) and OpenBLAS 0.3.29's SkylakeX
+# sgemm (a small-matrix kernel when M*N*K <= 96*96*100: sixteen FMA chains
+# over k mod 16, summed pairwise; else the blocked kernel: one FMA chain per
+# K block of 384, the blocks' sums added) -- found by bitwise search against
+# numpy and pinned by tests/test_oracle_blas32.py.  Shapes it does not cover
+# (a group of one query or one row -- OpenBLAS forwards those to gemv, whose
+# order depends on its thread split -- and groups of at most 3 x 3) return
+# None.  The GPU's split mode (x_select_wave_kernel) computes these values.
+_BLAS_SMALL_MNK = 96 * 96 * 100
+_BLAS_KBLOCK = 384
+
+
+def _f32(x):
+    return np.asarray(x, dtype=np.float32)
+
+
+def blas32_row_norms(x: np.ndarray) -> np.ndarray:
+    """np.einsum('ij,ij->i', x, x) for float32 rows whose length is a
+    multiple of 16, in numpy's summation order (see above)."""
+    x = np.asarray(x, dtype=np.float32)
+    n, d = x.shape
+    if d % 16:
+        raise ValueError("rows of a multiple of 16 elements")
+    acc = np.zeros((4, n), np.float32)
+    for g in range(0, d, 16):
+        for v in (3, 2, 1, 0):
+            blk = x[:, g + 4 * v:g + 4 * v + 4]
+            acc += (blk * blk).T            # (float32 product, then float32 add)
+    return (acc[0] + acc[1]) + (acc[2] + acc[3])
+
+
+def blas32_normalize(x: np.ndarray) -> np.ndarray:
+    """sklearn normalize(x) in float32, operation by operation."""
+    x = np.asarray(x, dtype=np.float32)
+    norms = np.sqrt(blas32_row_norms(x))
+    norms[norms < 10 * np.finfo(np.float32).eps] = np.float32(1.0)
+    return x / norms[:, None]
+
+
+def _fma_chain(a, b):
+    """sum_k a[:, k] * b[:, k] as one FMA chain in ascending k (float32 with
+    one rounding per step: the float64 product of two float32 values is
+    exact, so float64 add-then-round is the FMA)."""
+    acc = np.zeros(a.shape[0], np.float32)
+    for k in range(a.shape[1]):
+        acc = (acc.astype(np.float64) + a[:, k].astype(np.float64) * b[:, k].astype(np.float64)
+               ).astype(np.float32)
+    return acc
+
+
+def blas32_kernel(M: int, N: int, K: int):
+    """Which OpenBLAS sgemm path the reference's (M queries x N rows) float32
+    product takes: "small", "blocked", or None (gemv / tiny: not restated)."""
+    if M <= 1 or N <= 1 or (M <= 3 and N <= 3) or K % 16:
+        return None
+    return "small" if M * N * K <= _BLAS_SMALL_MNK else "blocked"
+
+
+def blas32_dot(qn: np.ndarray, yn: np.ndarray, kernel: str) -> np.ndarray:
+    """Row-wise dot of normalised float32 vectors qn[i] . yn[i] in the order of
+    `kernel` (blas32_kernel)."""
+    qn, yn = _f32(qn), _f32(yn)
+    K = qn.shape[1]
+    if kernel == "small":
+        parts = [_fma_chain(qn[:, l::16], yn[:, l::16]) for l in range(16)]
+        while len(parts) > 1:
+            parts = [parts[2 * i] + parts[2 * i + 1] for i in range(len(parts) // 2)]
+        return parts[0]
+    tot = None
+    for a in range(0, K, _BLAS_KBLOCK):
+        c = _fma_chain(qn[:, a:a + _BLAS_KBLOCK], yn[:, a:a + _BLAS_KBLOCK])
+        tot = c if tot is None else tot + c
+    return tot
+
+
+def blas32_pairwise_cosine(x, y):
+    """pairwise_cosine(x, y) of float32 x [M, d] (a group's queries) and y [N,
+    d] (a bucket's rows) from the restated operations; None when the shape's
+    kernel is not restated.  Equals pairwise_cosine bit for bit in this
+    container (tests/test_oracle_blas32.py)."""
+    x, y = _f32(x), _f32(y)
+    kern = blas32_kernel(x.shape[0], y.shape[0], x.shape[1])
+    if kern is None:
+        return None
+    xn, yn = blas32_normalize(x), blas32_normalize(y)
+    M, N = xn.shape[0], yn.shape[0]
+    S = blas32_dot(np.repeat(xn, N, axis=0), np.tile(yn, (M, 1)), kern).reshape(M, N)
+    return np.float32(1) - S
 
 
 # ---------------------------------------------------------------------------

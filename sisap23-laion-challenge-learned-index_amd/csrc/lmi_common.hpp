@@ -220,6 +220,15 @@ struct XArgs {
     // those within the k-th smallest d~ + two_eps are re-scored
     double two_eps;
     const int32_t* fix;  // [nq*R] pairs without a sampled bound (whole shard), or null
+    // ABI 10, the float32 output only: the reference's float32 operation order
+    // (oracle blas32_*; lmi_index_desc.corpus32): qn32 [nq][d_pad] the queries
+    // normalised as sklearn does in float32 (null: the exact value rounded),
+    // grp [R][C] queries of each (round, bucket) group, nrows_c [C] rows of
+    // each bucket in the whole index (null: this shard's)
+    const float* qn32;
+    const int32_t* grp;
+    const int64_t* nrows_c;
+    int32_t C;
 };
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);

@@ -791,6 +791,118 @@ __device__ inline void query_hat_x(const TQ* qrow, int d, int nps, double zero_e
         for (int j = 0; j < 4; ++j) qh[i][j] = qh[i][j] / n;
 }
 
+// ---- the reference's float32 operation order (ABI 10; oracle blas32_*) ------
+// utils.py:10-11 in float32 = sklearn normalize (np.einsum('ij,ij->i') row
+// norms, then a division) + numpy.matmul (OpenBLAS sgemm) + 1 - S.  The
+// orders are numpy 2.2's einsum loop (four lanes, each 16-element group's
+// vectors in reverse order, product then add) and OpenBLAS 0.3.29's SkylakeX
+// sgemm: the small-matrix kernel (sixteen FMA chains over k mod 16, summed
+// pairwise) when M*N*K <= 96*96*100, else one FMA chain per 384-wide K block,
+// the blocks added.  M = the (round, bucket) group's queries, N = the bucket's
+// rows (tests/test_oracle_blas32.py pins the restatement to numpy bit for bit).
+constexpr int kBlasSmallMNK = 96 * 96 * 100;
+constexpr int kBlasKBlock = 384;
+constexpr float kEps32f = 1.1920928955078125e-07f;
+
+// 0: not restated (the exact value rounded), 1: small kernel, 2: blocked
+__device__ inline int blas32_kernel_of(const XArgs& a, int64_t p) {
+    if (!a.qn32 || (a.d & 15)) return 0;
+    const int c = a.classes[p];
+    if (c < 0 || c >= a.C) return 0;
+    const int64_t M = a.grp[(size_t)(p % a.R) * a.C + c];
+    const int64_t N = a.nrows_c ? a.nrows_c[c] : a.bucket_off[c + 1] - a.bucket_off[c];
+    if (M <= 1 || N <= 1 || (M <= 3 && N <= 3)) return 0;
+    return M * N * (int64_t)a.d <= kBlasSmallMNK ? 1 : 2;
+}
+
+// (each function turns FMA contraction off in its own scope: every product
+// and sum is rounded where the reference rounds it)
+// sklearn's float32 norm of a row of d (a multiple of 16) values: the einsum
+// order, sqrt, the zero rule
+__device__ inline float blas32_norm(const float* y, int d) {
+#pragma clang fp contract(off)
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    for (int g = 0; g < d; g += 16) {
+#pragma unroll
+        for (int v = 3; v >= 0; --v) {
+            const float4 x = *reinterpret_cast<const float4*>(y + g + 4 * v);
+            a0 = a0 + x.x * x.x;
+            a1 = a1 + x.y * x.y;
+            a2 = a2 + x.z * x.z;
+            a3 = a3 + x.w * x.w;
+        }
+    }
+    float n = __builtin_sqrtf((a0 + a1) + (a2 + a3));
+    return n < 10.0f * kEps32f ? 1.0f : n;
+}
+
+// 1 - <qn, y / |y|> in the reference's float32 order (kern from
+// blas32_kernel_of; qn already normalised by x_qn32_kernel)
+__device__ inline float blas32_dist(const float* y, const float* qn, int d, int kern) {
+#pragma clang fp contract(off)
+    const float n = blas32_norm(y, d);
+    float s;
+    if (kern == 1) {
+        float c[16];
+#pragma unroll
+        for (int l = 0; l < 16; ++l) c[l] = 0.0f;
+        for (int e0 = 0; e0 < d; e0 += 16) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const float4 x = *reinterpret_cast<const float4*>(y + e0 + 4 * v);
+                const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * v);
+                c[4 * v + 0] = __builtin_fmaf(q.x, x.x / n, c[4 * v + 0]);
+                c[4 * v + 1] = __builtin_fmaf(q.y, x.y / n, c[4 * v + 1]);
+                c[4 * v + 2] = __builtin_fmaf(q.z, x.z / n, c[4 * v + 2]);
+                c[4 * v + 3] = __builtin_fmaf(q.w, x.w / n, c[4 * v + 3]);
+            }
+        }
+#pragma unroll
+        for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+            for (int i = 0; i < w; ++i) c[i] = c[2 * i] + c[2 * i + 1];
+        s = c[0];
+    } else {
+        s = 0.0f;
+        for (int b0 = 0; b0 < d; b0 += kBlasKBlock) {
+            float c = 0.0f;
+            const int b1 = b0 + kBlasKBlock < d ? b0 + kBlasKBlock : d;
+            for (int e = b0; e < b1; e += 4) {
+                const float4 x = *reinterpret_cast<const float4*>(y + e);
+                const float4 q = *reinterpret_cast<const float4*>(qn + e);
+                c = __builtin_fmaf(q.x, x.x / n, c);
+                c = __builtin_fmaf(q.y, x.y / n, c);
+                c = __builtin_fmaf(q.z, x.z / n, c);
+                c = __builtin_fmaf(q.w, x.w / n, c);
+            }
+            s = b0 == 0 ? c : s + c;
+        }
+    }
+    return 1.0f - s;
+}
+
+// the queries normalised as sklearn does in float32 (a thread per query)
+__global__ __launch_bounds__(64) void x_qn32_kernel(const float* __restrict__ q, int32_t ldq, int32_t nq, int32_t d,
+                                                    int32_t d_pad, float* __restrict__ out) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= nq) return;
+    const float* row = q + (size_t)i * ldq;
+    float* o = out + (size_t)i * d_pad;
+    if (d & 15) return;  // (not restated: blas32_kernel_of returns 0)
+    const float n = blas32_norm(row, d);
+    for (int e = 0; e < d_pad; ++e) o[e] = e < d ? row[e] / n : 0.0f;
+}
+
+// queries of every (round, bucket) group (grp zeroed by the caller)
+__global__ __launch_bounds__(256) void x_groups_kernel(const int32_t* __restrict__ classes, int64_t P, int32_t R,
+                                                       int32_t C, int32_t* __restrict__ grp) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= P) return;
+    const int c = classes[p];
+    if (c >= 0 && c < C) atomicAdd(&grp[(size_t)(p % R) * C + c], 1);
+}
+
 template <bool OUT64>
 __device__ inline double out_value(double x) {
     if constexpr (OUT64) return x;
@@ -891,7 +1003,19 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
         for (uint32_t i = tid; i < nr; i += kXT) sr[i] = (int32_t)(uint32_t)keys[i];
         __syncthreads();
     }
-    for (uint32_t j0 = (uint32_t)w * kB; j0 < nr; j0 += (kXT / 64) * kB) {
+    const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
+    if (kern != 0) {
+        // the reference's float32 order: a candidate per thread
+        const float* qn = a.qn32 + (size_t)(p / a.R) * a.d_pad;
+        for (uint32_t j = tid; j < nr; j += kXT) {
+            const int64_t x = band ? (int64_t)sr[j] : (int64_t)(uint32_t)src[j];
+            const bool ok = x >= 0 && x < a.n_rows;
+            if (!ok) atomicOr(a.status, LMI_STATUS_INTERNAL);
+            sd[j] = ok ? (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern) : __builtin_inf();
+            sr[j] = ok ? (int32_t)x : INT32_MAX;
+        }
+    }
+    for (uint32_t j0 = (uint32_t)w * kB; kern == 0 && j0 < nr; j0 += (kXT / 64) * kB) {
         int32_t r[kB];
 #pragma unroll
         for (int b = 0; b < kB; ++b) {
@@ -1016,7 +1140,25 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
         mine[s] = __builtin_inf();
         mrow[s] = INT32_MAX;
     }
-    for (int j0 = 0; j0 < nr; j0 += KB) {
+    const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
+    if (kern != 0) {
+        // the reference's float32 order: a candidate per lane (each a chain)
+        const float* qn = a.qn32 + (size_t)(p / a.R) * a.d_pad;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int j = 64 * s + lane;
+            if (j < nr) {
+                const int64_t x = rows[j];
+                if (x < 0 || x >= a.n_rows) {
+                    atomicOr(a.status, LMI_STATUS_INTERNAL);
+                } else {
+                    mine[s] = (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern);
+                    mrow[s] = (int32_t)x;
+                }
+            }
+        }
+    }
+    for (int j0 = 0; kern == 0 && j0 < nr; j0 += KB) {
         int32_t r[KB];
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
@@ -1184,6 +1326,17 @@ int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s) {
     if (a.out_f64) {
         if (a.rows64) return a.q64 ? launch_x3<double, double, true>(a, P, s) : launch_x3<double, float, true>(a, P, s);
         return a.q64 ? launch_x3<float, double, true>(a, P, s) : launch_x3<float, float, true>(a, P, s);
+    }
+    if (a.qn32) {
+        // the reference's float32 order: the queries normalised as sklearn
+        // does, the (round, bucket) group sizes (XArgs; oracle blas32_*)
+        hipLaunchKernelGGL(x_qn32_kernel, dim3((unsigned)((a.nq + 63) / 64)), dim3(64), 0, s, a.q, a.ldq, a.nq,
+                           a.d, a.d_pad, const_cast<float*>(a.qn32));
+        LMI_LAUNCH_CHECK("x_qn32_kernel");
+        LMI_TRY(fill_u32(const_cast<int32_t*>(a.grp), 0u, (size_t)a.R * a.C, s));
+        hipLaunchKernelGGL(x_groups_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a.classes, P, a.R,
+                           a.C, const_cast<int32_t*>(a.grp));
+        LMI_LAUNCH_CHECK("x_groups_kernel");
     }
     return launch_x3<float, float, false>(a, P, s);
 }

@@ -1673,7 +1673,7 @@ double split_eps(int d_pad) {
 namespace {
 struct XWs {
     size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
-        classes2, region, region_bytes, total;
+        classes2, qn32, grp, region, region_bytes, total;
     int32_t cap;
 };
 // k <= 10: the k-th of a per-bucket sample (the product scan over
@@ -1723,6 +1723,8 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.off2 = take(((size_t)2 * idx->n_buckets + 1) * 8);
     w.cf2 = take(((size_t)2 * idx->n_buckets + 1) * 4);
     w.classes2 = take(P * 4);
+    w.qn32 = take((size_t)nq * idx->d_pad * 4);
+    w.grp = take((size_t)R * idx->n_buckets * 4);
     w.bound = take(P * 4);
     w.ccount = take(P * 4);
     w.cand = take(P * (size_t)cap * 8);
@@ -1872,6 +1874,11 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     a.status = status;
     a.two_eps = sampled ? two_eps : 0.0;
     a.fix = sampled && !x_sample(k) ? fix : nullptr;
+    // (ABI 10: the float32 output in the reference's own float32 order)
+    a.qn32 = (!out_f64 && q) ? (const float*)(ws + w.qn32) : nullptr;
+    a.grp = (const int32_t*)(ws + w.grp);
+    a.nrows_c = idx->bucket_rows;
+    a.C = idx->n_buckets;
     // (pairs whose class is out of range keep the prefill of step 1's prep:
     // the outputs are prefilled here, by pair id, in step 3's own buffers)
     hipLaunchKernelGGL(x_prefill_kernel, dim3((unsigned)(((int64_t)P * k + 255) / 256)), dim3(256), 0, s,

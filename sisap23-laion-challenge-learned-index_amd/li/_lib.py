@@ -127,6 +127,7 @@ class IndexDesc(C.Structure):
         ("chunk_centroid", C.c_void_p),  # ABI 2
         ("corpus64", C.c_void_p),        # ABI 6
         ("corpus32", C.c_void_p),        # ABI 9
+        ("bucket_rows", C.c_void_p),     # ABI 10
     ]
 
 

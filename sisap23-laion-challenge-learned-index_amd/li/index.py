@@ -251,6 +251,9 @@ class DeviceIndex:
         self.max_chunks = int(mx)
         self.n_chunks = int(cf[-1])
         self.bucket_off_local = torch.from_numpy(loc_off).to(self.device)
+        # every bucket's rows in the whole index (lmi_index_desc.bucket_rows):
+        # the shape of the reference's per-bucket product
+        self.bucket_rows = torch.from_numpy(np.ascontiguousarray(self.bucket_size, dtype=np.int64)).to(self.device)
         self.chunk_first = torch.from_numpy(cf).to(self.device)
         self.chunk_centroid = None
         if subcluster and self.n_chunks > 0:
@@ -457,6 +460,7 @@ class IndexDescHolder:
         d.chunk_centroid = ptr(ix.chunk_centroid) if ix.chunk_centroid is not None else None
         d.corpus64 = ptr(ix.corpus64) if ix.corpus64 is not None else None
         d.corpus32 = ptr(ix.corpus32) if (ix.corpus32 is not None and not general32) else None
+        d.bucket_rows = ptr(ix.bucket_rows)
         self.desc = d
 
 

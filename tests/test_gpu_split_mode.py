@@ -223,3 +223,34 @@ def test_split_subcluster_layout_moves_the_float32_rows(k):
         assert O.compare_lists(ref_d64, ref_p64, d64.cpu().numpy(), p64.cpu().numpy(), atol=1e-12,
                                tie=1e-12) == 0
 
+
+
+@pytest.mark.parametrize("mode,seed", [("near", 661), ("skewed", 662), ("router", 663)])
+def test_split_float32_is_the_references_own_arithmetic(mode, seed):
+    """ABI 10: the split mode's float32 re-score follows the reference's
+    float32 operation order (oracle blas32_*: sklearn's einsum norms and
+    division, OpenBLAS sgemm's summation order for the (round, bucket)
+    group's shape), so wherever that shape's order is restated the lists'
+    float32 distances equal the oracle's (= numpy's = the reference's) bit for
+    bit and ids differ only inside runs of identical distances."""
+    w, x, q = _x(mode, seed, n=6000, nq=200)
+    C, R, k = w["C"], 4, 10
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
+    d, p, st = bucket_topk(ix, T(q), T(classes.astype(np.int32)), k)
+    assert int(st.item()) == 0
+    ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, R, k, C)
+    sizes = np.bincount(w["labels"], minlength=C)
+    keep = np.zeros(classes.shape, bool)
+    kinds = set()
+    for r in range(R):
+        grp = np.bincount(classes[:, r], minlength=C)
+        for i in range(classes.shape[0]):
+            kern = O.blas32_kernel(int(grp[classes[i, r]]), int(sizes[classes[i, r]]), x.shape[1])
+            keep[i, r] = kern is not None
+            kinds.add(kern)
+    assert keep.mean() > 0.9 and "blocked" in kinds
+    gd, gp = d.cpu().numpy()[keep], p.cpu().numpy()[keep]
+    rd, rp = ref_d[keep], ref_p[keep]
+    np.testing.assert_array_equal(gd, rd)     # float32 distances: bit for bit
+    assert O.compare_lists(rd, rp, gd, gp, atol=0.0, tie=0.0) == 0
