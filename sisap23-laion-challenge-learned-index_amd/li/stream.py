@@ -28,8 +28,9 @@ its block of the batch (1/G of the rows: the host-memory traffic of a new
 batch does not grow with G) and routes it; the one collective per launch, in
 F, all-gathers every rank's [lists of batch t-3 | query block and classes of
 batch t] buffer, so the list exchange carries the next batch's queries.  F is
-then two graphs: F1 (merge phase + all-gather), after which P of batch t
-unpacks the gathered queries beside F2 (K3 + replay + D2H)."""
+then three graphs: F1 (the merge phase, as soon as the scan is done), FX (the
+all-gather, once batch t's block is routed), after which P of batch t unpacks
+the gathered queries beside F2 (K3 + replay + D2H)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -290,8 +291,6 @@ class StreamedSearch:
                 phase(j, _lib.LMI_Q_PHASE_REFINE, band_x=(None, self.kall[j], Gk))
             else:
                 phase(j, _lib.LMI_Q_PHASE_MERGE)
-            if X:
-                xgather(j)
 
         def finish2(j):
             buf, ad, aa, ast = self.ans[j]
@@ -315,11 +314,16 @@ class StreamedSearch:
 
         def finish(j):
             finish1(j)
+            if X:
+                xgather(j)
             finish2(j)
 
         self._mdd, self._mpp = [None] * NS, [None] * NS
+        # (F1: the merge phase [float64: + the kth exchange and the REFINE
+        # phase]; FX: the all-gather of slot j's lists with the next batch's
+        # block, which waits for that block's route; F2: K3 + replay + D2H)
         self._f = dict(U=upload, R=route, X=xgather, P=plan, S=scan, F=finish, F1=finish1,
-                       F2=finish2)
+                       FX=xgather, F2=finish2)
         # four streams: the finish, the plan, the upload + route (the H2D on
         # the copy engine, then the router), and the scan on the caller's
         # stream, each on its own hardware queue (queue_streams); per-slot
@@ -364,9 +368,9 @@ class StreamedSearch:
         elif err is not None:
             raise err
         if capture:
-            # one graph per (stage, slot); F is F1 + F2 at G > 1 (the garbage
+            # one graph per (stage, slot); F is F1 + FX + F2 at G > 1 (the garbage
             # collector off meanwhile: li._host "graph lifetime")
-            names = ("R", "P", "S") + (("F1", "F2") if X else ("F",))
+            names = ("R", "P", "S") + (("F1", "FX", "F2") if X else ("F",))
             self.graphs = {}
             with no_gc_capture():
                 for name in names:
@@ -551,10 +555,16 @@ class StreamedSearch:
             with torch.cuda.stream(self._fs):
                 self._run("F", jf)
         else:
-            # F1 gathers slot jf's lists with slot jr's block (exchange buffer jf)
-            self._fs.wait_event(self._rdone[jr])
+            # F1, the merge phase, runs as soon as the scan is done; FX gathers
+            # slot jf's lists with slot jr's block (exchange buffer jf), so it
+            # also waits for that block's route (the router, starved by the
+            # scan's persistent grid, ends ~50 us after it: round 6 moved the
+            # merge phase out from behind it)
             with torch.cuda.stream(self._fs):
                 self._run("F1", jf)
+            self._fs.wait_event(self._rdone[jr])
+            with torch.cuda.stream(self._fs):
+                self._run("FX", jf)
             self._gdone[jf].record(self._fs)
             with torch.cuda.stream(self._fs):
                 self._run("F2", jf)

@@ -60,7 +60,7 @@ def main():
         # the batch stream: F1 (merge phase + the captured all-gather), F2
         # (lmi_merge_topk_packed + replay + D2H)
         ss = sx.streamed(w["qn"], w["q"], 4, k=10, dist=dd)
-        assert ss.X and ss.xall is not None and ("F1", 0) in ss.graphs and ("F2", 0) in ss.graphs
+        assert ss.X and ss.xall is not None and all((n, 0) in ss.graphs for n in ("F1", "FX", "F2"))
         got = list(ss.stream(batches))
         assert len(got) == len(batches) and ss.launches == len(batches) - 3
         for o, r in zip(got, ref):
