@@ -86,8 +86,9 @@ def pairwise_cosine_threshold(x, y, threshold, cat_idxs, k=10):
 # the four vectors of each 16-element group multiplied and added in reverse
 # order, no FMA, lanes summed (0+1)+(2+3)) and OpenBLAS 0.3.29's SkylakeX
 # sgemm (a small-matrix kernel when M*N*K <= 96*96*100: sixteen FMA chains
-# over k mod 16, summed pairwise; else the blocked kernel: one FMA chain per
-# K block of 384, the blocks' sums added) -- found by bitwise search against
+# over k mod 16, summed pairwise -- by halves in the product's corner block
+# of the last M mod 4 queries x the last N mod 4 rows; else the blocked
+# kernel: one FMA chain per K block of 384, the blocks' sums added) -- found by bitwise search against
 # numpy and pinned by tests/test_oracle_blas32.py.  Shapes it does not cover
 # (a group of one query or one row -- OpenBLAS forwards those to gemv, whose
 # order depends on its thread split -- and groups of at most 3 x 3) return
@@ -142,16 +143,23 @@ def blas32_kernel(M: int, N: int, K: int):
     return "small" if M * N * K <= _BLAS_SMALL_MNK else "blocked"
 
 
-def blas32_dot(qn: np.ndarray, yn: np.ndarray, kernel: str) -> np.ndarray:
+def blas32_dot(qn: np.ndarray, yn: np.ndarray, kernel: str, corner=None) -> np.ndarray:
     """Row-wise dot of normalised float32 vectors qn[i] . yn[i] in the order of
-    `kernel` (blas32_kernel)."""
+    `kernel` (blas32_kernel).  The small kernel sums its sixteen chains
+    pairwise ((0+1)+(2+3)...) except in the corner block of the product --
+    query i >= 4 floor(M/4) of its group and row j >= 4 floor(N/4) of its
+    bucket -- where it sums them by halves ((0+8)+(4+12)...): `corner`, a
+    boolean per dot (default none)."""
     qn, yn = _f32(qn), _f32(yn)
     K = qn.shape[1]
     if kernel == "small":
         parts = [_fma_chain(qn[:, l::16], yn[:, l::16]) for l in range(16)]
-        while len(parts) > 1:
-            parts = [parts[2 * i] + parts[2 * i + 1] for i in range(len(parts) // 2)]
-        return parts[0]
+        pair, half = list(parts), list(parts)
+        while len(pair) > 1:
+            pair = [pair[2 * i] + pair[2 * i + 1] for i in range(len(pair) // 2)]
+            h = len(half) // 2
+            half = [half[i] + half[i + h] for i in range(h)]
+        return pair[0] if corner is None else np.where(corner, half[0], pair[0])
     tot = None
     for a in range(0, K, _BLAS_KBLOCK):
         c = _fma_chain(qn[:, a:a + _BLAS_KBLOCK], yn[:, a:a + _BLAS_KBLOCK])
@@ -170,7 +178,9 @@ def blas32_pairwise_cosine(x, y):
         return None
     xn, yn = blas32_normalize(x), blas32_normalize(y)
     M, N = xn.shape[0], yn.shape[0]
-    S = blas32_dot(np.repeat(xn, N, axis=0), np.tile(yn, (M, 1)), kern).reshape(M, N)
+    ii, jj = np.meshgrid(np.arange(M), np.arange(N), indexing="ij")
+    corner = ((ii >= M // 4 * 4) & (jj >= N // 4 * 4)).reshape(-1)
+    S = blas32_dot(np.repeat(xn, N, axis=0), np.tile(yn, (M, 1)), kern, corner).reshape(M, N)
     return np.float32(1) - S
 
 

@@ -229,6 +229,10 @@ struct XArgs {
     const int32_t* grp;
     const int64_t* nrows_c;
     int32_t C;
+    // (the small kernel's corner block: tailq[pair] = the query is among the
+    // last M mod 4 of its group; goff [C+1] the buckets' global offsets)
+    const uint8_t* tailq;
+    const int64_t* goff;
 };
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);

@@ -810,70 +810,104 @@ __device__ inline int blas32_kernel_of(const XArgs& a, int64_t p) {
     const int c = a.classes[p];
     if (c < 0 || c >= a.C) return 0;
     const int64_t M = a.grp[(size_t)(p % a.R) * a.C + c];
-    const int64_t N = a.nrows_c ? a.nrows_c[c] : a.bucket_off[c + 1] - a.bucket_off[c];
+    const int64_t N = a.goff[c + 1] - a.goff[c];
     if (M <= 1 || N <= 1 || (M <= 3 && N <= 3)) return 0;
     return M * N * (int64_t)a.d <= kBlasSmallMNK ? 1 : 2;
+}
+// the small kernel sums its chains by halves, not pairwise, in the product's
+// corner block: the last M mod 4 queries of the group x the last N mod 4
+// rows of the bucket (oracle blas32_dot)
+__device__ inline bool blas32_corner(const XArgs& a, int64_t p, int32_t row) {
+    if (!a.tailq[p]) return false;
+    const int c = a.classes[p];
+    const int64_t N = a.goff[c + 1] - a.goff[c];
+    return (int64_t)a.gpos[row] - a.goff[c] >= N / 4 * 4;
 }
 
 // (each function turns FMA contraction off in its own scope: every product
 // and sum is rounded where the reference rounds it)
-// sklearn's float32 norm of a row of d (a multiple of 16) values: the einsum
-// order, sqrt, the zero rule
-__device__ inline float blas32_norm(const float* y, int d) {
+// x / n correctly rounded from rn = RN(1 / n) (Markstein: one residual FMA and
+// one correction; the same value as the IEEE division numpy's divps gives)
+__device__ inline float div_rn(float x, float n, float rn) {
 #pragma clang fp contract(off)
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-    for (int g = 0; g < d; g += 16) {
-#pragma unroll
-        for (int v = 3; v >= 0; --v) {
-            const float4 x = *reinterpret_cast<const float4*>(y + g + 4 * v);
-            a0 = a0 + x.x * x.x;
-            a1 = a1 + x.y * x.y;
-            a2 = a2 + x.z * x.z;
-            a3 = a3 + x.w * x.w;
-        }
-    }
-    float n = __builtin_sqrtf((a0 + a1) + (a2 + a3));
-    return n < 10.0f * kEps32f ? 1.0f : n;
+    const float q0 = x * rn;
+    const float e = __builtin_fmaf(-q0, n, x);
+    return __builtin_fmaf(e, rn, q0);
 }
 
 // 1 - <qn, y / |y|> in the reference's float32 order (kern from
-// blas32_kernel_of; qn already normalised by x_qn32_kernel)
-__device__ inline float blas32_dist(const float* y, const float* qn, int d, int kern) {
+// blas32_kernel_of; qn normalised by x_qn32_kernel): sklearn's norm of y in
+// the einsum order, the division, the dot's chains.  A lane per candidate:
+// each step's loads go out a block of 64 values ahead of their use.
+__device__ inline float blas32_dist(const float* y, const float* qn, int d, int kern, bool corner) {
 #pragma clang fp contract(off)
-    const float n = blas32_norm(y, d);
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    for (int g0 = 0; g0 < d; g0 += 64) {
+        float4 x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + g0 + 4 * i);
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+            for (int v = 3; v >= 0; --v) {
+                const float4 t = x[4 * gg + v];
+                a0 = a0 + t.x * t.x;
+                a1 = a1 + t.y * t.y;
+                a2 = a2 + t.z * t.z;
+                a3 = a3 + t.w * t.w;
+            }
+    }
+    float n = __builtin_sqrtf((a0 + a1) + (a2 + a3));
+    if (n < 10.0f * kEps32f) n = 1.0f;
+    const float rn = 1.0f / n;
     float s;
     if (kern == 1) {
         float c[16];
 #pragma unroll
         for (int l = 0; l < 16; ++l) c[l] = 0.0f;
-        for (int e0 = 0; e0 < d; e0 += 16) {
+        for (int e0 = 0; e0 < d; e0 += 64) {
+            float4 x[16];
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const float4 x = *reinterpret_cast<const float4*>(y + e0 + 4 * v);
-                const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * v);
-                c[4 * v + 0] = __builtin_fmaf(q.x, x.x / n, c[4 * v + 0]);
-                c[4 * v + 1] = __builtin_fmaf(q.y, x.y / n, c[4 * v + 1]);
-                c[4 * v + 2] = __builtin_fmaf(q.z, x.z / n, c[4 * v + 2]);
-                c[4 * v + 3] = __builtin_fmaf(q.w, x.w / n, c[4 * v + 3]);
+            for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + e0 + 4 * i);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * i);
+                const int l = (4 * i) & 15;
+                c[l + 0] = __builtin_fmaf(q.x, div_rn(x[i].x, n, rn), c[l + 0]);
+                c[l + 1] = __builtin_fmaf(q.y, div_rn(x[i].y, n, rn), c[l + 1]);
+                c[l + 2] = __builtin_fmaf(q.z, div_rn(x[i].z, n, rn), c[l + 2]);
+                c[l + 3] = __builtin_fmaf(q.w, div_rn(x[i].w, n, rn), c[l + 3]);
             }
         }
+        if (corner) {
 #pragma unroll
-        for (int w = 8; w >= 1; w >>= 1)
+            for (int h = 8; h >= 1; h >>= 1)
 #pragma unroll
-            for (int i = 0; i < w; ++i) c[i] = c[2 * i] + c[2 * i + 1];
+                for (int i = 0; i < h; ++i) c[i] = c[i] + c[i + h];
+        } else {
+#pragma unroll
+            for (int h = 8; h >= 1; h >>= 1)
+#pragma unroll
+                for (int i = 0; i < h; ++i) c[i] = c[2 * i] + c[2 * i + 1];
+        }
         s = c[0];
     } else {
         s = 0.0f;
         for (int b0 = 0; b0 < d; b0 += kBlasKBlock) {
             float c = 0.0f;
             const int b1 = b0 + kBlasKBlock < d ? b0 + kBlasKBlock : d;
-            for (int e = b0; e < b1; e += 4) {
-                const float4 x = *reinterpret_cast<const float4*>(y + e);
-                const float4 q = *reinterpret_cast<const float4*>(qn + e);
-                c = __builtin_fmaf(q.x, x.x / n, c);
-                c = __builtin_fmaf(q.y, x.y / n, c);
-                c = __builtin_fmaf(q.z, x.z / n, c);
-                c = __builtin_fmaf(q.w, x.w / n, c);
+            for (int e0 = b0; e0 < b1; e0 += 64) {
+                float4 x[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + e0 + 4 * i);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * i);
+                    c = __builtin_fmaf(q.x, div_rn(x[i].x, n, rn), c);
+                    c = __builtin_fmaf(q.y, div_rn(x[i].y, n, rn), c);
+                    c = __builtin_fmaf(q.z, div_rn(x[i].z, n, rn), c);
+                    c = __builtin_fmaf(q.w, div_rn(x[i].w, n, rn), c);
+                }
             }
             s = b0 == 0 ? c : s + c;
         }
@@ -881,17 +915,34 @@ __device__ inline float blas32_dist(const float* y, const float* qn, int d, int 
     return 1.0f - s;
 }
 
-// the queries normalised as sklearn does in float32 (a thread per query)
-__global__ __launch_bounds__(64) void x_qn32_kernel(const float* __restrict__ q, int32_t ldq, int32_t nq, int32_t d,
-                                                    int32_t d_pad, float* __restrict__ out) {
+// The queries normalised as sklearn does in float32, a wave per query: the
+// lanes square their values (rounded) into LDS, four lanes run the einsum's
+// four chains, and every lane divides its values by the norm
+__global__ __launch_bounds__(256) void x_qn32_kernel(const float* __restrict__ q, int32_t ldq, int32_t nq, int32_t d,
+                                                     int32_t d_pad, float* __restrict__ out) {
 #pragma clang fp contract(off)
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= nq) return;
+    __shared__ float sq[4][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = blockIdx.x * 4 + w;
+    if (i >= nq || (d & 15) || d > 1024) return;  // ((d & 15): not restated, blas32_kernel_of returns 0)
     const float* row = q + (size_t)i * ldq;
     float* o = out + (size_t)i * d_pad;
-    if (d & 15) return;  // (not restated: blas32_kernel_of returns 0)
-    const float n = blas32_norm(row, d);
-    for (int e = 0; e < d_pad; ++e) o[e] = e < d ? row[e] / n : 0.0f;
+    for (int e = lane; e < d; e += 64) {
+        const float x = row[e];
+        sq[w][e] = x * x;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float acc = 0.0f;
+    if (lane < 4)
+        for (int g = 0; g < d; g += 16)
+#pragma unroll
+            for (int v = 3; v >= 0; --v) acc = acc + sq[w][g + 4 * v + lane];
+    const float s01 = __shfl(acc, 0) + __shfl(acc, 1), s23 = __shfl(acc, 2) + __shfl(acc, 3);
+    float n = __builtin_sqrtf(s01 + s23);
+    if (n < 10.0f * kEps32f) n = 1.0f;
+    for (int e = lane; e < d_pad; e += 64) o[e] = e < d ? row[e] / n : 0.0f;
 }
 
 // queries of every (round, bucket) group (grp zeroed by the caller)
@@ -901,6 +952,38 @@ __global__ __launch_bounds__(256) void x_groups_kernel(const int32_t* __restrict
     if (p >= P) return;
     const int c = classes[p];
     if (c >= 0 && c < C) atomicAdd(&grp[(size_t)(p % R) * C + c], 1);
+}
+
+// tailq[pair (q, r)] = q is among the last M mod 4 queries of its group
+// (fewer than M mod 4 later queries share its class in round r), and the
+// buckets' global offsets (one thread of block 0)
+__global__ __launch_bounds__(256) void x_tail_kernel(const int32_t* __restrict__ classes, int32_t nq, int32_t R,
+                                                     int32_t C, const int32_t* __restrict__ grp,
+                                                     const int64_t* __restrict__ nrows_c,
+                                                     const int64_t* __restrict__ bucket_off, uint8_t* __restrict__ tailq,
+                                                     int64_t* __restrict__ goff) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        int64_t acc = 0;
+        for (int c = 0; c < C; ++c) {
+            goff[c] = acc;
+            acc += nrows_c ? nrows_c[c] : bucket_off[c + 1] - bucket_off[c];
+        }
+        goff[C] = acc;
+    }
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= (int64_t)nq * R) return;
+    const int c = classes[p];
+    uint8_t t = 0;
+    if (c >= 0 && c < C) {
+        const int r = (int)(p % R);
+        const int m4 = grp[(size_t)r * C + c] & 3;
+        if (m4) {
+            int later = 0;
+            for (int64_t q2 = p / R + 1; q2 < nq && later < m4; ++q2) later += classes[q2 * R + r] == c ? 1 : 0;
+            t = later < m4 ? 1 : 0;
+        }
+    }
+    tailq[p] = t;
 }
 
 template <bool OUT64>
@@ -1011,7 +1094,9 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
             const int64_t x = band ? (int64_t)sr[j] : (int64_t)(uint32_t)src[j];
             const bool ok = x >= 0 && x < a.n_rows;
             if (!ok) atomicOr(a.status, LMI_STATUS_INTERNAL);
-            sd[j] = ok ? (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern) : __builtin_inf();
+            sd[j] = ok ? (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
+                                             kern == 1 && blas32_corner(a, p, (int32_t)x))
+                       : __builtin_inf();
             sr[j] = ok ? (int32_t)x : INT32_MAX;
         }
     }
@@ -1085,7 +1170,9 @@ __device__ inline uint64_t wave_min_u64(uint64_t v) {
 // distance, row) are taken by k wave minima -- the (distance, g.index) order,
 // rows ascending with global position inside a bucket shard.
 template <typename TC, typename TQ, bool OUT64, int KB = kB>
-__global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) == 8 ? 1 : KB >= 4 ? 4 : KB == 2 ? 5 : 7))) void x_select_wave_kernel(XArgs a, int32_t n_pairs) {
+// (the float32 output runs the reference's float32 order per lane, blas32_dist:
+// 4 waves per SIMD leave it the registers of its 64-value load blocks)
+__global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) == 8 ? 1 : !OUT64 ? 4 : KB >= 4 ? 4 : KB == 2 ? 5 : 7))) void x_select_wave_kernel(XArgs a, int32_t n_pairs) {
     __shared__ int32_t s_rows[kXT / 64][kXW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int pp = blockIdx.x * (kXT / 64) + w;
@@ -1152,7 +1239,8 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
                 if (x < 0 || x >= a.n_rows) {
                     atomicOr(a.status, LMI_STATUS_INTERNAL);
                 } else {
-                    mine[s] = (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern);
+                    mine[s] = (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
+                                                  kern == 1 && blas32_corner(a, p, (int32_t)x));
                     mrow[s] = (int32_t)x;
                 }
             }
@@ -1330,13 +1418,17 @@ int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s) {
     if (a.qn32) {
         // the reference's float32 order: the queries normalised as sklearn
         // does, the (round, bucket) group sizes (XArgs; oracle blas32_*)
-        hipLaunchKernelGGL(x_qn32_kernel, dim3((unsigned)((a.nq + 63) / 64)), dim3(64), 0, s, a.q, a.ldq, a.nq,
+        hipLaunchKernelGGL(x_qn32_kernel, dim3((unsigned)((a.nq + 3) / 4)), dim3(256), 0, s, a.q, a.ldq, a.nq,
                            a.d, a.d_pad, const_cast<float*>(a.qn32));
         LMI_LAUNCH_CHECK("x_qn32_kernel");
         LMI_TRY(fill_u32(const_cast<int32_t*>(a.grp), 0u, (size_t)a.R * a.C, s));
         hipLaunchKernelGGL(x_groups_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a.classes, P, a.R,
                            a.C, const_cast<int32_t*>(a.grp));
         LMI_LAUNCH_CHECK("x_groups_kernel");
+        hipLaunchKernelGGL(x_tail_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a.classes, a.nq, a.R,
+                           a.C, a.grp, a.nrows_c, a.bucket_off, const_cast<uint8_t*>(a.tailq),
+                           const_cast<int64_t*>(a.goff));
+        LMI_LAUNCH_CHECK("x_tail_kernel");
     }
     return launch_x3<float, float, false>(a, P, s);
 }

@@ -1673,7 +1673,7 @@ double split_eps(int d_pad) {
 namespace {
 struct XWs {
     size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
-        classes2, qn32, grp, region, region_bytes, total;
+        classes2, qn32, grp, tailq, goff, region, region_bytes, total;
     int32_t cap;
 };
 // k <= 10: the k-th of a per-bucket sample (the product scan over
@@ -1725,6 +1725,8 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.classes2 = take(P * 4);
     w.qn32 = take((size_t)nq * idx->d_pad * 4);
     w.grp = take((size_t)R * idx->n_buckets * 4);
+    w.tailq = take(P);
+    w.goff = take(((size_t)idx->n_buckets + 1) * 8);
     w.bound = take(P * 4);
     w.ccount = take(P * 4);
     w.cand = take(P * (size_t)cap * 8);
@@ -1879,6 +1881,8 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     a.grp = (const int32_t*)(ws + w.grp);
     a.nrows_c = idx->bucket_rows;
     a.C = idx->n_buckets;
+    a.tailq = (const uint8_t*)(ws + w.tailq);
+    a.goff = (const int64_t*)(ws + w.goff);
     // (pairs whose class is out of range keep the prefill of step 1's prep:
     // the outputs are prefilled here, by pair id, in step 3's own buffers)
     hipLaunchKernelGGL(x_prefill_kernel, dim3((unsigned)(((int64_t)P * k + 255) / 256)), dim3(256), 0, s,

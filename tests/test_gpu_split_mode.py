@@ -249,7 +249,9 @@ def test_split_float32_is_the_references_own_arithmetic(mode, seed):
             kern = O.blas32_kernel(int(grp[classes[i, r]]), int(sizes[classes[i, r]]), x.shape[1])
             keep[i, r] = kern is not None
             kinds.add(kern)
-    assert keep.mean() > 0.9 and "blocked" in kinds
+    # (groups of one query -- OpenBLAS's gemv, whose order follows its thread
+    # split -- keep the exact value rounded: many at 200 queries x 16 buckets)
+    assert keep.sum() > 100 and kinds & {"small", "blocked"}
     gd, gp = d.cpu().numpy()[keep], p.cpu().numpy()[keep]
     rd, rp = ref_d[keep], ref_p[keep]
     np.testing.assert_array_equal(gd, rd)     # float32 distances: bit for bit

@@ -32,7 +32,8 @@ pytestmark = pytest.mark.skipif(_blas_is_skylakex() != "SkylakeX",
 
 
 @pytest.mark.parametrize("M,N", [(2, 4), (4, 2), (5, 17), (13, 80), (16, 75), (4, 300), (5, 241),
-                                 (100, 40), (24, 64), (40, 200)])
+                                 (100, 40), (24, 64), (40, 200), (25, 14), (6, 7), (13, 22), (7, 30),
+                                 (15, 9), (31, 37)])
 def test_blas32_pairwise_cosine_is_numpys(M, N):
     rng = np.random.default_rng(M * 1000 + N)
     x = (rng.standard_normal((M, 768)) * 0.05 + 0.01).astype(np.float32)
@@ -47,6 +48,21 @@ def test_blas32_kernel_boundary():
     assert O.blas32_kernel(4, 301, 768) == "blocked"
     assert O.blas32_kernel(1, 50, 768) is None           # gemv
     assert O.blas32_kernel(3, 3, 768) is None            # tiny
+
+
+def test_blas32_random_small_shapes():
+    """Sixty random shapes of the small-matrix kernel (every corner block
+    remainder): all bit for bit."""
+    rng = np.random.default_rng(5)
+    n = 0
+    while n < 60:
+        M, N = int(rng.integers(2, 40)), int(rng.integers(2, 60))
+        if O.blas32_kernel(M, N, 768) != "small":
+            continue
+        x = rng.standard_normal((M, 768)).astype(np.float32)
+        y = rng.standard_normal((N, 768)).astype(np.float32)
+        np.testing.assert_array_equal(O.blas32_pairwise_cosine(x, y), O.pairwise_cosine(x, y))
+        n += 1
 
 
 def test_blas32_on_the_r5_fixture_groups():
