@@ -233,6 +233,7 @@ struct XArgs {
     // last M mod 4 of its group; goff [C+1] the buckets' global offsets)
     const uint8_t* tailq;
     const int64_t* goff;
+    const int32_t* plan_counts;  // [C] pairs per bucket (the collect scan's plan)
 };
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);

@@ -803,6 +803,7 @@ __device__ inline void query_hat_x(const TQ* qrow, int d, int nps, double zero_e
 constexpr int kBlasSmallMNK = 96 * 96 * 100;
 constexpr int kBlasKBlock = 384;
 constexpr float kEps32f = 1.1920928955078125e-07f;
+constexpr int LMI_MAX_R = 16;  // rounds the tail flags rank at once
 
 // 0: not restated (the exact value rounded), 1: small kernel, 2: blocked
 __device__ inline int blas32_kernel_of(const XArgs& a, int64_t p) {
@@ -836,61 +837,62 @@ __device__ inline float div_rn(float x, float n, float rn) {
 }
 
 // 1 - <qn, y / |y|> in the reference's float32 order (kern from
-// blas32_kernel_of; qn normalised by x_qn32_kernel): sklearn's norm of y in
-// the einsum order, the division, the dot's chains.  A lane per candidate:
-// each step's loads go out a block of 64 values ahead of their use.
-__device__ inline float blas32_dist(const float* y, const float* qn, int d, int kern, bool corner) {
+// blas32_kernel_of; qn normalised by x_qn32_kernel), a quad of lanes per
+// candidate (every lane of the quad returns it): lane w = lane & 3 runs the
+// einsum's chain w (the values 16 g + 4 v + w, v = 3 .. 0) and the small
+// kernel's chains 4 v + w (v = 0 .. 3) -- the quad's four lanes read four
+// consecutive values, so each wave instruction touches 16 cache lines, not
+// 64 as a lane per row did -- and every lane of the quad runs the blocked
+// kernel's (sequential) chains itself
+__device__ inline float blas32_dist_quad(const float* y, const float* qn, int d, int kern, bool corner) {
 #pragma clang fp contract(off)
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+    const int w = threadIdx.x & 3;
+    float a = 0.0f;
     for (int g0 = 0; g0 < d; g0 += 64) {
-        float4 x[16];
+        float x[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + g0 + 4 * i);
+        for (int i = 0; i < 16; ++i) x[i] = y[g0 + 4 * i + w];
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg)
 #pragma unroll
-            for (int v = 3; v >= 0; --v) {
-                const float4 t = x[4 * gg + v];
-                a0 = a0 + t.x * t.x;
-                a1 = a1 + t.y * t.y;
-                a2 = a2 + t.z * t.z;
-                a3 = a3 + t.w * t.w;
-            }
+            for (int v = 3; v >= 0; --v) a = a + x[4 * gg + v] * x[4 * gg + v];
     }
-    float n = __builtin_sqrtf((a0 + a1) + (a2 + a3));
+    const int qb = (threadIdx.x & 63) & ~3;
+    const float s01 = __shfl(a, qb) + __shfl(a, qb + 1), s23 = __shfl(a, qb + 2) + __shfl(a, qb + 3);
+    float n = __builtin_sqrtf(s01 + s23);
     if (n < 10.0f * kEps32f) n = 1.0f;
     const float rn = 1.0f / n;
     float s;
     if (kern == 1) {
-        float c[16];
-#pragma unroll
-        for (int l = 0; l < 16; ++l) c[l] = 0.0f;
-        for (int e0 = 0; e0 < d; e0 += 64) {
-            float4 x[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + e0 + 4 * i);
+        float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // chains 4 v + w
+        for (int g0 = 0; g0 < d; g0 += 64) {
+            float x[16], q[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * i);
-                const int l = (4 * i) & 15;
-                c[l + 0] = __builtin_fmaf(q.x, div_rn(x[i].x, n, rn), c[l + 0]);
-                c[l + 1] = __builtin_fmaf(q.y, div_rn(x[i].y, n, rn), c[l + 1]);
-                c[l + 2] = __builtin_fmaf(q.z, div_rn(x[i].z, n, rn), c[l + 2]);
-                c[l + 3] = __builtin_fmaf(q.w, div_rn(x[i].w, n, rn), c[l + 3]);
+                x[i] = y[g0 + 4 * i + w];
+                q[i] = qn[g0 + 4 * i + w];
             }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) c[i & 3] = __builtin_fmaf(q[i], div_rn(x[i], n, rn), c[i & 3]);
         }
+        // chain l = 4 v + w sits in lane w as c[v]: all sixteen to every lane
+        float t[16];
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) t[4 * v + ww] = __shfl(c[v], qb + ww);
         if (corner) {
 #pragma unroll
             for (int h = 8; h >= 1; h >>= 1)
 #pragma unroll
-                for (int i = 0; i < h; ++i) c[i] = c[i] + c[i + h];
+                for (int i = 0; i < h; ++i) t[i] = t[i] + t[i + h];
         } else {
 #pragma unroll
             for (int h = 8; h >= 1; h >>= 1)
 #pragma unroll
-                for (int i = 0; i < h; ++i) c[i] = c[2 * i] + c[2 * i + 1];
+                for (int i = 0; i < h; ++i) t[i] = t[2 * i] + t[2 * i + 1];
         }
-        s = c[0];
+        s = t[0];
     } else {
         s = 0.0f;
         for (int b0 = 0; b0 < d; b0 += kBlasKBlock) {
@@ -955,35 +957,49 @@ __global__ __launch_bounds__(256) void x_groups_kernel(const int32_t* __restrict
 }
 
 // tailq[pair (q, r)] = q is among the last M mod 4 queries of its group
-// (fewer than M mod 4 later queries share its class in round r), and the
-// buckets' global offsets (one thread of block 0)
-__global__ __launch_bounds__(256) void x_tail_kernel(const int32_t* __restrict__ classes, int32_t nq, int32_t R,
-                                                     int32_t C, const int32_t* __restrict__ grp,
-                                                     const int64_t* __restrict__ nrows_c,
-                                                     const int64_t* __restrict__ bucket_off, uint8_t* __restrict__ tailq,
-                                                     int64_t* __restrict__ goff) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+// (its rank in the group, ascending q, is >= 4 floor(M / 4)), a wave per
+// bucket over the collect scan's plan (the bucket's pairs in ascending pair
+// id, so every round's pairs in ascending q: ranks by ballots, 64 pairs at a
+// time); and the buckets' global offsets (block 0, lane 0)
+__global__ __launch_bounds__(64) void x_tail_kernel(const int32_t* __restrict__ pair_q,
+                                                    const int32_t* __restrict__ counts, int32_t R, int32_t C,
+                                                    const int32_t* __restrict__ grp,
+                                                    const int64_t* __restrict__ nrows_c,
+                                                    const int64_t* __restrict__ bucket_off, uint8_t* __restrict__ tailq,
+                                                    int64_t* __restrict__ goff) {
+    const int lane = threadIdx.x, c = blockIdx.x;
+    if (c == 0 && lane == 0) {
         int64_t acc = 0;
-        for (int c = 0; c < C; ++c) {
-            goff[c] = acc;
-            acc += nrows_c ? nrows_c[c] : bucket_off[c + 1] - bucket_off[c];
+        for (int b = 0; b < C; ++b) {
+            goff[b] = acc;
+            acc += nrows_c ? nrows_c[b] : bucket_off[b + 1] - bucket_off[b];
         }
         goff[C] = acc;
     }
-    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (p >= (int64_t)nq * R) return;
-    const int c = classes[p];
-    uint8_t t = 0;
-    if (c >= 0 && c < C) {
-        const int r = (int)(p % R);
-        const int m4 = grp[(size_t)r * C + c] & 3;
-        if (m4) {
-            int later = 0;
-            for (int64_t q2 = p / R + 1; q2 < nq && later < m4; ++q2) later += classes[q2 * R + r] == c ? 1 : 0;
-            t = later < m4 ? 1 : 0;
+    int s = 0;
+    for (int b = lane; b < c; b += 64) s += counts[b];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    const int e = s + counts[c];
+    const uint64_t below = (1ull << lane) - 1ull;
+    int base[LMI_MAX_R];
+#pragma unroll
+    for (int r = 0; r < LMI_MAX_R; ++r) base[r] = 0;
+    for (int i0 = s; i0 < e; i0 += 64) {
+        const int i = i0 + lane;
+        const int p = i < e ? pair_q[i] : -1;
+        const int rp = p >= 0 ? p % R : -1;
+        int rank = 0;
+#pragma unroll
+        for (int r = 0; r < LMI_MAX_R; ++r) {
+            if (r < R) {
+                const uint64_t m = __ballot(rp == r);
+                if (rp == r) rank = base[r] + __popcll(m & below);
+                base[r] += __popcll(m);
+            }
         }
+        if (p >= 0) tailq[p] = rank >= (grp[(size_t)rp * C + c] & ~3) ? 1 : 0;
     }
-    tailq[p] = t;
 }
 
 template <bool OUT64>
@@ -1088,16 +1104,21 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     }
     const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
     if (kern != 0) {
-        // the reference's float32 order: a candidate per thread
+        // the reference's float32 order: a quad of lanes per candidate
         const float* qn = a.qn32 + (size_t)(p / a.R) * a.d_pad;
-        for (uint32_t j = tid; j < nr; j += kXT) {
-            const int64_t x = band ? (int64_t)sr[j] : (int64_t)(uint32_t)src[j];
+        for (uint32_t j0 = 0; j0 < nr; j0 += kXT / 4) {
+            const uint32_t j = j0 + (tid >> 2);
+            const int64_t x = j < nr ? (band ? (int64_t)sr[j] : (int64_t)(uint32_t)src[j]) : -1;
             const bool ok = x >= 0 && x < a.n_rows;
-            if (!ok) atomicOr(a.status, LMI_STATUS_INTERNAL);
-            sd[j] = ok ? (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
-                                             kern == 1 && blas32_corner(a, p, (int32_t)x))
-                       : __builtin_inf();
-            sr[j] = ok ? (int32_t)x : INT32_MAX;
+            const float v = ok ? blas32_dist_quad(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
+                                                  kern == 1 && blas32_corner(a, p, (int32_t)x))
+                               : __builtin_inff();
+            __syncthreads();  // (every quad read its row index before any is overwritten)
+            if (j < nr && (tid & 3) == 0) {
+                if (!ok) atomicOr(a.status, LMI_STATUS_INTERNAL);
+                sd[j] = ok ? (double)v : __builtin_inf();
+                sr[j] = ok ? (int32_t)x : INT32_MAX;
+            }
         }
     }
     for (uint32_t j0 = (uint32_t)w * kB; kern == 0 && j0 < nr; j0 += (kXT / 64) * kB) {
@@ -1229,19 +1250,27 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
     }
     const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
     if (kern != 0) {
-        // the reference's float32 order: a candidate per lane (each a chain)
+        // the reference's float32 order: a quad of lanes per candidate, 16
+        // at a time; entry j's value moves to its keeper, lane j % 64
         const float* qn = a.qn32 + (size_t)(p / a.R) * a.d_pad;
+        for (int j0 = 0; j0 < nr; j0 += 16) {
+            const int jq = j0 + (lane >> 2);
+            int64_t x = jq < nr ? (int64_t)rows[jq] : -1;
+            const bool ok = x >= 0 && x < a.n_rows;
+            if (jq < nr && !ok && (lane & 3) == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
+            const float v = ok ? blas32_dist_quad(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
+                                                  kern == 1 && blas32_corner(a, p, (int32_t)x))
+                               : __builtin_inff();
+            // (lanes j0 % 64 .. + 15 keep entries j0 .. j0 + 15, slot j0 / 64)
+            const int t = lane - (j0 & 63);
+            const float mv = __shfl(v, 4 * (t & 15));
+            const int32_t mx = __shfl(ok ? (int32_t)x : INT32_MAX, 4 * (t & 15));
+            if (t >= 0 && t < 16 && j0 + t < nr) {
+                const int sl = j0 >> 6;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int j = 64 * s + lane;
-            if (j < nr) {
-                const int64_t x = rows[j];
-                if (x < 0 || x >= a.n_rows) {
-                    atomicOr(a.status, LMI_STATUS_INTERNAL);
-                } else {
-                    mine[s] = (double)blas32_dist(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
-                                                  kern == 1 && blas32_corner(a, p, (int32_t)x));
-                    mrow[s] = (int32_t)x;
+                for (int s = 0; s < 4; ++s) {
+                    mine[s] = s == sl ? (double)mv : mine[s];
+                    mrow[s] = s == sl ? mx : mrow[s];
                 }
             }
         }
@@ -1425,9 +1454,9 @@ int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s) {
         hipLaunchKernelGGL(x_groups_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a.classes, P, a.R,
                            a.C, const_cast<int32_t*>(a.grp));
         LMI_LAUNCH_CHECK("x_groups_kernel");
-        hipLaunchKernelGGL(x_tail_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, a.classes, a.nq, a.R,
-                           a.C, a.grp, a.nrows_c, a.bucket_off, const_cast<uint8_t*>(a.tailq),
-                           const_cast<int64_t*>(a.goff));
+        LMI_CHECK_ARG(a.R <= LMI_MAX_R, "R=%d > %d", a.R, LMI_MAX_R);
+        hipLaunchKernelGGL(x_tail_kernel, dim3((unsigned)a.C), dim3(64), 0, s, a.pair_q, a.plan_counts, a.R, a.C,
+                           a.grp, a.nrows_c, a.bucket_off, const_cast<uint8_t*>(a.tailq), const_cast<int64_t*>(a.goff));
         LMI_LAUNCH_CHECK("x_tail_kernel");
     }
     return launch_x3<float, float, false>(a, P, s);

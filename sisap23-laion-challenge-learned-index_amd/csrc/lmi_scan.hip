@@ -1883,6 +1883,7 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     a.C = idx->n_buckets;
     a.tailq = (const uint8_t*)(ws + w.tailq);
     a.goff = (const int64_t*)(ws + w.goff);
+    a.plan_counts = (const int32_t*)(region + l.counts);
     // (pairs whose class is out of range keep the prefill of step 1's prep:
     // the outputs are prefilled here, by pair id, in step 3's own buffers)
     hipLaunchKernelGGL(x_prefill_kernel, dim3((unsigned)(((int64_t)P * k + 255) / 256)), dim3(256), 0, s,
