@@ -483,9 +483,10 @@ def main():
     q16_exact = index.storage == "f16" and all(
         bool(np.array_equal(b.astype(np.float16).astype(np.float32), b)) for _, b in host_batches)
     # the batch stream takes fp16-exact batches on an fp16 index (the phased
-    # scan); over gloo (the multi-rank rehearsal on one GPU) its stages run
-    # eagerly (gloo collectives cannot be captured)
-    use_stream = not args.no_graph and not args.no_stream and q16_exact
+    # scan), or float32 batches on the split mode's index (its phases, ABI 11);
+    # over gloo (the multi-rank rehearsal on one GPU) its stages run eagerly
+    # (gloo collectives cannot be captured)
+    use_stream = not args.no_graph and not args.no_stream and (q16_exact or index.storage == "f32x")
     qn_pin = torch.from_numpy(qn_h).pin_memory()
     q_pin = torch.from_numpy(q_h.astype(np.float16) if q16_exact else q_h).pin_memory()
     checks = {}

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 10
+#define LMI_ABI_VERSION 11
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -166,7 +166,11 @@ typedef struct lmi_index_desc {
      *      (distance, position) -- rounded to float32 first for the float32
      *      mode -- and the first k kept; a pair with more candidates than the
      *      collect buffer holds is scanned whole in float64.
-     * Needs d_pad == 768 (the fp16 scan's width) and no phase flags.
+     * Needs d_pad == 768 (the fp16 scan's width).  ABI 11: k <= 10 takes the
+     * phase flags (LMI_Q_PHASE_PLAN: the rounded queries and both scans'
+     * plans; SCAN: the sample scan, the bound and the collect scan; MERGE:
+     * step 3), so a stream of batches runs one batch's re-score beside the
+     * next one's scans; other k, no phase flags.
      * ABI 10: the float32 arithmetic re-scores in the reference's own float32
      * operation order -- sklearn's normalize (numpy einsum row norms, a
      * division) and OpenBLAS sgemm's summation order for the (round, bucket)
@@ -174,13 +178,21 @@ typedef struct lmi_index_desc {
      * the libraries the reference runs on in the build container) -- so its
      * float32 distances are the reference's bit for bit; shapes whose BLAS
      * path is not restated (a group of one query or one row, groups of at
-     * most 3 x 3) and the whole-shard fallback keep the exact value rounded
-     * to float32. */
+     * most 3 x 3) keep the exact value rounded to float32 (ABI 11: the
+     * whole-shard fallback follows the reference's order too). */
     const float* corpus32;
     /* ABI 10: optional (NULL = this shard's own) device [n_buckets] int64: the
      * rows of every bucket in the whole index (a G-GPU index's shards hold
      * slices): the shape of the reference's per-bucket product. */
     const int64_t* bucket_rows;
+    /* ABI 11: optional (NULL = normalised per candidate inside the call)
+     * device [n_rows][d_pad] float32: corpus32's rows divided by their
+     * float32 norms as sklearn's normalize computes them (numpy einsum row
+     * norms, zero rule, IEEE division; lmi_split_normalize fills it).  The
+     * normalised row depends on the row alone, so the float32 re-score then
+     * runs only the product's summation chains per candidate.  Same float32
+     * distances, bit for bit, with or without it. */
+    const float* corpus32n;
 } lmi_index_desc;
 
 /* Host helper: fills chunk_first_out[C+1] from host bucket offsets and returns
@@ -307,6 +319,12 @@ int lmi_bucket_topk_f64g(const lmi_index_desc* idx, const float* q, int32_t nq, 
  * is used), and so is the fp16 / fp32 class of qmode (the queries are
  * normalised and rounded inside the call). */
 double lmi_split_eps(int32_t d_pad);
+/* ABI 11: lmi_index_desc.corpus32n from corpus32 (device [n][d_pad] float32
+ * in and out, out's padding zeroed; a wave per row, index build, not the hot
+ * path).  Replaces, per row, the normalize(Y) of the reference's
+ * cosine_distances (utils.py:10-11; sklearn normalize: numpy einsum norms). */
+int lmi_split_normalize(const float* rows, int64_t n, int32_t d, int32_t d_pad, float* out,
+                        void* stream);
 /* Diagnostic (synchronises `stream`): how many (query, probe) pairs of the
  * last lmi_bucket_topk_f64 call on this workspace took the whole-bucket path
  * (the split mode: also of lmi_bucket_topk, whose workspace has the same layout). */

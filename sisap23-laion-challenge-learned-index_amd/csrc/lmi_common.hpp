@@ -234,6 +234,9 @@ struct XArgs {
     const uint8_t* tailq;
     const int64_t* goff;
     const int32_t* plan_counts;  // [C] pairs per bucket (the collect scan's plan)
+    // ABI 11: rows32 normalised as sklearn does in float32 (idx->corpus32n) or
+    // null (then normalised per candidate)
+    const float* rows32n;
 };
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);
@@ -241,7 +244,8 @@ size_t x_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k);
 size_t x_nfailed_offset(const lmi_index_desc* idx, int nq, int R, int k);
 int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq, const double* q64,
                   int32_t ldq64, const int32_t* classes, int32_t R, int32_t k, void* out_d, int out_f64,
-                  int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes, hipStream_t s);
+                  int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes, hipStream_t s,
+                  int phases = kPhaseAll);
 
 // n_words 32-bit words of `value` from p (4-byte aligned) on stream s, by a
 // kernel (lmi_merge.hip): workspace initialisation stays a kernel node when a

@@ -838,30 +838,36 @@ __device__ inline float div_rn(float x, float n, float rn) {
 
 // 1 - <qn, y / |y|> in the reference's float32 order (kern from
 // blas32_kernel_of; qn normalised by x_qn32_kernel), a quad of lanes per
-// candidate (every lane of the quad returns it): lane w = lane & 3 runs the
-// einsum's chain w (the values 16 g + 4 v + w, v = 3 .. 0) and the small
-// kernel's chains 4 v + w (v = 0 .. 3) -- the quad's four lanes read four
-// consecutive values, so each wave instruction touches 16 cache lines, not
-// 64 as a lane per row did -- and every lane of the quad runs the blocked
-// kernel's (sequential) chains itself
+// candidate (every lane of the quad returns it).  NORMED: y is the row
+// already normalised (lmi_index_desc.corpus32n: the row's own norm and
+// division, done once at build), else lane w = lane & 3 runs the einsum's
+// chain w (the values 16 g + 4 v + w, v = 3 .. 0) and every value is divided
+// here.  Small kernel: lane w runs the chains 4 v + w (v = 0 .. 3) -- the
+// quad's four lanes read four consecutive values, so each wave instruction
+// touches 16 cache lines, not 64 as a lane per row did.  Blocked kernel: lane
+// w runs the chain of K block w (d <= 4 * 384), the blocks then added in order.
+template <bool NORMED>
 __device__ inline float blas32_dist_quad(const float* y, const float* qn, int d, int kern, bool corner) {
 #pragma clang fp contract(off)
     const int w = threadIdx.x & 3;
-    float a = 0.0f;
-    for (int g0 = 0; g0 < d; g0 += 64) {
-        float x[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) x[i] = y[g0 + 4 * i + w];
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg)
-#pragma unroll
-            for (int v = 3; v >= 0; --v) a = a + x[4 * gg + v] * x[4 * gg + v];
-    }
     const int qb = (threadIdx.x & 63) & ~3;
-    const float s01 = __shfl(a, qb) + __shfl(a, qb + 1), s23 = __shfl(a, qb + 2) + __shfl(a, qb + 3);
-    float n = __builtin_sqrtf(s01 + s23);
-    if (n < 10.0f * kEps32f) n = 1.0f;
-    const float rn = 1.0f / n;
+    float n = 1.0f, rn = 1.0f;
+    if constexpr (!NORMED) {
+        float a = 0.0f;
+        for (int g0 = 0; g0 < d; g0 += 64) {
+            float x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = y[g0 + 4 * i + w];
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+                for (int v = 3; v >= 0; --v) a = a + x[4 * gg + v] * x[4 * gg + v];
+        }
+        const float s01 = __shfl(a, qb) + __shfl(a, qb + 1), s23 = __shfl(a, qb + 2) + __shfl(a, qb + 3);
+        n = __builtin_sqrtf(s01 + s23);
+        if (n < 10.0f * kEps32f) n = 1.0f;
+        rn = 1.0f / n;
+    }
     float s;
     if (kern == 1) {
         float c[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // chains 4 v + w
@@ -873,7 +879,10 @@ __device__ inline float blas32_dist_quad(const float* y, const float* qn, int d,
                 q[i] = qn[g0 + 4 * i + w];
             }
 #pragma unroll
-            for (int i = 0; i < 16; ++i) c[i & 3] = __builtin_fmaf(q[i], div_rn(x[i], n, rn), c[i & 3]);
+            for (int i = 0; i < 16; ++i) {
+                if constexpr (NORMED) c[i & 3] = __builtin_fmaf(q[i], x[i], c[i & 3]);
+                else c[i & 3] = __builtin_fmaf(q[i], div_rn(x[i], n, rn), c[i & 3]);
+            }
         }
         // chain l = 4 v + w sits in lane w as c[v]: all sixteen to every lane
         float t[16];
@@ -894,26 +903,88 @@ __device__ inline float blas32_dist_quad(const float* y, const float* qn, int d,
         }
         s = t[0];
     } else {
-        s = 0.0f;
-        for (int b0 = 0; b0 < d; b0 += kBlasKBlock) {
-            float c = 0.0f;
-            const int b1 = b0 + kBlasKBlock < d ? b0 + kBlasKBlock : d;
-            for (int e0 = b0; e0 < b1; e0 += 64) {
-                float4 x[16];
+        float c = 0.0f;
+        const int b0 = w * kBlasKBlock;
+        const int b1 = b0 + kBlasKBlock < d ? b0 + kBlasKBlock : d;
+        for (int e0 = b0; e0 < b1; e0 += 64) {
+            // (a 64-value step passes b1 only inside d_pad's zero padding:
+            // d_pad = 768 and d a multiple of 16 in the split mode)
+            float4 x[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + e0 + 4 * i);
+            for (int i = 0; i < 16; ++i) x[i] = *reinterpret_cast<const float4*>(y + e0 + 4 * i);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * i);
+            for (int i = 0; i < 16; ++i) {
+                const float4 q = *reinterpret_cast<const float4*>(qn + e0 + 4 * i);
+                if constexpr (NORMED) {
+                    c = __builtin_fmaf(q.x, x[i].x, c);
+                    c = __builtin_fmaf(q.y, x[i].y, c);
+                    c = __builtin_fmaf(q.z, x[i].z, c);
+                    c = __builtin_fmaf(q.w, x[i].w, c);
+                } else {
                     c = __builtin_fmaf(q.x, div_rn(x[i].x, n, rn), c);
                     c = __builtin_fmaf(q.y, div_rn(x[i].y, n, rn), c);
                     c = __builtin_fmaf(q.z, div_rn(x[i].z, n, rn), c);
                     c = __builtin_fmaf(q.w, div_rn(x[i].w, n, rn), c);
                 }
             }
-            s = b0 == 0 ? c : s + c;
+        }
+        const int nb = (d + kBlasKBlock - 1) / kBlasKBlock;
+        s = __shfl(c, qb);
+        for (int b = 1; b < nb; ++b) s = s + __shfl(c, qb + b);
+    }
+    return 1.0f - s;
+}
+
+// Lanes per candidate of the float32 re-score (wave-uniform: kern is the
+// pair's): the blocked kernel on normalised rows takes one lane per K block
+// (d <= 768: 1 or 2 lanes), everything else a quad (blas32_dist_quad)
+__device__ inline int blas32_lanes(const XArgs& a, int kern) {
+    return (kern == 2 && a.rows32n) ? (a.d + kBlasKBlock - 1) / kBlasKBlock : 4;
+}
+
+// The float32 distance of local row x in the reference's order by its group
+// of L = blas32_lanes lanes (every lane of the group returns it; ok is the
+// group's).  L < 4: lane b of the group runs the chain of K block b over the
+// normalised row, the blocks then added in order.
+// NORM: a.rows32n is set (a compile-time split: each form keeps only its own
+// registers).
+template <bool NORM>
+__device__ inline float blas32_dist_group(const XArgs& a, int64_t p, const float* qn, int64_t x, bool ok,
+                                          int kern, int L) {
+#pragma clang fp contract(off)
+    if (!ok) return __builtin_inff();
+    if (!NORM || L == 4) {
+        const bool cr = kern == 1 && blas32_corner(a, p, (int32_t)x);
+        return blas32_dist_quad<NORM>((NORM ? a.rows32n : a.rows32) + (size_t)x * a.d_pad, qn, a.d, kern, cr);
+    }
+    // the query's two K blocks through the scalar cache (qn is the pair's:
+    // wave-uniform; the constant address space lets the loads be scalar) and
+    // each lane's block picked per element; d_pad = 768 in the split mode, so
+    // block 1's 384 values are inside the query's row even when L == 1, and a
+    // step past d reads the zero padding (adding exact zeros)
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    using cv4f = __attribute__((address_space(4))) const v4f;
+    const cv4f* q0 = (cv4f*)(qn);
+    const cv4f* q1 = (cv4f*)(qn + kBlasKBlock);
+    const bool hi = (threadIdx.x & (L - 1)) != 0;
+    const float* y = a.rows32n + (size_t)x * a.d_pad + (hi ? kBlasKBlock : 0);
+    float c = 0.0f;
+    for (int e0 = 0; e0 < kBlasKBlock; e0 += 64) {
+        float4 v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = *reinterpret_cast<const float4*>(y + e0 + 4 * i);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const v4f qa = q0[e0 / 4 + i], qb = q1[e0 / 4 + i];
+            c = __builtin_fmaf(hi ? qb.x : qa.x, v[i].x, c);
+            c = __builtin_fmaf(hi ? qb.y : qa.y, v[i].y, c);
+            c = __builtin_fmaf(hi ? qb.z : qa.z, v[i].z, c);
+            c = __builtin_fmaf(hi ? qb.w : qa.w, v[i].w, c);
         }
     }
+    const int base = (threadIdx.x & 63) & ~(L - 1);
+    float s = __shfl(c, base);
+    for (int b = 1; b < L; ++b) s = s + __shfl(c, base + b);
     return 1.0f - s;
 }
 
@@ -1037,17 +1108,12 @@ __device__ inline bool x_wave_pair(const XArgs& a, uint32_t n, int p) {
     return a.two_eps > 0.0 && n <= (uint32_t)kXW && n <= (uint32_t)a.cap && !(a.fix && a.fix[p]);
 }
 
-// One workgroup per grouped pair of the collect scan: the exact distance of
+// A workgroup on one grouped pair of the collect scan: the exact distance of
 // every candidate (a wave per kB rows), a bitonic sort of (distance, row) in
 // LDS -- rows ascend with global position inside a bucket shard, so this is
 // the reference's (distance, g.index) order -- and the first k written.
 template <typename TC, typename TQ, bool OUT64>
-__global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
-    extern __shared__ double x_lds[];
-    double* sd = x_lds;
-    int32_t* sr = reinterpret_cast<int32_t*>(x_lds + a.cap);
-    __shared__ uint32_t s_nr;
-    const int pp = blockIdx.x;
+__device__ inline void x_select_pair(const XArgs& a, const int pp, double* sd, int32_t* sr, uint32_t& s_nr) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (a.pair_bucket[pp] < 0) return;
     const int p = a.pair_q[pp];
@@ -1060,10 +1126,6 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
         if (tid == 0) a.failed[atomicAdd(a.n_failed, 1)] = p;
         return;
     }
-    const double zero_eps = OUT64 ? kEps64 : kEps32;
-    const int nps = (a.d + 255) / 256;
-    double qh[3][4];
-    query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
     const uint64_t* src = a.cand + (size_t)pp * a.cap;
     const bool band = a.two_eps > 0.0;
     uint32_t nr = n;  // candidates re-scored
@@ -1104,23 +1166,27 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     }
     const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
     if (kern != 0) {
-        // the reference's float32 order: a quad of lanes per candidate
+        // the reference's float32 order: a group of L lanes per candidate
         const float* qn = a.qn32 + (size_t)(p / a.R) * a.d_pad;
-        for (uint32_t j0 = 0; j0 < nr; j0 += kXT / 4) {
-            const uint32_t j = j0 + (tid >> 2);
+        const int L = blas32_lanes(a, kern);
+        for (uint32_t j0 = 0; j0 < nr; j0 += kXT / L) {
+            const uint32_t j = j0 + tid / L;
             const int64_t x = j < nr ? (band ? (int64_t)sr[j] : (int64_t)(uint32_t)src[j]) : -1;
             const bool ok = x >= 0 && x < a.n_rows;
-            const float v = ok ? blas32_dist_quad(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
-                                                  kern == 1 && blas32_corner(a, p, (int32_t)x))
-                               : __builtin_inff();
-            __syncthreads();  // (every quad read its row index before any is overwritten)
-            if (j < nr && (tid & 3) == 0) {
+            const float v = a.rows32n ? blas32_dist_group<true>(a, p, qn, x, ok, kern, L)
+                                       : blas32_dist_group<false>(a, p, qn, x, ok, kern, L);
+            __syncthreads();  // (every group read its row index before any is overwritten)
+            if (j < nr && (tid & (L - 1)) == 0) {
                 if (!ok) atomicOr(a.status, LMI_STATUS_INTERNAL);
                 sd[j] = ok ? (double)v : __builtin_inf();
                 sr[j] = ok ? (int32_t)x : INT32_MAX;
             }
         }
     }
+    const double zero_eps = OUT64 ? kEps64 : kEps32;
+    const int nps = (a.d + 255) / 256;
+    double qh[3][4];
+    if (kern == 0) query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
     for (uint32_t j0 = (uint32_t)w * kB; kern == 0 && j0 < nr; j0 += (kXT / 64) * kB) {
         int32_t r[kB];
 #pragma unroll
@@ -1174,6 +1240,20 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     }
 }
 
+// (a grid of a few workgroups per CU walks the grouped pairs: most of them
+// are the wave kernel's, and an early exit costs a loop step, not a
+// workgroup launch at this kernel's register count)
+template <typename TC, typename TQ, bool OUT64>
+__global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
+    extern __shared__ double x_lds[];
+    __shared__ uint32_t s_nr;
+    const int P = a.nq * a.R;
+    for (int pp = blockIdx.x; pp < P; pp += gridDim.x) {
+        x_select_pair<TC, TQ, OUT64>(a, pp, x_lds, reinterpret_cast<int32_t*>(x_lds + a.cap), s_nr);
+        __syncthreads();  // (the pair's LDS lists are read before the next pair's fill)
+    }
+}
+
 __device__ inline uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1190,13 +1270,14 @@ __device__ inline uint64_t wave_min_u64(uint64_t v) {
 // row list (any order), re-scored kB at a time, and the first k by (exact
 // distance, row) are taken by k wave minima -- the (distance, g.index) order,
 // rows ascending with global position inside a bucket shard.
-template <typename TC, typename TQ, bool OUT64, int KB = kB>
-// (the float32 output runs the reference's float32 order per lane, blas32_dist:
-// 4 waves per SIMD leave it the registers of its 64-value load blocks)
+template <typename TC, typename TQ, bool OUT64, int KB = kB, bool NORM = false>
+// (the float32 output runs the reference's float32 order, blas32_dist_group;
+// NORM: over the normalised rows, a.rows32n; 4 waves per SIMD leave it the
+// registers of its 64-value load blocks)
 __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) == 8 ? 1 : !OUT64 ? 4 : KB >= 4 ? 4 : KB == 2 ? 5 : 7))) void x_select_wave_kernel(XArgs a, int32_t n_pairs) {
     __shared__ int32_t s_rows[kXT / 64][kXW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int pp = blockIdx.x * (kXT / 64) + w;
+    const int pp = __builtin_amdgcn_readfirstlane(blockIdx.x * (kXT / 64) + w);
     if (pp >= n_pairs || a.pair_bucket[pp] < 0) return;
     const int p = a.pair_q[pp];
     const int64_t P = (int64_t)a.nq * a.R;
@@ -1211,10 +1292,6 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
         key[s] = i < n ? src[i] : kEmptyKey;
         work[s] = key[s];
     }
-    const double zero_eps = OUT64 ? kEps64 : kEps32;
-    const int nps = (a.d + 255) / 256;
-    double qh[3][4];
-    query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
     const int k = a.k;
     // the k-th smallest key (keys are distinct: one per row)
     uint64_t kth = kEmptyKey;
@@ -1250,22 +1327,21 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
     }
     const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
     if (kern != 0) {
-        // the reference's float32 order: a quad of lanes per candidate, 16
-        // at a time; entry j's value moves to its keeper, lane j % 64
+        // the reference's float32 order: a group of L lanes per candidate,
+        // 64 / L at a time; entry j's value moves to its keeper, lane j % 64
         const float* qn = a.qn32 + (size_t)(p / a.R) * a.d_pad;
-        for (int j0 = 0; j0 < nr; j0 += 16) {
-            const int jq = j0 + (lane >> 2);
+        const int L = blas32_lanes(a, kern), per = 64 / L;
+        for (int j0 = 0; j0 < nr; j0 += per) {
+            const int jq = j0 + lane / L;
             int64_t x = jq < nr ? (int64_t)rows[jq] : -1;
             const bool ok = x >= 0 && x < a.n_rows;
-            if (jq < nr && !ok && (lane & 3) == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
-            const float v = ok ? blas32_dist_quad(a.rows32 + (size_t)x * a.d_pad, qn, a.d, kern,
-                                                  kern == 1 && blas32_corner(a, p, (int32_t)x))
-                               : __builtin_inff();
-            // (lanes j0 % 64 .. + 15 keep entries j0 .. j0 + 15, slot j0 / 64)
+            if (jq < nr && !ok && (lane & (L - 1)) == 0) atomicOr(a.status, LMI_STATUS_INTERNAL);
+            const float v = blas32_dist_group<NORM>(a, p, qn, x, ok, kern, L);
+            // (lanes j0 % 64 .. + per - 1 keep entries j0 .. j0 + per - 1, slot j0 / 64)
             const int t = lane - (j0 & 63);
-            const float mv = __shfl(v, 4 * (t & 15));
-            const int32_t mx = __shfl(ok ? (int32_t)x : INT32_MAX, 4 * (t & 15));
-            if (t >= 0 && t < 16 && j0 + t < nr) {
+            const float mv = __shfl(v, L * (t & (per - 1)));
+            const int32_t mx = __shfl(ok ? (int32_t)x : INT32_MAX, L * (t & (per - 1)));
+            if (t >= 0 && t < per && j0 + t < nr) {
                 const int sl = j0 >> 6;
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
@@ -1275,6 +1351,12 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
             }
         }
     }
+    // (the query's float64 hat only where it is used: the float32 order's
+    // chains keep those registers)
+    const double zero_eps = OUT64 ? kEps64 : kEps32;
+    const int nps = (a.d + 255) / 256;
+    double qh[3][4];
+    if (kern == 0) query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
     for (int j0 = 0; kern == 0 && j0 < nr; j0 += KB) {
         int32_t r[KB];
 #pragma unroll
@@ -1332,8 +1414,10 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
 }
 
 // One workgroup per overflowed pair: the exact distance of every row of its
-// bucket shard (a wave per kB rows), lane 0 of each wave keeps the wave's
-// top-k by (distance, row) in LDS, thread 0 merges the waves' lists.
+// bucket shard (a wave per kB rows; the float32 output in the reference's
+// order, a quad per row, where blas32_kernel_of restates it), lane 0 of each
+// wave keeps the wave's top-k by (distance, row) in LDS, thread 0 merges the
+// waves' lists.
 template <typename TC, typename TQ, bool OUT64>
 __global__ __launch_bounds__(kFbT) void x_fallback_kernel(XArgs a) {
     __shared__ double sd[kFbT / 64][LMI_MAX_K];
@@ -1356,7 +1440,32 @@ __global__ __launch_bounds__(kFbT) void x_fallback_kernel(XArgs a) {
                 L[i] = __builtin_inf();
                 G[i] = INT32_MAX;
             }
-        for (int64_t r0 = b0 + (int64_t)w * kB; r0 < b1; r0 += (int64_t)(kFbT / 64) * kB) {
+        const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
+        // the reference's float32 order: a group of nl lanes per row, 64 / nl
+        // rows a wave, lane 0 keeping them in ascending row order
+        const int nl = kern != 0 ? blas32_lanes(a, kern) : 4, per = 64 / nl;
+        const float* qn = kern != 0 ? a.qn32 + (size_t)(p / a.R) * a.d_pad : nullptr;
+        for (int64_t r0 = b0 + (int64_t)w * per; kern != 0 && r0 < b1; r0 += (int64_t)(kFbT / 64) * per) {
+            const int64_t x = r0 + lane / nl;
+            const float v = a.rows32n ? blas32_dist_group<true>(a, p, qn, x, x < b1, kern, nl)
+                                       : blas32_dist_group<false>(a, p, qn, x, x < b1, kern, nl);
+            for (int j = 0; j < per; ++j) {
+                const float vj = __shfl(v, nl * j);
+                const int32_t rr = (int32_t)(r0 + j);
+                if (lane != 0 || r0 + j >= b1) continue;
+                const double xv = (double)vj;
+                if (!lt_dp(xv, rr, L[k - 1], G[k - 1])) continue;
+                int i = k - 1;
+                while (i > 0 && lt_dp(xv, rr, L[i - 1], G[i - 1])) {
+                    L[i] = L[i - 1];
+                    G[i] = G[i - 1];
+                    --i;
+                }
+                L[i] = xv;
+                G[i] = rr;
+            }
+        }
+        for (int64_t r0 = b0 + (int64_t)w * kB; kern == 0 && r0 < b1; r0 += (int64_t)(kFbT / 64) * kB) {
             int32_t r[kB];
 #pragma unroll
             for (int b = 0; b < kB; ++b) r[b] = r0 + b < b1 ? (int32_t)(r0 + b) : -1;
@@ -1415,18 +1524,30 @@ int launch_x3(const XArgs& a, int64_t P, hipStream_t s) {
     if (a.two_eps > 0.0) {
         const dim3 wg((unsigned)((P + kXT / 64 - 1) / (kXT / 64)));
         // (float32 rows: LMI_XSEL_KB rows in flight per wave; float64 rows: 4)
-        const int kb = sizeof(TC) == 4 ? env_config().xsel_kb : 4;
+        int kb = sizeof(TC) == 4 ? env_config().xsel_kb : 4;
+        if constexpr (!OUT64 && sizeof(TC) == 4) {
+            if (a.rows32n) {  // (the float32 order over the normalised rows)
+                if (kb == 1)
+                    hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 1, true>), wg, dim3(kXT), 0, s, a, (int32_t)P);
+                else if (kb == 2)
+                    hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 2, true>), wg, dim3(kXT), 0, s, a, (int32_t)P);
+                else
+                    hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 4, true>), wg, dim3(kXT), 0, s, a, (int32_t)P);
+                kb = -1;
+            }
+        }
         if constexpr (sizeof(TC) == 4) {
             if (kb == 1)
                 hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 1>), wg, dim3(kXT), 0, s, a, (int32_t)P);
             else if (kb == 2)
                 hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 2>), wg, dim3(kXT), 0, s, a, (int32_t)P);
         }
-        if (kb != 1 && kb != 2)
+        if (kb != 1 && kb != 2 && kb != -1)
             hipLaunchKernelGGL((x_select_wave_kernel<TC, TQ, OUT64, 4>), wg, dim3(kXT), 0, s, a, (int32_t)P);
         LMI_LAUNCH_CHECK("x_select_wave_kernel");
     }
-    hipLaunchKernelGGL((x_select_kernel<TC, TQ, OUT64>), dim3((unsigned)P), dim3(kXT), lds, s, a);
+    const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P, 4 * num_cus_ref()));
+    hipLaunchKernelGGL((x_select_kernel<TC, TQ, OUT64>), dim3(sg), dim3(kXT), lds, s, a);
     LMI_LAUNCH_CHECK("x_select_kernel");
     const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref()));
     hipLaunchKernelGGL((x_fallback_kernel<TC, TQ, OUT64>), dim3(fg), dim3(kFbT), 0, s, a);
@@ -1573,13 +1694,10 @@ int bucket_topk_f64_impl(const lmi_index_desc* idx, const float* q, int32_t nq, 
     if (nq == 0) return LMI_OK;
     LMI_CHECK_ARG(q && classes && out_d && out_pos && status && workspace, "null pointer");
     LMI_CHECK_ARG(q64 == nullptr || ldq64 >= idx->d, "ldq64 < d");
-    if (idx->corpus32) {
-        if (phases != kPhaseAll) {
-            set_error("phase flags are not supported in the split mode (corpus32)");
-            return LMI_E_UNSUPPORTED;
-        }
+    if (idx->corpus32) {  // (phases: k <= 10, ABI 11; not the global band's REFINE)
+        LMI_CHECK_ARG(!global, "the global band needs an index without corpus32");
         return bucket_topk_x(idx, q, nq, ldq, q64, ldq64, classes, R, k, out_d, 1, out_pos, status,
-                             workspace, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+                             workspace, ws_bytes, reinterpret_cast<hipStream_t>(stream), phases);
     }
     const RefineWs w = refine_ws(idx, nq, R, k, qmode);
     if (ws_bytes < w.total) {
@@ -1713,5 +1831,22 @@ extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_
     LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + at, 4,
                                hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
     LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return LMI_OK;
+}
+
+extern "C" int lmi_split_normalize(const float* rows, int64_t n, int32_t d, int32_t d_pad, float* out,
+                                   void* stream) {
+    using namespace lmi;
+    LMI_CHECK_ARG(n >= 0 && (n == 0 || (rows && out)), "null pointer");
+    LMI_CHECK_ARG(d > 0 && d <= 1024 && (d & 15) == 0 && d_pad >= d,
+                  "split normalise: d=%d d_pad=%d (d a multiple of 16, at most 1024)", d, d_pad);
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    constexpr int64_t kStep = int64_t(1) << 28;  // rows per launch (int32 row ids inside)
+    for (int64_t a = 0; a < n; a += kStep) {
+        const int32_t m = (int32_t)std::min<int64_t>(kStep, n - a);
+        hipLaunchKernelGGL(x_qn32_kernel, dim3((unsigned)((m + 3) / 4)), dim3(256), 0, s, rows + (size_t)a * d_pad,
+                           d_pad, m, d, d_pad, out + (size_t)a * d_pad);
+        LMI_LAUNCH_CHECK("x_qn32_kernel");
+    }
     return LMI_OK;
 }

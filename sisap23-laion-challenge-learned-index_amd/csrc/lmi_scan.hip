@@ -1324,14 +1324,9 @@ extern "C" int lmi_bucket_topk(const lmi_index_desc* idx, const float* q, int32_
     const bool seed = (qmode & LMI_Q_SEED_ROUND0) != 0;
     qmode &= ~LMI_Q_SEED_ROUND0;
     const int phases = take_phases(qmode);
-    if (idx && idx->corpus32) {
-        if (phases != kPhaseAll) {
-            set_error("phase flags are not supported in the split mode (corpus32)");
-            return LMI_E_UNSUPPORTED;
-        }
+    if (idx && idx->corpus32)  // (phases: k <= 10, ABI 11)
         return bucket_topk_x(idx, q, nq, ldq, nullptr, 0, classes, R, k, out_d, 0, out_pos, status, workspace,
-                             ws_bytes, s);
-    }
+                             ws_bytes, s, phases);
     if (k <= LMI_MAX_K)
         return bucket_topk_impl(idx, q, nq, ldq, classes, R, k, qmode, out_d, out_pos, nullptr,
                                 status, workspace, ws_bytes, s, nullptr, 0, true, seed, 0.0f, phases);
@@ -1673,7 +1668,7 @@ double split_eps(int d_pad) {
 namespace {
 struct XWs {
     size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
-        classes2, qn32, grp, tailq, goff, region, region_bytes, total;
+        classes2, qn32, grp, tailq, goff, region, region_bytes, region_s, region_s_bytes, total;
     int32_t cap;
 };
 // k <= 10: the k-th of a per-bucket sample (the product scan over
@@ -1737,6 +1732,13 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.region_bytes = std::max({ws_layout(idx, nq, R, k, LMI_Q_F16).total, ws_layout(idx, nq, R, 10, LMI_Q_F16).total,
                                ws_layout(&bd, nq, R, 15, LMI_Q_F16).total, ws_layout(&sd, nq, R, k, LMI_Q_F16).total});
     w.region = take(w.region_bytes);
+    // k <= 10: the sample scan's own region (ABI 11), so the plans of both
+    // scans are laid down in one PLAN phase and the batch stream can run the
+    // phases of one batch apart
+    if (x_sample(k)) {
+        w.region_s_bytes = ws_layout(&sd, nq, R, k, LMI_Q_F16).total;
+        w.region_s = take(w.region_s_bytes);
+    }
     w.total = off;
     return w;
 }
@@ -1750,7 +1752,8 @@ size_t x_nfailed_offset(const lmi_index_desc* idx, int nq, int R, int k) { retur
 // rounded here whatever their class).
 int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq, const double* q64,
                   int32_t ldq64, const int32_t* classes, int32_t R, int32_t k, void* out_d, int out_f64,
-                  int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes, hipStream_t s) {
+                  int32_t* out_pos, int32_t* status, void* workspace, size_t ws_bytes, hipStream_t s,
+                  int phases) {
     LMI_CHECK_ARG(idx != nullptr, "null index");
     LMI_CHECK_ARG(idx->corpus32 != nullptr && idx->dtype == LMI_F16 && idx->d_pad == v2::D,
                   "split mode needs corpus32, an fp16 scan corpus and d_pad %d", v2::D);
@@ -1759,6 +1762,10 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     if (nq == 0) return LMI_OK;
     LMI_CHECK_ARG((q || q64) && classes && out_d && out_pos && status && workspace, "null pointer");
     LMI_CHECK_ARG(q64 ? ldq64 >= idx->d : ldq >= idx->d, "ldq < d");
+    if (phases != kPhaseAll && !x_sample(k)) {
+        set_error("split mode: phase flags need k <= 10 (the sample's bound)");
+        return LMI_E_UNSUPPORTED;
+    }
     const XWs w = x_ws(idx, nq, R, k);
     if (ws_bytes < w.total) {
         set_error("workspace %zu B < required %zu B", ws_bytes, w.total);
@@ -1773,32 +1780,58 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     auto* ccount = (uint32_t*)(ws + w.ccount);
     auto* cand = (uint64_t*)(ws + w.cand);
     unsigned char* region = ws + w.region;
-    hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)), dim3(kThreads),
-                       0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
-    LMI_LAUNCH_CHECK("x_round_queries_kernel");
-    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
     const double two_eps = 2.0 * split_eps(idx->d_pad);
     const bool sampled = x_sampled(k);
     int32_t* fix = (int32_t*)(ws + w.fix);
     int rc;
+    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
     if (x_sample(k)) {
-        // 1. the k-th of every pair's bucket sample (its first chunk_rows
-        //    rows): the product scan over the 2C-bucket sample descriptor,
-        //    then that k-th + 2 eps as the collect bound
+        // (PLAN: the rounded queries and both scans' plans; SCAN: the sample
+        // scan and its merge, the bound, the collect scan; MERGE: step 3)
         auto* off2 = (int64_t*)(ws + w.off2);
         auto* cf2 = (int32_t*)(ws + w.cf2);
         auto* classes2 = (int32_t*)(ws + w.classes2);
-        hipLaunchKernelGGL(x_sample_desc_kernel, dim3((unsigned)std::min(1024, (P + 63) / 64)), dim3(64), 0, s,
-                           idx->bucket_off, idx->n_buckets, (int64_t)idx->chunk_rows, classes, P, off2, cf2, classes2);
-        LMI_LAUNCH_CHECK("x_sample_desc_kernel");
         const lmi_index_desc sd = x_sample_desc(idx, off2, cf2);
-        rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, nullptr, status, region,
-                              w.region_bytes, s);
-        if (rc != LMI_OK) return rc;
-        hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld, two_eps,
-                           bound);
-        LMI_LAUNCH_CHECK("x_bound_kernel");
-    } else if (sampled) {
+        unsigned char* region_s = ws + w.region_s;
+        if (phases & kPhasePlan) {
+            hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)),
+                               dim3(kThreads), 0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
+            LMI_LAUNCH_CHECK("x_round_queries_kernel");
+            LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
+            hipLaunchKernelGGL(x_sample_desc_kernel, dim3((unsigned)std::min(1024, (P + 63) / 64)), dim3(64), 0, s,
+                               idx->bucket_off, idx->n_buckets, (int64_t)idx->chunk_rows, classes, P, off2, cf2,
+                               classes2);
+            LMI_LAUNCH_CHECK("x_sample_desc_kernel");
+            rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
+                                  region_s, w.region_s_bytes, s, nullptr, 0, true, false, 0.0f, kPhasePlan);
+            if (rc != LMI_OK) return rc;
+            rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status,
+                                  region, w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhasePlan, &m2);
+            if (rc != LMI_OK) return rc;
+        }
+        if (phases & kPhaseScan) {
+            // 1. the k-th of every pair's bucket sample (its first chunk_rows
+            //    rows): the product scan over the 2C-bucket sample descriptor,
+            //    then that k-th + 2 eps as the collect bound
+            rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
+                                  region_s, w.region_s_bytes, s, nullptr, 0, true, false, 0.0f,
+                                  kPhaseScan | kPhaseMerge);
+            if (rc != LMI_OK) return rc;
+            hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld, two_eps,
+                               bound);
+            LMI_LAUNCH_CHECK("x_bound_kernel");
+            // 2. every row under the bound (the collect scan, as the wide path's)
+            rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status,
+                                  region, w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhaseScan, &m2);
+            if (rc != LMI_OK) return rc;
+        }
+        if (!(phases & kPhaseMerge)) return LMI_OK;
+    } else {
+    hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)), dim3(kThreads),
+                       0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
+    LMI_LAUNCH_CHECK("x_round_queries_kernel");
+    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
+    if (sampled) {
         // 1. a bound per pair from a sample: the wide path's chunk-list scan
         //    (two lists per bucket, each scanning the first quarter of its
         //    rows, every list its part's own top-15), the 15th smallest entry
@@ -1837,14 +1870,15 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
         LMI_LAUNCH_CHECK("x_bound_kernel");
     }
     // 2. every row under the bound (the collect scan, as the wide path's)
-    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
     rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status, region,
                           w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhasePlan | kPhaseScan, &m2);
     if (rc != LMI_OK) return rc;
+    }
     // 3. the candidates' exact distances, sorted; overflowed pairs whole
     const WsLayout l = ws_layout(idx, nq, R, 10, LMI_Q_F16);
     XArgs a{};
     a.rows32 = idx->corpus32;
+    a.rows32n = idx->corpus32n;
     a.rows64 = out_f64 ? idx->corpus64 : nullptr;
     a.d = idx->d;
     a.d_pad = idx->d_pad;

@@ -64,6 +64,7 @@ EXPORTS = (
     "lmi_bucket_topk_f64g",
     "lmi_refine_fallback_count",
     "lmi_split_eps",
+    "lmi_split_normalize",
     "lmi_replay_device_phase",
     "lmi_merge_topk_f64",
     "lmi_packed_rank_words",
@@ -106,7 +107,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 
 class IndexDesc(C.Structure):
@@ -128,6 +129,7 @@ class IndexDesc(C.Structure):
         ("corpus64", C.c_void_p),        # ABI 6
         ("corpus32", C.c_void_p),        # ABI 9
         ("bucket_rows", C.c_void_p),     # ABI 10
+        ("corpus32n", C.c_void_p),       # ABI 11
     ]
 
 
@@ -152,6 +154,7 @@ _SIGNATURES = {
                                        _I32, _I32, C.c_double, _P, _P, _I32, _I64, _P, _P, _P, _P,
                                        C.c_size_t, _P]),
     "lmi_split_eps": (C.c_double, [_I32]),
+    "lmi_split_normalize": (C.c_int, [_P, _I64, _I32, _I32, _P, _P]),
     "lmi_replay_device_phase": (C.c_int, [_I32, _I32, _P, _I32, _I32, _I32, _P, _P, _I32, _I32, _P, _I32,
                                           _P, _I64, _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,

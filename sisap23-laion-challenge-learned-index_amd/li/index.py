@@ -213,6 +213,7 @@ class DeviceIndex:
 
     corpus64 = None  # float64 rows (float64 input that float32 rounding changes)
     corpus32 = None  # float32 rows of the split mode (storage "f32x")
+    corpus32n = None  # corpus32 normalised as sklearn does in float32 (ABI 11)
     inv_norm32 = None  # 1/||y|| of corpus32 (the general scan's, k > 16 in f32x)
 
     def __init__(self, data, labels, n_buckets: int, *, ids=None, device=None,
@@ -332,6 +333,15 @@ class DeviceIndex:
             self.corpus[a:a + step, : self.d] = blk.to(tdt)
             self.inv_norm[a:a + step] = _inv_norm(blk.to(tdt))
             del blk, f
+        if storage == "f32x" and self.d % 16 == 0 and os.environ.get("LMI_SPLIT_NORM32", "1") != "0":
+            # every row divided by its float32 norm as the reference's
+            # normalize(Y) computes it, once (lmi_index_desc.corpus32n): the
+            # float32 re-score then runs only the product's chains per row
+            # (LMI_SPLIT_NORM32=0: normalised per candidate; the same values)
+            self.corpus32n = torch.empty_like(self.corpus32)
+            check("lmi_split_normalize", _lib.load().lmi_split_normalize(
+                ptr(self.corpus32), n_rows, self.d, self.d_pad, ptr(self.corpus32n),
+                _lib.stream_handle(self.device)))
 
     @torch.no_grad()
     def _fill_from_source(self, src: "RowSource", gpos):
@@ -406,7 +416,7 @@ class DeviceIndex:
                 self.gpos[a:b] = self.gpos[a:b][order]
                 # the row arrays that share corpus's local row index (the
                 # split mode's float32 rows, the float64 rows) move with it
-                for name in ("corpus32", "inv_norm32", "corpus64"):
+                for name in ("corpus32", "corpus32n", "inv_norm32", "corpus64"):
                     t = getattr(self, name)
                     if t is not None:
                         t[a:b] = t[a:b][order]
@@ -461,6 +471,7 @@ class IndexDescHolder:
         d.corpus64 = ptr(ix.corpus64) if ix.corpus64 is not None else None
         d.corpus32 = ptr(ix.corpus32) if (ix.corpus32 is not None and not general32) else None
         d.bucket_rows = ptr(ix.bucket_rows)
+        d.corpus32n = ptr(ix.corpus32n) if (ix.corpus32n is not None and not general32) else None
         self.desc = d
 
 

@@ -124,8 +124,11 @@ class StreamedSearch:
     captured).  `lookahead` (default True): the next launch's scan is enqueued
     at the end of each launch, waiting on the device for its plan (one launch
     earlier) and for this launch's F; False enqueues each scan at the start of
-    its own launch.  fp16 index and fp16-exact query batches only (the phased
-    scan is the fp16 scan); other batches go through Searcher.search."""
+    its own launch.  fp16 index and fp16-exact query batches (the phased scan
+    is the fp16 scan; other batches go through Searcher.search), or the split
+    mode (storage f32x, k_round <= 10, float32 batches: its SCAN phase is the
+    sample scan, the bound and the collect scan, its MERGE phase the exact
+    re-score; ABI 11)."""
 
     NS = 4
 
@@ -156,8 +159,13 @@ class StreamedSearch:
         nq, d, dn = int(qs.shape[0]), ix.d, int(nav.shape[1])
         if qs.shape != (nq, d) or nav.shape[0] != nq:
             raise ValueError("query shapes do not match the index")
-        if not (ix.storage == "f16" and d % 2 == 0):
-            raise ValueError("the batch stream needs an fp16 index with an even d")
+        # (the split mode, storage f32x: float32 batches, its phases need
+        # k_round <= 10, ABI 11)
+        self.split = split = ix.storage == "f32x"
+        if split and k_round > 10:
+            raise ValueError("the split mode's batch stream needs k_round <= 10")
+        if not (split or (ix.storage == "f16" and d % 2 == 0)):
+            raise ValueError("the batch stream needs an fp16 index with an even d, or the split mode")
         self.nq, self.d, self.dn = nq, d, dn
         f64 = dist == "f64"
         self.w = k_round if R == 1 else k
@@ -165,7 +173,7 @@ class StreamedSearch:
         NS, X = self.NS, self.X
         self.per = per = -(-nq // G)                 # rows of a rank's block
         self.lo, self.hi = min(nq, g * per), min(nq, (g + 1) * per)
-        wq = d // 2                                  # int32 words per fp16 row
+        wq = d if split else d // 2                  # int32 words per fp16 (split: float32) row
         # a rank's block, int32 words: [pca96 f32 per*dn | clip768 f16 per*wq |
         # not-fp16 flag, pad | classes per*R (G > 1)]; stage() writes and the
         # H2D moves everything before the classes
@@ -262,16 +270,17 @@ class StreamedSearch:
 
         def plan(j):
             st = self.lists[j][2]
+            qdt = torch.float32 if split else torch.float16
             if not X:
                 blk = self.d_blk[j]
-                self.q32[j].copy_(blk[self.o_q:self.o_flag].view(torch.float16).view(nq, d))
+                self.q32[j].copy_(blk[self.o_q:self.o_flag].view(qdt).view(nq, d))
                 # the scan's status word starts with the staged block's
                 # not-fp16 flag (the scan only ORs bits into it)
                 st.copy_(blk[self.o_flag:self.o_flag + 1])
             else:
                 xa = self.xall[(j + 1) % NS].view(G, self.W)[:, self.wl:self.wl + self.bw]
                 self.q32[j].view(G, per, d).copy_(
-                    xa[:, self.o_q:self.o_flag].view(torch.float16).view(G, per, d))
+                    xa[:, self.o_q:self.o_flag].view(qdt).view(G, per, d))
                 self.cls[j].view(G, per, R).copy_(xa[:, self.o_cls:].view(G, per, R))
                 torch.amax(xa[:, self.o_flag:self.o_flag + 1], dim=0, out=st)
             phase(j, _lib.LMI_Q_PHASE_PLAN)
@@ -446,6 +455,11 @@ class StreamedSearch:
         lo, hi = self.lo, self.hi
         blk = self.h_stage[slot].numpy()
         stage_rows_f32(blk[:(hi - lo) * dn].view(np.float32).reshape(hi - lo, dn), nav[lo:hi])
+        if self.split:  # (float32 rows as given: the split mode rounds them itself)
+            stage_rows_f32(blk[self.o_q:self.o_q + (hi - lo) * d].view(np.float32).reshape(hi - lo, d),
+                           qs[lo:hi])
+            blk[self.o_flag] = 0
+            return True
         ok = stage_rows_f16(blk[self.o_q:self.o_q + (hi - lo) * (d // 2)].view(np.float16)
                             .reshape(hi - lo, d), qs[lo:hi])
         blk[self.o_flag] = 0 if ok else _lib.LMI_STATUS_QUERY_NOT_F16

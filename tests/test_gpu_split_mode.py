@@ -106,6 +106,10 @@ def test_split_overflow_takes_the_whole_shard():
     d, p, st = bucket_topk(ix, T(q), cls, 10)
     ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, 1, 10, C)
     assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-5, tie=1e-6) == 0
+    # (ABI 11: the whole-shard path computes float32 in the reference's order:
+    # one group of 64 queries x the bucket, OpenBLAS's blocked kernel)
+    assert O.blas32_kernel(q.shape[0], int(np.sum(w["labels"] == big)), x.shape[1]) == "blocked"
+    np.testing.assert_array_equal(d.cpu().numpy(), ref_d)
     d64, p64, st64, nfb = bucket_topk_f64(ix, T(q.astype(np.float64)), cls, 10, fallback_count=True)
     assert nfb > 0  # the whole-shard path ran
     ref_d64, ref_p64 = O.bucket_lists(w["labels"], x, q.astype(np.float64), classes, 1, 10, C)
@@ -225,17 +229,22 @@ def test_split_subcluster_layout_moves_the_float32_rows(k):
 
 
 
+@pytest.mark.parametrize("norm32", ["1", "0"])
 @pytest.mark.parametrize("mode,seed", [("near", 661), ("skewed", 662), ("router", 663)])
-def test_split_float32_is_the_references_own_arithmetic(mode, seed):
+def test_split_float32_is_the_references_own_arithmetic(mode, seed, norm32, monkeypatch):
     """ABI 10: the split mode's float32 re-score follows the reference's
     float32 operation order (oracle blas32_*: sklearn's einsum norms and
     division, OpenBLAS sgemm's summation order for the (round, bucket)
     group's shape), so wherever that shape's order is restated the lists'
     float32 distances equal the oracle's (= numpy's = the reference's) bit for
-    bit and ids differ only inside runs of identical distances."""
+    bit and ids differ only inside runs of identical distances.  Both with the
+    rows normalised once at build (ABI 11, corpus32n) and per candidate
+    (LMI_SPLIT_NORM32=0)."""
+    monkeypatch.setenv("LMI_SPLIT_NORM32", norm32)
     w, x, q = _x(mode, seed, n=6000, nq=200)
     C, R, k = w["C"], 4, 10
     ix = DeviceIndex(x, w["labels"], C, chunk_rows=512, device="cuda")
+    assert (ix.corpus32n is not None) == (norm32 == "1")
     classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R]
     d, p, st = bucket_topk(ix, T(q), T(classes.astype(np.int32)), k)
     assert int(st.item()) == 0
@@ -256,3 +265,26 @@ def test_split_float32_is_the_references_own_arithmetic(mode, seed):
     rd, rp = ref_d[keep], ref_p[keep]
     np.testing.assert_array_equal(gd, rd)     # float32 distances: bit for bit
     assert O.compare_lists(rd, rp, gd, gp, atol=0.0, tie=0.0) == 0
+
+
+def test_split_normalize_is_sklearns_float32_normalize():
+    """ABI 11: lmi_split_normalize (corpus32n) = sklearn's normalize(Y) in
+    float32 (oracle blas32_normalize: numpy einsum norms, the zero rule, IEEE
+    division), bit for bit, padding zeroed; zero rows stay zero."""
+    w, x, q = _x("dup", 671, n=3000)
+    x = x.copy()
+    x[5] = 0.0
+    ix = DeviceIndex(x, w["labels"], w["C"], chunk_rows=512, device="cuda")
+    assert ix.corpus32n is not None and ix.corpus32n.shape == ix.corpus32.shape
+    rows = ix.layout.order[ix.gpos.cpu().numpy().astype(np.int64)]
+    got = ix.corpus32n.cpu().numpy()
+    np.testing.assert_array_equal(got[:, : x.shape[1]], O.blas32_normalize(x[rows]))
+    assert not got[:, x.shape[1]:].any()
+    # through the C-ABI directly, rows not a multiple of 4 (a partial workgroup)
+    lib = _lib.load()
+    src = T(np.ascontiguousarray(x[:7]))
+    out = torch.full_like(src, 7.0)
+    assert lib.lmi_split_normalize(src.data_ptr(), 7, x.shape[1], x.shape[1], out.data_ptr(),
+                                   _lib.stream_handle(src.device)) == 0
+    np.testing.assert_array_equal(out.cpu().numpy(), O.blas32_normalize(x[:7]))
+    assert lib.lmi_split_normalize(src.data_ptr(), 7, 100, 128, out.data_ptr(), None) != 0
