@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 11
+#define LMI_ABI_VERSION 12
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -496,6 +496,14 @@ int32_t lmi_abi_version(void);
  * lmi_scan_f64_workspace_bytes) -- a workspace sized under the old knobs may
  * be refused with LMI_E_WORKSPACE, never overrun. */
 int lmi_config_reload(void);
+/* The persistent scan's grid (ABI 12): the number of workgroups (one per CU)
+ * the scan kernels of lmi_bucket_topk[_f64*] launch from this thread, so a
+ * caller can leave CUs to work that runs beside the scan on other streams
+ * (li.stream.StreamedSearch: the finish chain of the previous batch).  0: one
+ * per CU (or LMI_SCAN_WGS).  Thread-local, read at launch (a captured graph
+ * keeps the grid it was captured with); results never depend on it.  Returns
+ * the previous setting. */
+int32_t lmi_scan_set_workgroups(int32_t wgs);
 
 #ifdef __cplusplus
 }

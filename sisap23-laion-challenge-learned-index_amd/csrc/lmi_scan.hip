@@ -1213,6 +1213,10 @@ int split_parts() {
     return std::max(2, std::min(kSplitMaxParts, env_config().scan_split_parts));
 }
 
+namespace {
+thread_local int t_scan_wgs = 0;  // lmi_scan_set_workgroups (0: env / every CU)
+}  // namespace
+
 int num_cus() {
     static int n = 0;
     static std::once_flag once;
@@ -1222,7 +1226,7 @@ int num_cus() {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) n = 256;
     });
     const int cus = n > 0 ? n : 256;
-    const int w = env_config().scan_wgs;
+    const int w = t_scan_wgs > 0 ? t_scan_wgs : env_config().scan_wgs;
     return w > 0 ? std::min(w, cus) : cus;
 }
 
@@ -2193,6 +2197,12 @@ int bucket_topk_wide(const lmi_index_desc* idx, const float* q, int32_t nq, int3
 }
 }  // namespace lmi
 
+
+extern "C" int32_t lmi_scan_set_workgroups(int32_t wgs) {
+    const int prev = lmi::t_scan_wgs;
+    lmi::t_scan_wgs = wgs > 0 ? wgs : 0;
+    return prev;
+}
 
 extern "C" double lmi_split_eps(int32_t d_pad) { return d_pad > 0 ? lmi::split_eps(d_pad) : 0.0; }
 

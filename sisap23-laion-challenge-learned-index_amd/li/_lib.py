@@ -82,6 +82,7 @@ EXPORTS = (
     "lmi_last_error",
     "lmi_abi_version",
     "lmi_config_reload",
+    "lmi_scan_set_workgroups",
     "lmi_host_hash64",
     "lmi_host_stage_f16",
     "lmi_host_copy",
@@ -107,7 +108,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 
 class IndexDesc(C.Structure):
@@ -179,6 +180,7 @@ _SIGNATURES = {
     "lmi_last_error": (C.c_char_p, []),
     "lmi_abi_version": (C.c_int32, []),
     "lmi_config_reload": (C.c_int, []),
+    "lmi_scan_set_workgroups": (C.c_int32, [_I32]),
     "lmi_host_hash64": (C.c_uint64, [_P, C.c_uint64, _I32]),
     "lmi_host_stage_f16": (C.c_int32, [_P, C.c_uint64, _P, _I32]),
     "lmi_host_copy": (C.c_int, [_P, _P, C.c_uint64, _I32]),

@@ -111,6 +111,18 @@ def queue_streams(dev, n: int):
     return have
 
 
+def stream_reserve(dev, exchange: bool, dist: str, split: bool) -> int:
+    """The default `reserve_cus` of a StreamedSearch: LMI_STREAM_RESERVE if set,
+    else 0.  Measured (10M, W = 1, profiles/r06p_reserve_ab.txt): leaving 2,
+    4 or 8 CUs to the finish made the float32 step 7.41-7.47 ms against
+    7.20-7.25 with none -- the route, the plan and the finish of a launch then
+    share those few CUs and outlast the ~7 ms scan -- and at W = 8 (a ~1 ms
+    stripe scan) 1.34-1.51 against 1.26 ms (profiles/r06o_*); float64 and
+    the split mode's finish are heavier still."""
+    env = os.environ.get("LMI_STREAM_RESERVE")
+    return int(env) if env is not None else 0
+
+
 class QueryNotF16(RuntimeError):
     """A streamed batch held clip768 values that fp16 cannot represent: the
     phased scan (fp16 MFMA) cannot answer it; Searcher.search can (exact fp32
@@ -123,8 +135,11 @@ class StreamedSearch:
     functions eagerly (the gloo rehearsal of the G > 1 path: gloo cannot be
     captured).  `lookahead` (default True): the next launch's scan is enqueued
     at the end of each launch, waiting on the device for its plan (one launch
-    earlier) and for this launch's F; False enqueues each scan at the start of
-    its own launch.  fp16 index and fp16-exact query batches (the phased scan
+    earlier) and, unless `reserve_cus` > 0, for this launch's F; False
+    enqueues each scan at the start of its own launch.  `reserve_cus` (None:
+    stream_reserve's default): CUs the scan's persistent grid leaves to the
+    finish chain, which then runs beside the next scan.  fp16 index and
+    fp16-exact query batches (the phased scan
     is the fp16 scan; other batches go through Searcher.search), or the split
     mode (storage f32x, k_round <= 10, float32 batches: its SCAN phase is the
     sample scan, the bound and the collect scan, its MERGE phase the exact
@@ -134,7 +149,8 @@ class StreamedSearch:
 
     def __init__(self, searcher, q_nav, q_search, R: int, k: int = 10, *,
                  k_round: int = 10, use_threshold: bool = True, dist: str = "f32",
-                 capture: bool = True, lookahead: bool = True, kth_peers=None):
+                 capture: bool = True, lookahead: bool = True, kth_peers=None,
+                 reserve_cus: Optional[int] = None):
         s = searcher
         ix = s.index
         dev = ix.device
@@ -290,7 +306,14 @@ class StreamedSearch:
                           phases=_lib.LMI_REPLAY_PHASE_GROUPS, ws=self.rws[j], k_list=kl)
 
         def scan(j):
-            phase(j, _lib.LMI_Q_PHASE_SCAN)
+            if not self.scan_wgs:
+                phase(j, _lib.LMI_Q_PHASE_SCAN)
+                return
+            prev = lib.lmi_scan_set_workgroups(self.scan_wgs)
+            try:
+                phase(j, _lib.LMI_Q_PHASE_SCAN)
+            finally:
+                lib.lmi_scan_set_workgroups(prev)
 
         def finish1(j):
             if gband:
@@ -351,6 +374,17 @@ class StreamedSearch:
         self.time_scans = False
         self._scan_ev = []
         self.lookahead = lookahead
+        # reserve_cus > 0: the scan's persistent grid leaves that many CUs to
+        # the finish chain (lmi_scan_set_workgroups, ABI 12), and the
+        # lookahead scan does not wait for this launch's finish (its slot is
+        # not the finish's), so the finish runs beside the next scan instead
+        # of between two scans (DESIGN.md §5 "The finish beside the scan")
+        self.reserve_cus = r = stream_reserve(dev, X, dist, split) if reserve_cus is None else int(reserve_cus)
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        if not 0 <= r < ncu:
+            raise ValueError(f"reserve_cus={r} outside [0, {ncu})")
+        self.scan_wgs = ncu - r if r > 0 else 0
+        self.overlap = r > 0
         self._s_ahead = False  # the next launch's scan is already enqueued
         for j in range(NS):
             if not self.stage(nav, qs, slot=j):
@@ -590,7 +624,8 @@ class StreamedSearch:
         if self.lookahead:
             jn = (t + 3) % NS
             main.wait_event(self._pdone[jn])
-            main.wait_event(self._fdone[jf])
+            if not self.overlap:
+                main.wait_event(self._fdone[jf])
             self._run_scan(jn, main)
         self._s_ahead = bool(self.lookahead)
         self._t += 1

@@ -120,6 +120,29 @@ def test_stream_with_and_without_lookahead(setup, lookahead):
         np.testing.assert_array_equal(a, a0)
 
 
+@pytest.mark.parametrize("dist,reserve", [("f32", 0), ("f32", 8), ("f32", 255), ("f64", 16)])
+def test_stream_with_cus_left_to_the_finish(setup, dist, reserve):
+    """reserve_cus (ABI 12 lmi_scan_set_workgroups): the scan's grid leaves
+    CUs to the finish chain and the lookahead scan stops waiting for it --
+    the same answers, batch by batch; the setting is the stream's own (the
+    thread's grid is back to every CU after each scan)."""
+    w, s = setup
+    lib = _lib.load()
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    reserve = min(reserve, ncu - 1)
+    bs = _batches(w, 6, seed=70 + reserve)
+    ref = [s.search(T(a), T(b), 4, k=10, dist=dist) for a, b in bs]
+    st = s.streamed(w["qn"], w["q"], 4, k=10, dist=dist, reserve_cus=reserve)
+    assert st.overlap == (reserve > 0) and st.scan_wgs == (ncu - reserve if reserve else 0)
+    got = list(st.stream(bs))
+    for (d, a), (d0, a0) in zip(got, ref):
+        np.testing.assert_array_equal(d, d0)
+        np.testing.assert_array_equal(a, a0)
+    assert lib.lmi_scan_set_workgroups(0) == 0
+    with pytest.raises(ValueError):
+        s.streamed(w["qn"], w["q"], 4, k=10, reserve_cus=ncu)
+
+
 @pytest.mark.parametrize("where", [0, 2, 5])
 def test_inexact_batch_in_a_stream_is_answered_eagerly(setup, where):
     """A batch whose clip768 values fp16 cannot hold, in the middle of a stream

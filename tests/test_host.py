@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 11
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 12
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
@@ -291,3 +291,18 @@ def test_default_chunk_rows_by_world_and_size():
     assert default_chunk_rows(1, 300_000) == 4096
     assert default_chunk_rows(1, 100_000) == 1024
     assert default_chunk_rows(4, 1_000) == 1024
+
+
+def test_scan_workgroups_setting_is_per_thread():
+    """lmi_scan_set_workgroups (ABI 12) returns the previous setting, clamps
+    negatives to 0 (every CU) and is the calling thread's own."""
+    import threading
+    lib = _lib.load()
+    assert lib.lmi_scan_set_workgroups(200) == 0
+    seen = []
+    t = threading.Thread(target=lambda: seen.append(lib.lmi_scan_set_workgroups(5)))
+    t.start()
+    t.join()
+    assert seen == [0]
+    assert lib.lmi_scan_set_workgroups(-3) == 200
+    assert lib.lmi_scan_set_workgroups(0) == 0
