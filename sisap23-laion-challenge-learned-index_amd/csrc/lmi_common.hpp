@@ -143,7 +143,9 @@ inline int take_phases(int32_t& qmode) {
 // mode's band lists -- the scan's filter widened by seed_margin (2 eps), every
 // pair's first 15 entries, and out_bound[pair] a distance such that each row
 // of the shard the list does not hold failed the widened filter or has
-// d32 >= it (chunk_merge_band_kernel).
+// d32 >= it (chunk_merge_band_kernel); kth_out (nullable, with out_bound):
+// each pair's first kth_k list distances also written to kth_out[pair * kth_k]
+// (the float64 global band's kth_send, ABI 10).
 // The scans of the wide path (k > 16, bucket_topk_wide): mode 1 writes every
 // (pair, chunk part) list as that part's own top-15 (no global bound); mode 2
 // collects every row within the pair's bound bound_ord[pair id] (a distance
@@ -165,7 +167,8 @@ int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int3
                      size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g = nullptr,
                      int32_t ldo = 0, bool prefill = true, bool seed_r0 = false,
                      float seed_margin = 0.0f, int phases = kPhaseAll,
-                     const WideScan* wide = nullptr, float* out_bound = nullptr);
+                     const WideScan* wide = nullptr, float* out_bound = nullptr,
+                     float* kth_out = nullptr, int32_t kth_k = 0);
 // scan v3 serves this index and query class (the float64 mode's band lists)
 bool band_capable(const lmi_index_desc* idx, int qmode);
 size_t scan_workspace_bytes(const lmi_index_desc* idx, int32_t nq, int32_t R, int32_t k,

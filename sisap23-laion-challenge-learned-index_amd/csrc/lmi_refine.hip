@@ -72,31 +72,44 @@ struct RefineArgs {
     const float* kth_all;
     int32_t kth_G;
     int64_t kth_stride;
+    const float* kth_g;  // [nq*R] that k-th per pair (band_kth_kernel), read by refine_kernel
 };
 
-// the k-th smallest of G ascending lists of k values (lane g < G holds list g
-// in registers): k steps of a wave minimum, the winning lane (lowest on ties)
-// shifting its list; +inf when the lists hold fewer than k finite values
-__device__ inline float global_kth(const float* kth_all, int G, int64_t stride, int64_t p, int k) {
+// The k-th smallest of the G ascending lists of k values of every pair (the
+// multiset union: equal values on different lists each count; +inf when the
+// lists hold fewer than k finite values), before the refine: segments of W =
+// the power of two >= G lanes, 64 / W pairs a wave, lane g of a segment
+// holding list g in registers; k steps of a segment minimum, the winning lane
+// (lowest on ties) shifting its list.  (In the refine itself, one wave per
+// pair ran these k steps once or twice -- the seeded rounds read pair (q, 0)'s
+// too -- beside the list and the query: a per-pair fixed cost of the refine
+// at G = 8, where most pairs have no band row on a stripe.)
+__global__ __launch_bounds__(256) void band_kth_kernel(const float* __restrict__ kth_all, int32_t G,
+                                                       int64_t stride, int64_t P, int32_t k, float* __restrict__ out) {
     const int lane = threadIdx.x & 63;
+    int W = 1;
+    while (W < G) W <<= 1;
+    const int per = 64 / W, seg = lane / W, g = lane - seg * W;
+    const int64_t p = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * per + seg;
+    const bool live = p < P && g < G;
     float v[LMI_MAX_K];
-    const float* L = kth_all + (size_t)(lane < G ? lane : 0) * stride + (size_t)p * k;
+    const float* L = kth_all + (size_t)(live ? g : 0) * stride + (size_t)(live ? p : 0) * k;
 #pragma unroll
-    for (int i = 0; i < LMI_MAX_K; ++i) v[i] = (lane < G && i < k) ? L[i] : __builtin_inff();
+    for (int i = 0; i < LMI_MAX_K; ++i) v[i] = (live && i < k) ? L[i] : __builtin_inff();
+    const uint64_t segmask = (W == 64 ? ~0ull : ((1ull << W) - 1ull)) << (seg * W);
     float m = __builtin_inff();
     for (int step = 0; step < k; ++step) {
         float mn = v[0];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
+        for (int off = W >> 1; off > 0; off >>= 1) mn = fminf(mn, __shfl_xor(mn, off));
         m = mn;
-        const uint64_t b = __ballot(v[0] == mn);
-        if (lane == (int)__builtin_ctzll(b)) {
+        const uint64_t b = __ballot(v[0] == mn) & segmask;
+        if (b != 0ull && lane == (int)__builtin_ctzll(b)) {
 #pragma unroll
             for (int i = 0; i + 1 < LMI_MAX_K; ++i) v[i] = v[i + 1];
             v[LMI_MAX_K - 1] = __builtin_inff();
         }
     }
-    return m;
+    if (p < P && g == 0) out[p] = m;
 }
 
 __device__ inline double wave_sum_d(double v) {
@@ -295,8 +308,8 @@ void refine_kernel(RefineArgs a) {
     // pair's band; computed before the query's registers are live
     float tg = 0.0f, tg0 = 0.0f;
     if (a.lbound && a.kth_all) {
-        tg = global_kth(a.kth_all, a.kth_G, a.kth_stride, p, k);
-        if (a.seeded && p % a.R != 0) tg0 = global_kth(a.kth_all, a.kth_G, a.kth_stride, p - p % a.R, k);
+        tg = a.kth_g[p];
+        if (a.seeded && p % a.R != 0) tg0 = a.kth_g[p - p % a.R];
     }
     const int nps = (a.d + 255) / 256;
     double* od = a.out_d + (size_t)p * k;
@@ -427,6 +440,49 @@ constexpr int kFbSliceK = 16;
 constexpr int kFbSlices = 32;
 constexpr int kFbSlicedPairs = 512;
 constexpr int kFbSliceT = 256;
+// one wave on sliced failed pair f: its kFbSlices slice lists (k each, by
+// (d64, position)) merged to the first k (wave 0 of fallback_kernel's
+// workgroups, after fallback_slice_kernel: one launch fewer on the path)
+__device__ void fallback_merge_pair(const RefineArgs& a, int f) {
+    const int k = a.k;
+    const int lane = threadIdx.x & 63;
+    {
+        const int64_t p = a.failed[f];
+        const double* pd = a.pd + (size_t)f * kFbSlices * kFbSliceK;
+        const int32_t* pg = a.pg + (size_t)f * kFbSlices * kFbSliceK;
+        // lane s < kFbSlices walks slice s; each round the wave's minimum head
+        // is taken (position breaks distance ties, like every merge here)
+        int h = 0;
+        double* od = a.out_d + (size_t)p * k;
+        int32_t* op = a.out_pos + (size_t)p * k;
+        for (int j = 0; j < k; ++j) {
+            const bool has = lane < kFbSlices && h < k;
+            const double x = has ? pd[lane * kFbSliceK + h] : __builtin_inf();
+            const int32_t g = has ? pg[lane * kFbSliceK + h] : INT32_MAX;
+            double bx = x;
+            int32_t bg = g;
+            int bl = lane;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const double ox = __shfl_xor(bx, off);
+                const int32_t og = __shfl_xor(bg, off);
+                const int ol = __shfl_xor(bl, off);
+                if (lt_dp(ox, og, bx, bg) || (ox == bx && og == bg && ol < bl)) {
+                    bx = ox;
+                    bg = og;
+                    bl = ol;
+                }
+            }
+            if (lane == bl) ++h;
+            if (lane == 0) {
+                const bool empty = bg == INT32_MAX;
+                od[j] = empty ? __builtin_inf() : bx;
+                op[j] = empty ? -1 : bg;
+            }
+        }
+    }
+}
+
 template <typename TC, typename TQ>
 __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
     __shared__ double sd[kFbT / 64][kFbK];
@@ -436,8 +492,10 @@ __global__ __launch_bounds__(kFbT) void fallback_kernel(RefineArgs a) {
     const int k = a.k;
     const int nps = (a.d + 255) / 256;
     // (the first kFbSlicedPairs failed pairs of k <= kFbSliceK take the
-    // sliced path: fallback_slice_kernel + fallback_merge_kernel)
+    // sliced path: fallback_slice_kernel, then their merge in wave 0 here)
     const int f0 = a.pd ? kFbSlicedPairs : 0;
+    if (a.pd && w == 0)
+        for (int f = blockIdx.x; f < min(nf, kFbSlicedPairs); f += gridDim.x) fallback_merge_pair(a, f);
     for (int f = f0 + blockIdx.x; f < nf; f += gridDim.x) {
         const int64_t p = a.failed[f];
         const int c = a.classes[p];  // classes is [nq][R]: pair p = q*R + r
@@ -583,51 +641,8 @@ __global__ __launch_bounds__(kFbSliceT) void fallback_slice_kernel(RefineArgs a)
     }
 }
 
-// one wave per sliced failed pair: its kFbSlices slice lists (k each, by
-// (d64, position)) merged to the first k
-__global__ __launch_bounds__(64) void fallback_merge_kernel(RefineArgs a) {
-    const int nf = min(*a.n_failed, kFbSlicedPairs);
-    const int k = a.k;
-    const int lane = threadIdx.x;
-    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
-        const int64_t p = a.failed[f];
-        const double* pd = a.pd + (size_t)f * kFbSlices * kFbSliceK;
-        const int32_t* pg = a.pg + (size_t)f * kFbSlices * kFbSliceK;
-        // lane s < kFbSlices walks slice s; each round the wave's minimum head
-        // is taken (position breaks distance ties, like every merge here)
-        int h = 0;
-        double* od = a.out_d + (size_t)p * k;
-        int32_t* op = a.out_pos + (size_t)p * k;
-        for (int j = 0; j < k; ++j) {
-            const bool has = lane < kFbSlices && h < k;
-            const double x = has ? pd[lane * kFbSliceK + h] : __builtin_inf();
-            const int32_t g = has ? pg[lane * kFbSliceK + h] : INT32_MAX;
-            double bx = x;
-            int32_t bg = g;
-            int bl = lane;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const double ox = __shfl_xor(bx, off);
-                const int32_t og = __shfl_xor(bg, off);
-                const int ol = __shfl_xor(bl, off);
-                if (lt_dp(ox, og, bx, bg) || (ox == bx && og == bg && ol < bl)) {
-                    bx = ox;
-                    bg = og;
-                    bl = ol;
-                }
-            }
-            if (lane == bl) ++h;
-            if (lane == 0) {
-                const bool empty = bg == INT32_MAX;
-                od[j] = empty ? __builtin_inf() : bx;
-                op[j] = empty ? -1 : bg;
-            }
-        }
-    }
-}
-
 struct RefineWs {
-    size_t scan, ld, lrow, lpos, lbound, failed, nfailed, pd, pg, total;
+    size_t scan, ld, lrow, lpos, lbound, failed, nfailed, pd, pg, kth_g, total;
     int kl;       // scan list length refined (>= k + 5, or 15 for k <= 10)
     int passes;   // 0: one scan of kl entries, else lower-bound passes
 };
@@ -657,6 +672,7 @@ RefineWs refine_ws(const lmi_index_desc* idx, int nq, int R, int k, int qmode) {
     w.nfailed = take(256);
     w.pd = take((size_t)kFbSlicedPairs * kFbSlices * kFbSliceK * 8);
     w.pg = take((size_t)kFbSlicedPairs * kFbSlices * kFbSliceK * 4);
+    w.kth_g = take(P * 4);
     w.scan = take(w.passes ? wide_ws_bytes(idx, nq, R, k + 5, qmode, w.kl)
                            : scan_workspace_bytes(idx, nq, R, w.kl, qmode));
     w.total = off;
@@ -1624,7 +1640,6 @@ void launch_refine(const RefineArgs& a, dim3 grid, dim3 fgrid, hipStream_t s) {
     if (a.pd) {
         hipLaunchKernelGGL((fallback_slice_kernel<TC, TQ>), dim3(2 * (unsigned)num_cus_ref()), dim3(kFbSliceT), 0,
                            s, a);
-        hipLaunchKernelGGL(fallback_merge_kernel, dim3((unsigned)num_cus_ref()), dim3(64), 0, s, a);
     }
     hipLaunchKernelGGL((fallback_kernel<TC, TQ>), fgrid, dim3(kFbT), 0, s, a);
 }
@@ -1647,16 +1662,11 @@ extern "C" int lmi_bucket_topk_f64(const lmi_index_desc* idx, const float* q, in
 
 namespace lmi {
 namespace {
-__global__ void kth_send_kernel(const float* ld, int kl, int k, int64_t P, float* out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P * k) return;
-    const int64_t p = i / k;
-    out[i] = ld[(size_t)p * kl + (i - p * k)];
-}
 
 // lmi_bucket_topk_f64q, and with `global` (ABI 10, lmi_bucket_topk_f64g) the
 // band decided over every rank's lists: the MERGE phase writes each pair's k
-// smallest d32 to kth_send, the REFINE phase reads the gathered kth_all
+// smallest d32 to kth_send (chunk_merge_band_kernel, beside the lists), the
+// REFINE phase reads the gathered kth_all
 int bucket_topk_f64_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                          const double* q64, int32_t ldq64, const int32_t* classes, int32_t R,
                          int32_t k, int32_t qmode, double eps, double* out_d, int32_t* out_pos,
@@ -1668,7 +1678,7 @@ int bucket_topk_f64_impl(const lmi_index_desc* idx, const float* q, int32_t nq, 
     int phases;
     bool do_refine;
     if (global) {
-        // PLAN / SCAN / MERGE (the chunk merge, then kth_send) and REFINE;
+        // PLAN / SCAN / MERGE (the chunk merge, writing kth_send) and REFINE;
         // none = all four (one rank: kth_all == kth_send)
         const bool ref = (qmode & LMI_Q_PHASE_REFINE) != 0;
         qmode &= ~LMI_Q_PHASE_REFINE;
@@ -1765,16 +1775,20 @@ int bucket_topk_f64_impl(const lmi_index_desc* idx, const float* q, int32_t nq, 
         : bucket_topk_impl(idx, q, nq, ldq, classes, R, kl, qmode, (float*)(ws + w.ld),
                            (int32_t*)(ws + w.lpos), (int32_t*)(ws + w.lrow), status,
                            ws + w.scan, w.total - w.scan, s, nullptr, 0, true, seed,
-                           (float)(2.0 * eps), phases, nullptr, band ? (float*)(ws + w.lbound) : nullptr);
+                           (float)(2.0 * eps), phases, nullptr, band ? (float*)(ws + w.lbound) : nullptr,
+                           global ? kth_send : nullptr, k);
     if (rc != LMI_OK) return rc;
     const int64_t P = (int64_t)nq * R;
-    if (global && (phases & kPhaseMerge) && P > 0) {
-        const int64_t n = P * k;
-        hipLaunchKernelGGL(kth_send_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                           (const float*)(ws + w.ld), kl, k, P, kth_send);
-        LMI_LAUNCH_CHECK("kth_send_kernel");
-    }
     if (!do_refine) return LMI_OK;
+    if (global && P > 0) {
+        int W = 1;
+        while (W < kth_G) W <<= 1;
+        const int64_t pairs_per_block = 4 * (64 / W);
+        a.kth_g = (const float*)(ws + w.kth_g);
+        hipLaunchKernelGGL(band_kth_kernel, dim3((unsigned)((P + pairs_per_block - 1) / pairs_per_block)), dim3(256), 0,
+                           s, kth_all, kth_G, kth_stride, P, k, (float*)(ws + w.kth_g));
+        LMI_LAUNCH_CHECK("band_kth_kernel");
+    }
     const dim3 grid((unsigned)((P + kRefT / 64 - 1) / (kRefT / 64)));
     const dim3 fgrid((unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref())));
     if (idx->corpus64)

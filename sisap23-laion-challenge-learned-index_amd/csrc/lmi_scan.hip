@@ -699,11 +699,19 @@ __global__ __launch_bounds__(kMergeBlock) void chunk_merge_band_kernel(
     const int32_t* __restrict__ pair_bucket, const int32_t* __restrict__ chunk_first,
     const int32_t* __restrict__ gpos, int32_t P, int32_t k, int32_t ldo, float* __restrict__ out_d,
     int32_t* __restrict__ out_pos, int32_t* __restrict__ out_row, float* __restrict__ out_bound,
-    int64_t n_rows, int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask, int32_t S) {
+    int64_t n_rows, int32_t* __restrict__ status, const uint32_t* __restrict__ split_mask, int32_t S,
+    float* __restrict__ kth_out, int32_t kth_k, const int32_t* __restrict__ classes, int32_t C) {
     constexpr int NB = kBandSlot, KB = kBandSlot - 1;
     const int gt = blockIdx.x * kMergeBlock + threadIdx.x;
     const int pp = gt / kMergeLanes, sub = gt % kMergeLanes;
     if (pp >= P) return;
+    // (kth_out of a pair whose class is out of range -- it has no grouped
+    // position -- is +inf: lane 1 of grouped position pp takes pair id pp)
+    if (kth_out != nullptr && sub == 1) {
+        const int cl = classes[pp];
+        if (cl < 0 || cl >= C)
+            for (int i = 0; i < kth_k; ++i) kth_out[(size_t)pp * kth_k + i] = __builtin_inff();
+    }
     const int c = pair_bucket[pp];
     if (c < 0) return;
     const int nch_c = chunk_first[c + 1] - chunk_first[c];
@@ -722,9 +730,11 @@ __global__ __launch_bounds__(kMergeBlock) void chunk_merge_band_kernel(
         if (i < k && i % kMergeLanes == sub) {
             const uint64_t key = M[i];
             const bool empty = key == kEmptyKey;
-            out_d[o + i] = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
+            const float dv = empty ? __builtin_inff() : ord2f((uint32_t)(key >> 32));
+            out_d[o + i] = dv;
             out_pos[o + i] = empty ? -1 : (int32_t)(uint32_t)key;
             out_row[o + i] = empty ? -1 : W[i];
+            if (kth_out != nullptr && i < kth_k) kth_out[(size_t)pid * kth_k + i] = dv;
         }
     }
     if (sub == 0) out_bound[pid] = ub == 0xffffffffu ? __builtin_inff() : ord2f(ub);
@@ -1368,7 +1378,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                           int32_t* out_pos, int32_t* out_row, int32_t* status, void* workspace,
                           size_t ws_bytes, hipStream_t s, const unsigned long long* lo_g, int32_t ldo,
                           bool prefill, bool seed_r0, float seed_margin, int phases,
-                          const WideScan* wide, float* out_bound) {
+                          const WideScan* wide, float* out_bound, float* kth_out, int32_t kth_k) {
     const bool do_plan = phases & kPhasePlan, do_scan = phases & kPhaseScan,
                do_merge = phases & kPhaseMerge;
     using namespace lmi;
@@ -1417,6 +1427,7 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
         fills.v[fills.n] = 0x7f800000u;
         fills.per_q[fills.n] = R;
         ++fills.n;
+
     }
     if (idx->n_rows > 0) {
         auto add = [&](void* ptr, uint32_t v, int per_q) {
@@ -1440,7 +1451,11 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
                            out_row, prefill ? R * ldo : 0, fills);
         LMI_LAUNCH_CHECK("prep_kernel");
     }
-    if (idx->n_rows == 0) return LMI_OK;
+    if (idx->n_rows == 0) {
+        // (an empty shard lists nothing: its kth block is all +inf)
+        if (kth_out != nullptr && do_merge) LMI_TRY(fill_u32(kth_out, 0x7f800000u, (size_t)P * kth_k, s));
+        return LMI_OK;
+    }
 
     int32_t* counts = (int32_t*)(ws + w.counts);
     int32_t* pair_q = (int32_t*)(ws + w.pair_q);
@@ -1629,7 +1644,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     if (band) {
         hipLaunchKernelGGL(chunk_merge_band_kernel, dim3(grid), dim3(kMergeBlock), 0, s, a.partial, a.max_chunks,
                            pair_q, pair_bucket, idx->chunk_first, idx->gpos, P, k, ldo, out_d, out_pos,
-                           out_row, out_bound, idx->n_rows, status, split_mask, w.split_s);
+                           out_row, out_bound, idx->n_rows, status, split_mask, w.split_s, kth_out, kth_k,
+                           classes, C);
         LMI_LAUNCH_CHECK("chunk_merge_band_kernel");
         return LMI_OK;
     }

@@ -128,3 +128,39 @@ def test_global_band_not_offered_without_band_lists():
     assert global_band(ix, 40, 4, 10, _lib.LMI_Q_F16)
     assert not global_band(ix, 40, 4, 12, _lib.LMI_Q_F16)   # k > 10: 15-entry lane lists
     assert not global_band(ix, 40, 4, 10, _lib.LMI_Q_F32)   # the general fp32 scan
+
+
+@pytest.mark.parametrize("n,G", [(6000, 3), (6, 8)])
+def test_kth_blocks_cover_every_pair(n, G):
+    """The MERGE phase writes each pair's k smallest d32 beside its band list
+    (chunk_merge_band_kernel): every entry of the kth block is written -- +inf
+    for pairs whose class is out of range (no grouped position) and for a
+    stripe with no rows at all (n = 6 over 8 stripes) -- and the stripes still
+    merge to the one-GPU float64 lists."""
+    w = workloads.clustered(n=n, nq=40, C=4 if n < 100 else 16, seed=705,
+                            label_mode="router" if n < 100 else "near")
+    w["x"] = w["x"].astype(np.float16).astype(np.float32)  # (fp16-exact: the band lists' scan)
+    R, k = 4, 10
+    classes = O.rank_classes(O.mlp_forward(w["qn"], w["layers"]))[:, :R].astype(np.int32)
+    classes[0, :] = -1
+    classes[1, 2] = w["C"]
+    cls = T(classes)
+    q = T(w["q"])
+    nq = classes.shape[0]
+    P = nq * R
+    one = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=256, device="cuda")
+    d0, p0, st0 = bucket_topk_f64(one, q, cls, k, qmode=_lib.LMI_Q_F16)
+    for g in range(G):
+        ix = DeviceIndex(w["x"], w["labels"], w["C"], chunk_rows=256, device="cuda", rank=g, world=G)
+        kth = torch.full((P * k,), float("nan"), dtype=torch.float32, device="cuda")
+        d = torch.empty((nq, R, k), dtype=torch.float64, device="cuda")
+        p = torch.empty((nq, R, k), dtype=torch.int32, device="cuda")
+        st = torch.zeros((1,), dtype=torch.int32, device="cuda")
+        bucket_topk_f64(ix, q, cls, k, qmode=_lib.LMI_Q_F16, out=(d, p, st), phases=PH3,
+                        band_x=(kth, None, G))
+        kb = kth.view(nq, R, k).cpu().numpy()
+        assert not np.isnan(kb).any()
+        assert np.isinf(kb[0]).all() and np.isinf(kb[1, 2]).all()
+        assert (np.diff(kb, axis=2)[np.isfinite(kb[..., 1:])] >= 0).all()
+    md, mp, _, _ = _stripes_global(w, w["x"], q, cls, G, k, False)
+    assert torch.equal(md, d0) and torch.equal(mp, p0)
