@@ -131,6 +131,14 @@ __device__ __forceinline__ uint64_t lds_get_u64_at(uint32_t addr) {
     asm volatile("ds_read_b64 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
     return v;
 }
+// an LDS atomic add returning the old value (inline asm like the list
+// accesses: the compiler would put a vmcnt wait -- the LDS-DMA writes into the
+// ring -- in front of a C++ LDS access in the block loop)
+__device__ __forceinline__ uint32_t lds_add_rtn_u32(uint32_t addr, uint32_t v) {
+    uint32_t r;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr), "v"(v) : "memory");
+    return r;
+}
 template <int KL, int OFF = 0, int ES = 512>
 __device__ __forceinline__ void list_store(uint32_t addr, const uint64_t (&L)[KL]) {
     [&]<int... I>(std::integer_sequence<int, I...>) {
@@ -347,6 +355,12 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
     uint64_t* lists = reinterpret_cast<uint64_t*>(smem + NSLOT * STAGE);
     int* wtab = reinterpret_cast<int*>(lists + NW * 64 * LS);  // [NW] SIMD ids, [NW] tile
     int& s_tile = wtab[NW];
+    // MODE 2 (collect): the lists' area holds instead each of the tile's 256
+    // pairs' candidate stage (kXS keys) and its count
+    constexpr int kXS = 19;
+    static_assert(MODE != 2 || (size_t)NW * 32 * (kXS * 8 + 4) <= (size_t)NW * 64 * LS * 8, "collect stage");
+    uint64_t* xst = lists;
+    uint32_t* xcnt = reinterpret_cast<uint32_t*>(lists + NW * 32 * kXS);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -506,6 +520,8 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             list_clear<KL>(E);
             list_store<KL, 0, ES>(opaque_u(lbase), E);
             if constexpr (MODE == 3) lds_put_u64_at<KL * ES>(opaque_u(lbase), kEmptyKey);
+        } else {
+            if (h == 0) xcnt[32 * slot + col] = 0u;
         }
         __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
         __syncthreads();
@@ -567,18 +583,20 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                 }
             }
             if constexpr (MODE == 2) {
-                // collect: the pair's two lanes reserve their candidates'
-                // slots with one atomic (lane hh = 0), then store them in
-                // row order; slots past cap are counted, not stored
+                // collect: each lane reserves slots of its pair's stage in
+                // LDS (an LDS atomic) and writes its candidates there -- no
+                // global memory op in the block loop, whose return the early
+                // wave would wait for behind its next block's DMA (vmcnt);
+                // the stage goes to the pair's candidate buffer at the tile
+                // end.  Keys past kXS go to the buffer directly (a global
+                // atomic each: rare); slots past cap are counted, not stored.
                 if (__any(mask != 0)) {
                     const uint32_t rb = (uint32_t)(row0u + eb * 32 + 4 * hh);
                     const uint32_t c = (uint32_t)__builtin_popcount(mask);
-                    const uint32_t cp = partner_u32(c, hh);
-                    uint32_t base = 0;
-                    if (hh == 0 && c + cp != 0) base = atomicAdd(&a.ccount[pp], c + cp);
-                    const uint32_t bp = partner_u32(base, hh);
-                    uint32_t at = hh == 0 ? base : bp + cp;
-                    uint64_t* dst = a.cand + (size_t)pp * (uint32_t)a.cap;
+                    const int lp = 32 * slot + col;
+                    uint32_t at = 0;
+                    if (c != 0) at = lds_add_rtn_u32((uint32_t)(uintptr_t)(xcnt + lp), c);
+                    const uint32_t sa = (uint32_t)(uintptr_t)(xst + lp * kXS);
                     uint32_t m = mask;
 #pragma unroll 1
                     while (__any(m != 0)) {
@@ -589,7 +607,13 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
                             const int i = (rg & 3) + 8 * (rg >> 2);
                             const float n1 = *reinterpret_cast<const float*>(nb + i * 4);
                             const float d = fmaf(-select16(acc, rg), my_invq * n1, 1.0f);
-                            if (at < (uint32_t)a.cap) dst[at] = make_key(d, rb + (uint32_t)i);
+                            const uint64_t key = make_key(d, rb + (uint32_t)i);
+                            if (at < (uint32_t)kXS) {
+                                lds_put_u64_at<0>(sa + 8u * at, key);
+                            } else {
+                                const uint32_t g = atomicAdd(&a.ccount[pp], 1u);
+                                if (g < (uint32_t)a.cap) a.cand[(size_t)pp * (uint32_t)a.cap + g] = key;
+                            }
                             ++at;
                         }
                     }
@@ -824,6 +848,19 @@ __global__ __launch_bounds__(512, 1) void scan3_kernel(Scan2Args a) {
             }
         }
         __syncthreads();  // every wave's DMA drained (the tail waited vmcnt(0))
+
+        // ---- collect: each pair's stage to its candidate buffer ------------
+        if (MODE == 2 && h == 0 && live) {
+            const int lp = 32 * slot + col;
+            const uint32_t n = std::min<uint32_t>(xcnt[lp], (uint32_t)kXS);
+            if (n != 0) {
+                const uint32_t base = atomicAdd(&a.ccount[pp], n);
+                uint64_t* dst = a.cand + (size_t)pp * (uint32_t)a.cap;
+#pragma unroll 1
+                for (uint32_t i = 0; i < n; ++i)
+                    if (base + i < (uint32_t)a.cap) dst[base + i] = xst[lp * kXS + i];
+            }
+        }
 
         // ---- merge the two partial lists of each query (lanes col, col+32) ----
         if (MODE == 3 && h == 0 && live) {
