@@ -145,19 +145,27 @@ constexpr int kUCap = 8192;  // relevant positions of a group held in LDS
 constexpr int kBmBits = 196608;  // selection bitmap: U's positions spanning < 192K (24 KiB)
 constexpr int kTG = 1024;    // group kernel: one large workgroup per category
 
-template <int NT>
-__device__ inline int block_reduce_g(int v, int* sh, bool is_min) {
-    v = is_min ? wave_min_i(v) : __ockl_wfred_add_i32(v);
+// sum, min and max over the workgroup in one pass (one barrier; sh3 is used
+// once per workgroup, so no trailing barrier)
+__device__ inline void block_sum_min_max_g(int& s, int& mn, int& mx, int (*sh3)[kTG / 64]) {
+    s = __ockl_wfred_add_i32(s);
+    mn = wave_min_i(mn);
+    mx = -wave_min_i(-mx);
+    if ((threadIdx.x & 63) == 0) {
+        sh3[0][threadIdx.x >> 6] = s;
+        sh3[1][threadIdx.x >> 6] = mn;
+        sh3[2][threadIdx.x >> 6] = mx;
+    }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-    __syncthreads();
-    int t = sh[0];
-    for (int w = 1; w < NT / 64; ++w) t = is_min ? min(t, sh[w]) : t + sh[w];
-    __syncthreads();
-    return t;
+    s = sh3[0][0];
+    mn = sh3[1][0];
+    mx = sh3[2][0];
+    for (int w = 1; w < kTG / 64; ++w) {
+        s += sh3[0][w];
+        mn = min(mn, sh3[1][w]);
+        mx = max(mx, sh3[2][w]);
+    }
 }
-__device__ inline int block_sum_g(int v, int* sh) { return block_reduce_g<kTG>(v, sh, false); }
-__device__ inline int block_min_g(int v, int* sh) { return block_reduce_g<kTG>(v, sh, true); }
 
 // The groups of every round at once (grid (C + 1) x R), before round 0:
 // category c of round r = the queries with classes[q, r] == c in ascending q,
@@ -231,7 +239,6 @@ __global__ __launch_bounds__(kTG) void replay_groups_kernel(const int32_t* __res
 }
 
 __device__ void replay_group_body(const RoundArgs& a, const int c) {
-    __shared__ int sh[kTG / 64];
     __shared__ int32_t S[2 * kMaxKr + 16];  // smallest members of U, ascending
     __shared__ Ent qrow[kMaxKr];            // the quirk row of the group
     __shared__ int32_t Ul[kUCap];
@@ -239,6 +246,7 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
     __shared__ int nsw[kTG / 64 + 1];
     __shared__ int wsum[kTG / 64];
     __shared__ uint32_t bm[kBmBits / 32];  // U as a bitmap (positions - umin)
+    __shared__ int sh3[3][kTG / 64];
     const int tid = threadIdx.x;
     if (c >= a.C) return;               // out-of-range classes: no group
     if (a.bucket_size[c] <= 0) return;  // groupby visits non-empty categories only
@@ -262,6 +270,11 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
         constexpr int kUL = 8;
         int nb_tot = 0;
         int umin = INT32_MAX, umax = -1;  // range of U's relevant positions
+        // (this thread's first kUL entries stay in registers for the B_q
+        // writes below: no second round of dependent global loads)
+        int32_t p0v[kUL];
+        int q0v[kUL];
+        double d0v[kUL];
         for (int e0 = tid; e0 < nU; e0 += kUL * kTG) {
             int qv[kUL];
             size_t ov[kUL];
@@ -291,12 +304,15 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
                     umin = min(umin, pv[u]);
                     umax = max(umax, pv[u]);
                 }
+                if (e0 == tid) {
+                    p0v[u] = (e < nU && rel) ? pv[u] : INT32_MAX;
+                    q0v[u] = qv[u];
+                    d0v[u] = dv[u];
+                }
             }
         }
-        nb_tot = block_sum_g(nb_tot, sh);  // (its barriers publish U)
+        block_sum_min_max_g(nb_tot, umin, umax, sh3);  // (its barrier publishes U)
         if (nb_tot == 0) return;  // LearnedIndex.py:157-159
-        umin = block_min_g(umin, sh);
-        umax = -block_min_g(-umax, sh);
         const int want = kr + kl_use;
         const int lane = tid & 63, wv = tid >> 6;
         if (umax - umin < kBmBits) {
@@ -434,19 +450,28 @@ __device__ void replay_group_body(const RoundArgs& a, const int c) {
             for (int e0 = tid; e0 < nU; e0 += kUL * kTG) {
                 int32_t pv[kUL];
                 int qv[kUL];
-#pragma unroll
-                for (int u = 0; u < kUL; ++u) {
-                    const int e = e0 + u * kTG;
-                    pv[u] = e < nU ? U[e] : INT32_MAX;
-                    const int gi = g0 + e / kl_use;
-                    qv[u] = pv[u] != INT32_MAX ? G[gi] : 0;
-                }
                 double dv[kUL];
+                if (e0 == tid) {
 #pragma unroll
-                for (int u = 0; u < kUL; ++u) {
-                    const int e = e0 + u * kTG;
-                    const int j = e - (e / kl_use) * kl_use;
-                    dv[u] = pv[u] != INT32_MAX ? list_d(a, ((size_t)qv[u] * a.R + a.r) * a.kl + j) : 0.0;
+                    for (int u = 0; u < kUL; ++u) {
+                        pv[u] = p0v[u];
+                        qv[u] = q0v[u];
+                        dv[u] = d0v[u];
+                    }
+                } else {
+#pragma unroll
+                    for (int u = 0; u < kUL; ++u) {
+                        const int e = e0 + u * kTG;
+                        pv[u] = e < nU ? U[e] : INT32_MAX;
+                        const int gi = g0 + e / kl_use;
+                        qv[u] = pv[u] != INT32_MAX ? G[gi] : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kUL; ++u) {
+                        const int e = e0 + u * kTG;
+                        const int j = e - (e / kl_use) * kl_use;
+                        dv[u] = pv[u] != INT32_MAX ? list_d(a, ((size_t)qv[u] * a.R + a.r) * a.kl + j) : 0.0;
+                    }
                 }
 #pragma unroll
                 for (int u = 0; u < kUL; ++u) {
