@@ -111,7 +111,7 @@ def queue_streams(dev, n: int):
     return have
 
 
-def stream_reserve(dev, exchange: bool, dist: str, split: bool) -> int:
+def stream_reserve() -> int:
     """The default `reserve_cus` of a StreamedSearch: LMI_STREAM_RESERVE if set,
     else 0.  Measured (10M, W = 1, profiles/r06p_reserve_ab.txt): leaving 2,
     4 or 8 CUs to the finish made the float32 step 7.41-7.47 ms against
@@ -379,7 +379,7 @@ class StreamedSearch:
         # lookahead scan does not wait for this launch's finish (its slot is
         # not the finish's), so the finish runs beside the next scan instead
         # of between two scans (DESIGN.md §5 "The finish beside the scan")
-        self.reserve_cus = r = stream_reserve(dev, X, dist, split) if reserve_cus is None else int(reserve_cus)
+        self.reserve_cus = r = stream_reserve() if reserve_cus is None else int(reserve_cus)
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
         if not 0 <= r < ncu:
             raise ValueError(f"reserve_cus={r} outside [0, {ncu})")
