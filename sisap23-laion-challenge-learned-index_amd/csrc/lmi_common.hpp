@@ -240,6 +240,11 @@ struct XArgs {
     // ABI 11: rows32 normalised as sklearn does in float32 (idx->corpus32n) or
     // null (then normalised per candidate)
     const float* rows32n;
+    // the grouped pairs x_select_wave_kernel leaves to x_select_kernel (more
+    // candidates, overflowed, unbounded), appended by the wave kernel, and
+    // their count (null: x_select_kernel walks every grouped pair)
+    int32_t* wgl;
+    int32_t* n_wgl;
 };
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);

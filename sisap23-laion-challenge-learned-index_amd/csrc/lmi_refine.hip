@@ -1264,8 +1264,11 @@ __global__ __launch_bounds__(kXT) void x_select_kernel(XArgs a) {
     extern __shared__ double x_lds[];
     __shared__ uint32_t s_nr;
     const int P = a.nq * a.R;
-    for (int pp = blockIdx.x; pp < P; pp += gridDim.x) {
-        x_select_pair<TC, TQ, OUT64>(a, pp, x_lds, reinterpret_cast<int32_t*>(x_lds + a.cap), s_nr);
+    // (after x_select_wave_kernel: only the pairs it listed -- a walk over
+    // every grouped pair cost ~0.36 ms a batch of dependent loads to skip them)
+    const int n = a.wgl ? *a.n_wgl : P;
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        x_select_pair<TC, TQ, OUT64>(a, a.wgl ? a.wgl[i] : i, x_lds, reinterpret_cast<int32_t*>(x_lds + a.cap), s_nr);
         __syncthreads();  // (the pair's LDS lists are read before the next pair's fill)
     }
 }
@@ -1299,7 +1302,11 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
     const int64_t P = (int64_t)a.nq * a.R;
     if (p < 0 || p >= P) return;
     const uint32_t n = a.ccount[pp];
-    if (!x_wave_pair(a, n, p)) return;
+    if (!x_wave_pair(a, n, p)) {
+        // (x_select_kernel's: it walks this list instead of every pair)
+        if (a.wgl && lane == 0) a.wgl[atomicAdd(a.n_wgl, 1)] = pp;
+        return;
+    }
     const uint64_t* src = a.cand + (size_t)pp * a.cap;
     uint64_t key[4], work[4];
 #pragma unroll

@@ -1687,7 +1687,7 @@ double split_eps(int d_pad) {
 
 namespace {
 struct XWs {
-    size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
+    size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, wgl, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
         classes2, qn32, grp, tailq, goff, region, region_bytes, region_s, region_s_bytes, total;
     int32_t cap;
 };
@@ -1746,7 +1746,8 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.ccount = take(P * 4);
     w.cand = take(P * (size_t)cap * 8);
     w.failed = take(P * 4);
-    w.nfailed = take(256);
+    w.nfailed = take(256);  // (word 0: the failed pairs; word 16: the wgl pairs)
+    w.wgl = take(P * 4);
     const lmi_index_desc bd = bound_desc(idx, kXLists, nullptr);
     const lmi_index_desc sd = x_sample_desc(idx, nullptr, nullptr);
     w.region_bytes = std::max({ws_layout(idx, nq, R, k, LMI_Q_F16).total, ws_layout(idx, nq, R, 10, LMI_Q_F16).total,
@@ -1817,7 +1818,7 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
             hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)),
                                dim3(kThreads), 0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
             LMI_LAUNCH_CHECK("x_round_queries_kernel");
-            LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
+            LMI_TRY(fill_u32(ws + w.nfailed, 0u, 32, s));
             hipLaunchKernelGGL(x_sample_desc_kernel, dim3((unsigned)std::min(1024, (P + 63) / 64)), dim3(64), 0, s,
                                idx->bucket_off, idx->n_buckets, (int64_t)idx->chunk_rows, classes, P, off2, cf2,
                                classes2);
@@ -1850,7 +1851,7 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)), dim3(kThreads),
                        0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
     LMI_LAUNCH_CHECK("x_round_queries_kernel");
-    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 1, s));
+    LMI_TRY(fill_u32(ws + w.nfailed, 0u, 32, s));
     if (sampled) {
         // 1. a bound per pair from a sample: the wide path's chunk-list scan
         //    (two lists per bucket, each scanning the first quarter of its
@@ -1927,6 +1928,8 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     a.out_pos = out_pos;
     a.failed = (int32_t*)(ws + w.failed);
     a.n_failed = (int32_t*)(ws + w.nfailed);
+    a.wgl = sampled ? (int32_t*)(ws + w.wgl) : nullptr;  // (two_eps > 0: the wave kernel runs)
+    a.n_wgl = (int32_t*)(ws + w.nfailed) + 16;
     a.status = status;
     a.two_eps = sampled ? two_eps : 0.0;
     a.fix = sampled && !x_sample(k) ? fix : nullptr;
