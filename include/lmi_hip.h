@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define LMI_ABI_VERSION 12
+#define LMI_ABI_VERSION 13
 
 /* ---- status codes ---------------------------------------------------- */
 #define LMI_OK 0
@@ -331,6 +331,13 @@ int lmi_split_normalize(const float* rows, int64_t n, int32_t d, int32_t d_pad, 
 int lmi_refine_fallback_count(const void* workspace, const lmi_index_desc* idx, int32_t nq,
                               int32_t R, int32_t k, int32_t qmode, int32_t* count_out,
                               void* stream);
+/* ABI 13, diagnostic (synchronises `stream`): the split mode (k <= 10) collects
+ * the rest of every bucket whose sample is at most a quarter of it and takes the
+ * sample's rows from the sample scan's own list; how many pairs of the last call
+ * on this workspace had a band reaching that list's k-th and were scored over
+ * their sample rows and candidates instead (x_fallback_kernel). */
+int lmi_split_sample_fallback_count(const void* workspace, const lmi_index_desc* idx, int32_t nq,
+                                    int32_t R, int32_t k, int32_t* count_out, void* stream);
 /* K3 on float64 lists: order (d64, pos). */
 int lmi_merge_topk_f64(const double* d_in, const int32_t* pos_in, int32_t G, int64_t rows,
                        int32_t k, double* out_d, int32_t* out_pos, void* stream);

@@ -45,6 +45,7 @@ EnvConfig read_env() {
     e.router_qg = env_i("LMI_ROUTER_QG", 0);
     e.refine_kb = env_i("LMI_REFINE_KB", 1);
     e.xsel_kb = env_i("LMI_XSEL_KB", 1);
+    e.x_skip = env_i("LMI_X_SKIP_SHARE", 4);
     return e;
 }
 

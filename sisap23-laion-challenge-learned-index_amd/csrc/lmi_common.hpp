@@ -160,6 +160,13 @@ struct WideScan {
     int32_t nbins;
     const int32_t* sub_rows;  // mode 1: Scan2Args::sub_rows / sub_take
     const int32_t* sub_take;
+    // mode 2: a pair whose (odd) bucket b has rows skipped in front of it
+    // (bucket b - 1 of the descriptor not empty: the split mode's sample,
+    // x_collect_desc) starts with its app_k (distance, row) entries app_d /
+    // app_row [pair id][app_k] as candidates (-1 rows skipped); null: none
+    const float* app_d;
+    const int32_t* app_row;
+    int32_t app_k;
 };
 int bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t ldq,
                      const int32_t* classes, int32_t R, int32_t k, int32_t qmode, float* out_d,
@@ -245,7 +252,27 @@ struct XArgs {
     // their count (null: x_select_kernel walks every grouped pair)
     int32_t* wgl;
     int32_t* n_wgl;
+    // the collect scan skipped each split bucket's sample rows (x_collect_desc):
+    // soff [2C+1] (bucket c's sample rows [soff[2c], soff[2c+1]), empty where the
+    // bucket was collected whole) and skth [nq*R][k] the sample's own lists (the
+    // pair's k-th at k - 1); a pair whose band reaches its sample's k-th goes to
+    // sfailed (grouped pair ids, count n_sfailed) and x_fallback_kernel scores
+    // its sample rows and its candidates exactly.  null: none skipped.  plan_cm:
+    // plan_counts has plan_cm entries per bucket, the pairs of bucket c at
+    // plan_cm c + plan_cm - 1
+    const int64_t* soff;
+    const float* skth;
+    int32_t* sfailed;
+    int32_t* n_sfailed;
+    double* spd;     // the sliced sfailed pairs' slice lists (x_fallback_slice_kernel)
+    int32_t* spg;
+    int32_t plan_cm;
 };
+// the sliced sample fallback (x_fallback_slice_kernel): the first
+// kXSlicedPairs sfailed pairs, kXSlices slices each (XArgs::spd / spg hold
+// kXSlicedPairs x kXSlices x k entries)
+constexpr int kXSlices = 32;
+constexpr int kXSlicedPairs = 256;
 int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s);
 double split_eps(int d_pad);
 size_t x_ws_bytes(const lmi_index_desc* idx, int nq, int R, int k);

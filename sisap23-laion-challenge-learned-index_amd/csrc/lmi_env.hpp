@@ -27,6 +27,7 @@ struct EnvConfig {
     bool router_fma;     // LMI_ROUTER_FMA: FMA-chain router instead of MFMA
     int router_qg;       // LMI_ROUTER_QG: 1/2/4 query groups per workgroup, 0 = auto
     int xsel_kb;         // LMI_XSEL_KB: rows in flight per wave in the split mode's one-wave select (1, 2 or 4; default 1: 7 waves per SIMD)
+    int x_skip;          // LMI_X_SKIP_SHARE: the split mode's collect skips a bucket's sample of at most 1/N of it (default 4; 0: never)
     int refine_kb;       // LMI_REFINE_KB: fp16 rows in flight per wave in the float64 refine (1, 2 or 4; default 1: 8 waves per SIMD)
 };
 const EnvConfig& env_config();

@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(256) void x_groups_kernel(const int32_t* __restrict
 // id, so every round's pairs in ascending q: ranks by ballots, 64 pairs at a
 // time); and the buckets' global offsets (block 0, lane 0)
 __global__ __launch_bounds__(64) void x_tail_kernel(const int32_t* __restrict__ pair_q,
-                                                    const int32_t* __restrict__ counts, int32_t R, int32_t C,
+                                                    const int32_t* __restrict__ counts, int32_t cm, int32_t R, int32_t C,
                                                     const int32_t* __restrict__ grp,
                                                     const int64_t* __restrict__ nrows_c,
                                                     const int64_t* __restrict__ bucket_off, uint8_t* __restrict__ tailq,
@@ -1063,11 +1063,13 @@ __global__ __launch_bounds__(64) void x_tail_kernel(const int32_t* __restrict__ 
         }
         goff[C] = acc;
     }
+    // (the plan's bucket of c: cm c + cm - 1, cm buckets per class)
+    const int cb = cm * c + cm - 1;
     int s = 0;
-    for (int b = lane; b < c; b += 64) s += counts[b];
+    for (int b = lane; b < cb; b += 64) s += counts[b];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    const int e = s + counts[c];
+    const int e = s + counts[cb];
     const uint64_t below = (1ull << lane) - 1ull;
     int base[LMI_MAX_R];
 #pragma unroll
@@ -1124,6 +1126,16 @@ __device__ inline bool x_wave_pair(const XArgs& a, uint32_t n, int p) {
     return a.two_eps > 0.0 && n <= (uint32_t)kXW && n <= (uint32_t)a.cap && !(a.fix && a.fix[p]);
 }
 
+// the collect scan skipped the pair's sample rows (XArgs::soff) and its band
+// (d~ <= t) reaches the sample's own k-th: an unlisted sample row may lie in
+// it, so the pair is scored over its sample rows (x_fallback_kernel)
+__device__ inline bool x_band_past_sample(const XArgs& a, int p, double t) {
+    if (!a.soff) return false;
+    const int c = a.classes[p];
+    if (c < 0 || c >= a.C || !(a.soff[2 * c] < a.soff[2 * c + 1])) return false;
+    return (double)a.skth[(size_t)p * a.k + a.k - 1] <= t;
+}
+
 // A workgroup on one grouped pair of the collect scan: the exact distance of
 // every candidate (a wave per kB rows), a bitonic sort of (distance, row) in
 // LDS -- rows ascend with global position inside a bucket shard, so this is
@@ -1172,6 +1184,10 @@ __device__ inline void x_select_pair(const XArgs& a, const int pp, double* sd, i
         }
         const double t = n >= (uint32_t)a.k ? (double)ord2f((uint32_t)(keys[a.k - 1] >> 32)) + a.two_eps
                                             : __builtin_inf();
+        if (x_band_past_sample(a, p, t)) {
+            if (tid == 0) a.sfailed[atomicAdd(a.n_sfailed, 1)] = pp;
+            return;
+        }
         uint32_t c = 0;
         for (uint32_t i = tid; i < n; i += kXT) c += (double)ord2f((uint32_t)(keys[i] >> 32)) <= t ? 1u : 0u;
         atomicAdd(&s_nr, c);
@@ -1327,6 +1343,10 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
     }
     const double t = (n >= (uint32_t)k && kth != kEmptyKey)
                          ? (double)ord2f((uint32_t)(kth >> 32)) + a.two_eps : __builtin_inf();
+    if (x_band_past_sample(a, p, t)) {
+        if (lane == 0) a.sfailed[atomicAdd(a.n_sfailed, 1)] = pp;
+        return;
+    }
     int32_t* rows = s_rows[w];
     int nr = 0;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -1436,100 +1456,208 @@ __global__ __launch_bounds__(kXT) __attribute__((amdgpu_waves_per_eu(sizeof(TC) 
     }
 }
 
+// The exact distances of a pair's rows vrow(j), j = j_lo .. j_hi - 1 (-1:
+// none) by the NW waves of a workgroup (a wave per kB rows; the float32 output
+// in the reference's order, a group of lanes per row, where blas32_kernel_of
+// restates it); lane 0 of wave w keeps the wave's top-k by (distance, row) in
+// L[w] / G[w].
+template <typename TC, typename TQ, bool OUT64, int NW, typename VR>
+__device__ inline void x_rows_topk(const XArgs& a, int64_t p, const VR& vrow, int64_t j_lo, int64_t j_hi,
+                                   double (*L)[LMI_MAX_K], int32_t (*G)[LMI_MAX_K]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k = a.k;
+    const int nps = (a.d + 255) / 256;
+    const double zero_eps = OUT64 ? kEps64 : kEps32;
+    double* Lw = L[w];
+    int32_t* Gw = G[w];
+    if (lane == 0)
+        for (int i = 0; i < k; ++i) {
+            Lw[i] = __builtin_inf();
+            Gw[i] = INT32_MAX;
+        }
+    auto keep = [&](double xv, int32_t rr) {
+        if (!lt_dp(xv, rr, Lw[k - 1], Gw[k - 1])) return;
+        int i = k - 1;
+        while (i > 0 && lt_dp(xv, rr, Lw[i - 1], Gw[i - 1])) {
+            Lw[i] = Lw[i - 1];
+            Gw[i] = Gw[i - 1];
+            --i;
+        }
+        Lw[i] = xv;
+        Gw[i] = rr;
+    };
+    const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
+    // the reference's float32 order: a group of nl lanes per row, 64 / nl rows
+    // a wave
+    const int nl = kern != 0 ? blas32_lanes(a, kern) : 4, per = 64 / nl;
+    const float* qn = kern != 0 ? a.qn32 + (size_t)(p / a.R) * a.d_pad : nullptr;
+    for (int64_t j0 = j_lo + (int64_t)w * per; kern != 0 && j0 < j_hi; j0 += (int64_t)NW * per) {
+        const int64_t jx = j0 + lane / nl;
+        const int64_t x = jx < j_hi ? vrow(jx) : -1;
+        const bool ok = x >= 0 && x < a.n_rows;
+        const float v = a.rows32n ? blas32_dist_group<true>(a, p, qn, ok ? x : 0, ok, kern, nl)
+                                   : blas32_dist_group<false>(a, p, qn, ok ? x : 0, ok, kern, nl);
+        for (int j = 0; j < per; ++j) {
+            const float vj = __shfl(v, nl * j);
+            const int32_t rr = __shfl(ok ? (int32_t)x : -1, nl * j);
+            if (lane == 0 && rr >= 0) keep((double)vj, rr);
+        }
+    }
+    double qh[3][4];
+    if (kern == 0) query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
+    for (int64_t j0 = j_lo + (int64_t)w * kB; kern == 0 && j0 < j_hi; j0 += (int64_t)NW * kB) {
+        int32_t r[kB];
+#pragma unroll
+        for (int b = 0; b < kB; ++b) {
+            const int64_t x = j0 + b < j_hi ? vrow(j0 + b) : -1;
+            r[b] = (x >= 0 && x < a.n_rows) ? (int32_t)x : -1;
+        }
+        double dv[kB];
+        rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
+        if (lane == 0) {
+#pragma unroll
+            for (int b = 0; b < kB; ++b)
+                if (r[b] >= 0) keep(out_value<OUT64>(dv[b]), r[b]);
+        }
+    }
+}
+
+// thread 0: the first k of the NW waves' lists (ascending, (inf, INT32_MAX)
+// padded) by (distance, row), handed to put(j, distance, row)
+template <int NW, typename PUT>
+__device__ inline void x_merge_waves(int k, double (*L)[LMI_MAX_K], int32_t (*G)[LMI_MAX_K], const PUT& put) {
+    int head[NW] = {};
+    for (int j = 0; j < k; ++j) {
+        int best = -1;
+        for (int v = 0; v < NW; ++v) {
+            if (head[v] >= k) continue;
+            if (best < 0 || lt_dp(L[v][head[v]], G[v][head[v]], L[best][head[best]], G[best][head[best]])) best = v;
+        }
+        put(j, L[best][head[best]], G[best][head[best]]);
+        ++head[best];
+    }
+}
+
+// A pair of sfailed (its band reached its skipped sample's k-th): its rows are
+// the sample's [soff[2c], soff[2c+1]) and then its collected candidates
+// outside it -- a superset of the pair's answer, each row once.
+struct XSampleRows {
+    int64_t b0, b1, nv;
+    const uint64_t* cnd;
+    __device__ int64_t operator()(int64_t j) const {
+        if (j >= nv) return -1;
+        if (j < b1 - b0) return b0 + j;
+        const int64_t x = (int64_t)(uint32_t)cnd[j - (b1 - b0)];
+        return (x >= b0 && x < b1) ? -1 : x;
+    }
+};
+__device__ inline XSampleRows x_sample_rows(const XArgs& a, int pp, int64_t p) {
+    const int c = a.classes[p];
+    XSampleRows v;
+    v.b0 = a.soff[2 * c];
+    v.b1 = a.soff[2 * c + 1];
+    v.cnd = a.cand + (size_t)pp * a.cap;
+    v.nv = (v.b1 - v.b0) + (int64_t)min(a.ccount[pp], (uint32_t)a.cap);
+    return v;
+}
+struct XBucketRows {
+    int64_t b0, b1;
+    __device__ int64_t operator()(int64_t j) const { return b0 + j < b1 ? b0 + j : -1; }
+};
+
+// The first kXSlicedPairs sfailed pairs: each pair's rows cut into kXSlices
+// slices, every (pair, slice) a workgroup item (a pair's ~n_c / 16 sample rows
+// on kXSlices CUs instead of one: ~1 ms a batch with one such pair before),
+// each writing its slice's top-k to spd / spg; x_fallback_kernel merges them.
+constexpr int kXSliceT = 256;  // (kXSlices, kXSlicedPairs: lmi_common.hpp)
+template <typename TC, typename TQ, bool OUT64>
+__global__ __launch_bounds__(kXSliceT) void x_fallback_slice_kernel(XArgs a) {
+    __shared__ double sd[kXSliceT / 64][LMI_MAX_K];
+    __shared__ int32_t sr[kXSliceT / 64][LMI_MAX_K];
+    const int ns = min(*a.n_sfailed, kXSlicedPairs);
+    for (int item = blockIdx.x; item < ns * kXSlices; item += gridDim.x) {
+        const int f = item / kXSlices, sl = item - f * kXSlices;
+        const int pp = a.sfailed[f];
+        const int64_t p = a.pair_q[pp];
+        const XSampleRows v = x_sample_rows(a, pp, p);
+        x_rows_topk<TC, TQ, OUT64, kXSliceT / 64>(a, p, v, v.nv * sl / kXSlices, v.nv * (sl + 1) / kXSlices, sd, sr);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double* od = a.spd + ((size_t)f * kXSlices + sl) * a.k;
+            int32_t* og = a.spg + ((size_t)f * kXSlices + sl) * a.k;
+            x_merge_waves<kXSliceT / 64>(a.k, sd, sr, [&](int j, double x, int32_t r) {
+                od[j] = x;
+                og[j] = r;
+            });
+        }
+        __syncthreads();
+    }
+}
+
+// one wave on sliced sfailed pair f: its kXSlices slice lists merged to the
+// first k (lane s walks slice s; position breaks distance ties)
+template <bool OUT64>
+__device__ inline void x_merge_slices(const XArgs& a, int f) {
+    const int k = a.k, lane = threadIdx.x & 63;
+    const int64_t p = a.pair_q[a.sfailed[f]];
+    const double* pd = a.spd + (size_t)f * kXSlices * k;
+    const int32_t* pg = a.spg + (size_t)f * kXSlices * k;
+    int h = 0;
+    for (int j = 0; j < k; ++j) {
+        const bool has = lane < kXSlices && h < k;
+        double bx = has ? pd[lane * k + h] : __builtin_inf();
+        int32_t bg = has ? pg[lane * k + h] : INT32_MAX;
+        int bl = lane;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const double ox = __shfl_xor(bx, off);
+            const int32_t og = __shfl_xor(bg, off);
+            const int ol = __shfl_xor(bl, off);
+            if (lt_dp(ox, og, bx, bg) || (ox == bx && og == bg && ol < bl)) {
+                bx = ox;
+                bg = og;
+                bl = ol;
+            }
+        }
+        if (lane == bl) ++h;
+        const bool empty = bg == INT32_MAX;
+        if (lane == 0) x_store<OUT64>(a, (size_t)p * k + j, empty ? __builtin_inf() : bx, empty ? -1 : a.gpos[bg]);
+    }
+}
+
 // One workgroup per overflowed pair: the exact distance of every row of its
-// bucket shard (a wave per kB rows; the float32 output in the reference's
-// order, a quad per row, where blas32_kernel_of restates it), lane 0 of each
-// wave keeps the wave's top-k by (distance, row) in LDS, thread 0 merges the
-// waves' lists.
+// bucket shard (x_rows_topk over 16 waves), thread 0 merges the waves' lists;
+// then the sfailed pairs past the sliced ones, over their sample rows and
+// candidates.  Wave 0 first merges the sliced sfailed pairs' slice lists.
 template <typename TC, typename TQ, bool OUT64>
 __global__ __launch_bounds__(kFbT) void x_fallback_kernel(XArgs a) {
     __shared__ double sd[kFbT / 64][LMI_MAX_K];
     __shared__ int32_t sr[kFbT / 64][LMI_MAX_K];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6;
     const int nf = *a.n_failed;
+    const int ns = a.n_sfailed ? *a.n_sfailed : 0;
+    const int nsl = min(ns, kXSlicedPairs);
     const int k = a.k;
-    const int nps = (a.d + 255) / 256;
-    const double zero_eps = OUT64 ? kEps64 : kEps32;
-    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
-        const int64_t p = a.failed[f];
-        const int c = a.classes[p];  // classes [nq][R]: pair p = q*R + r
-        const int64_t b0 = a.bucket_off[c], b1 = a.bucket_off[c + 1];
-        double qh[3][4];
-        query_hat_x<TQ, 3>(x_query<TQ>(a, p / a.R), a.d, nps, zero_eps, qh);
-        double* L = sd[w];
-        int32_t* G = sr[w];
-        if (lane == 0)
-            for (int i = 0; i < k; ++i) {
-                L[i] = __builtin_inf();
-                G[i] = INT32_MAX;
-            }
-        const int kern = OUT64 ? 0 : blas32_kernel_of(a, p);
-        // the reference's float32 order: a group of nl lanes per row, 64 / nl
-        // rows a wave, lane 0 keeping them in ascending row order
-        const int nl = kern != 0 ? blas32_lanes(a, kern) : 4, per = 64 / nl;
-        const float* qn = kern != 0 ? a.qn32 + (size_t)(p / a.R) * a.d_pad : nullptr;
-        for (int64_t r0 = b0 + (int64_t)w * per; kern != 0 && r0 < b1; r0 += (int64_t)(kFbT / 64) * per) {
-            const int64_t x = r0 + lane / nl;
-            const float v = a.rows32n ? blas32_dist_group<true>(a, p, qn, x, x < b1, kern, nl)
-                                       : blas32_dist_group<false>(a, p, qn, x, x < b1, kern, nl);
-            for (int j = 0; j < per; ++j) {
-                const float vj = __shfl(v, nl * j);
-                const int32_t rr = (int32_t)(r0 + j);
-                if (lane != 0 || r0 + j >= b1) continue;
-                const double xv = (double)vj;
-                if (!lt_dp(xv, rr, L[k - 1], G[k - 1])) continue;
-                int i = k - 1;
-                while (i > 0 && lt_dp(xv, rr, L[i - 1], G[i - 1])) {
-                    L[i] = L[i - 1];
-                    G[i] = G[i - 1];
-                    --i;
-                }
-                L[i] = xv;
-                G[i] = rr;
-            }
-        }
-        for (int64_t r0 = b0 + (int64_t)w * kB; kern == 0 && r0 < b1; r0 += (int64_t)(kFbT / 64) * kB) {
-            int32_t r[kB];
-#pragma unroll
-            for (int b = 0; b < kB; ++b) r[b] = r0 + b < b1 ? (int32_t)(r0 + b) : -1;
-            double dv[kB];
-            rows_dist64_x<TC, 3>(x_rows<TC, TQ>(a), (size_t)a.d_pad, r, a.d, nps, qh, zero_eps, dv);
-            if (lane == 0) {
-#pragma unroll
-                for (int b = 0; b < kB; ++b) {
-                    if (r[b] < 0) break;
-                    const double x = out_value<OUT64>(dv[b]);
-                    if (!lt_dp(x, r[b], L[k - 1], G[k - 1])) continue;
-                    int i = k - 1;
-                    while (i > 0 && lt_dp(x, r[b], L[i - 1], G[i - 1])) {
-                        L[i] = L[i - 1];
-                        G[i] = G[i - 1];
-                        --i;
-                    }
-                    L[i] = x;
-                    G[i] = r[b];
-                }
-            }
+    if (w == 0)
+        for (int f = blockIdx.x; f < nsl; f += gridDim.x) x_merge_slices<OUT64>(a, f);
+    for (int f = blockIdx.x; f < nf + (ns - nsl); f += gridDim.x) {
+        const bool whole = f < nf;
+        const int pp = whole ? -1 : a.sfailed[nsl + f - nf];
+        const int64_t p = whole ? a.failed[f] : a.pair_q[pp];
+        if (whole) {
+            const int c = a.classes[p];  // classes [nq][R]: pair p = q*R + r
+            const XBucketRows v{a.bucket_off[c], a.bucket_off[c + 1]};
+            x_rows_topk<TC, TQ, OUT64, kFbT / 64>(a, p, v, 0, v.b1 - v.b0, sd, sr);
+        } else {
+            const XSampleRows v = x_sample_rows(a, pp, p);
+            x_rows_topk<TC, TQ, OUT64, kFbT / 64>(a, p, v, 0, v.nv, sd, sr);
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            int head[kFbT / 64] = {};
-            const size_t o = (size_t)p * k;
-            for (int j = 0; j < k; ++j) {
-                int best = -1;
-                for (int v = 0; v < kFbT / 64; ++v) {
-                    if (head[v] >= k) continue;
-                    if (best < 0 || lt_dp(sd[v][head[v]], sr[v][head[v]], sd[best][head[best]],
-                                          sr[best][head[best]]))
-                        best = v;
-                }
-                const double x = sd[best][head[best]];
-                const int32_t rr = sr[best][head[best]];
-                ++head[best];
+        if (threadIdx.x == 0)
+            x_merge_waves<kFbT / 64>(k, sd, sr, [&](int j, double x, int32_t rr) {
                 const bool empty = rr == INT32_MAX;
-                x_store<OUT64>(a, o + j, empty ? __builtin_inf() : x, empty ? -1 : a.gpos[rr]);
-            }
-        }
+                x_store<OUT64>(a, (size_t)p * k + j, empty ? __builtin_inf() : x, empty ? -1 : a.gpos[rr]);
+            });
         __syncthreads();
     }
 }
@@ -1572,6 +1700,13 @@ int launch_x3(const XArgs& a, int64_t P, hipStream_t s) {
     const unsigned sg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P, 4 * num_cus_ref()));
     hipLaunchKernelGGL((x_select_kernel<TC, TQ, OUT64>), dim3(sg), dim3(kXT), lds, s, a);
     LMI_LAUNCH_CHECK("x_select_kernel");
+    if (a.n_sfailed) {
+        // (the sfailed pairs' slices: no work unless a pair's band reached its
+        // skipped sample's k-th)
+        const unsigned xg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P * kXSlices, 4 * num_cus_ref()));
+        hipLaunchKernelGGL((x_fallback_slice_kernel<TC, TQ, OUT64>), dim3(xg), dim3(kXSliceT), 0, s, a);
+        LMI_LAUNCH_CHECK("x_fallback_slice_kernel");
+    }
     const unsigned fg = (unsigned)std::max<int64_t>(1, std::min<int64_t>(P, num_cus_ref()));
     hipLaunchKernelGGL((x_fallback_kernel<TC, TQ, OUT64>), dim3(fg), dim3(kFbT), 0, s, a);
     LMI_LAUNCH_CHECK("x_fallback_kernel");
@@ -1599,7 +1734,8 @@ int launch_x_refine(const XArgs& a, int64_t P, hipStream_t s) {
                            a.C, const_cast<int32_t*>(a.grp));
         LMI_LAUNCH_CHECK("x_groups_kernel");
         LMI_CHECK_ARG(a.R <= LMI_MAX_R, "R=%d > %d", a.R, LMI_MAX_R);
-        hipLaunchKernelGGL(x_tail_kernel, dim3((unsigned)a.C), dim3(64), 0, s, a.pair_q, a.plan_counts, a.R, a.C,
+        hipLaunchKernelGGL(x_tail_kernel, dim3((unsigned)a.C), dim3(64), 0, s, a.pair_q, a.plan_counts,
+                           std::max(1, a.plan_cm), a.R, a.C,
                            a.grp, a.nrows_c, a.bucket_off, const_cast<uint8_t*>(a.tailq), const_cast<int64_t*>(a.goff));
         LMI_LAUNCH_CHECK("x_tail_kernel");
     }
@@ -1849,6 +1985,19 @@ extern "C" int lmi_refine_fallback_count(const void* workspace, const lmi_index_
     qmode &= ~LMI_Q_SEED_ROUND0;
     take_phases(qmode);
     const size_t at = idx->corpus32 ? x_nfailed_offset(idx, nq, R, k) : refine_ws(idx, nq, R, k, qmode).nfailed;
+    LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + at, 4,
+                               hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
+    LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));
+    return LMI_OK;
+}
+
+extern "C" int lmi_split_sample_fallback_count(const void* workspace, const lmi_index_desc* idx, int32_t nq,
+                                               int32_t R, int32_t k, int32_t* count_out, void* stream) {
+    using namespace lmi;
+    LMI_CHECK_ARG(workspace && idx && count_out, "null pointer");
+    LMI_CHECK_ARG(idx->corpus32 != nullptr, "not a split-mode index (corpus32)");
+    LMI_CHECK_ARG(nq >= 0 && R >= 1 && k >= 1 && k <= LMI_MAX_K, "bad nq/R/k");
+    const size_t at = x_nfailed_offset(idx, nq, R, k) + 8 * sizeof(int32_t);
     LMI_HIP_TRY(hipMemcpyAsync(count_out, (const unsigned char*)workspace + at, 4,
                                hipMemcpyDeviceToHost, reinterpret_cast<hipStream_t>(stream)));
     LMI_HIP_TRY(hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream)));

@@ -906,17 +906,33 @@ __global__ __launch_bounds__(64) void kth_bound_kernel(
 }
 
 // the collect scan's per-grouped-pair bound (thr_g: the distance ordinal in
-// the high word) and candidate count
+// the high word) and candidate count; a pair whose bucket has skipped rows in
+// front of it (WideScan::app_d) starts with the skipped rows' own list
 __global__ __launch_bounds__(256) void set_bound_kernel(const int32_t* __restrict__ pair_q, int32_t P,
                                                         const uint32_t* __restrict__ bound_ord,
                                                         unsigned long long* __restrict__ thr_g,
-                                                        uint32_t* __restrict__ ccount) {
+                                                        uint32_t* __restrict__ ccount,
+                                                        const int32_t* __restrict__ pair_bucket,
+                                                        const int64_t* __restrict__ bucket_off,
+                                                        const float* __restrict__ app_d,
+                                                        const int32_t* __restrict__ app_row, int32_t app_k,
+                                                        uint64_t* __restrict__ cand, int32_t cap) {
     const int pp = blockIdx.x * 256 + threadIdx.x;
     if (pp >= P) return;
     const int p = pair_q[pp];
     const uint32_t b = (p < 0 || p >= P) ? 0u : bound_ord[p];
     thr_g[pp] = ((unsigned long long)b << 32) | 0xffffffffull;
-    ccount[pp] = 0u;
+    uint32_t n = 0u;
+    const int c = pair_bucket[pp];
+    if (app_d && b != 0u && c > 0 && (c & 1) && bucket_off[c - 1] < bucket_off[c]) {
+        for (int i = 0; i < app_k && (int)n < cap; ++i) {
+            const float dv = app_d[(size_t)p * app_k + i];
+            const int32_t r = app_row[(size_t)p * app_k + i];
+            if (r < 0 || !(dv < __builtin_inff())) continue;
+            cand[(size_t)pp * cap + n++] = ((uint64_t)f2ord(dv) << 32) | (uint32_t)r;
+        }
+    }
+    ccount[pp] = n;
 }
 
 // Per grouped pair of the collect scan (one 256-lane workgroup): its
@@ -1093,13 +1109,25 @@ __global__ __launch_bounds__(256) void x_margin_kernel(int64_t P, double two_eps
 // the k-th of its bucket's sample, an upper bound of its own (and the collect
 // then finds about k n_c / s_c <= k kXSampleDiv rows under it, far inside
 // its buffer at any bucket size).
+//
+// The collect scan's descriptor (x_collect_desc) skips the sample where it is
+// at most a quarter of the bucket (LMI_X_SKIP_SHARE): bucket 2c = the sample (no chunks, never
+// probed), 2c + 1 = the rest; a bucket with a larger sample is collected whole
+// (2c empty, 2c + 1 = the bucket).  The skipped rows' candidates are the
+// sample scan's own list (set_bound_kernel appends it): every skipped row the
+// select needs is in it unless the pair's band reaches the sample's k-th
+// (x_select_wave_kernel checks; 0.03% of the pairs on the 10M mixture,
+// tools/x_sample_cover.py), and those pairs are scored exactly over their
+// sample rows and candidates (x_fallback_kernel).
 constexpr int kXSampleDiv = 16;
 __global__ __launch_bounds__(64) void x_sample_desc_kernel(const int64_t* __restrict__ bucket_off, int32_t C,
                                                            int64_t chunk_rows, const int32_t* __restrict__ classes,
                                                            int32_t P, int64_t* __restrict__ off2,
-                                                           int32_t* __restrict__ cf2, int32_t* __restrict__ classes2) {
+                                                           int32_t* __restrict__ cf2, int32_t* __restrict__ classes2,
+                                                           int64_t* __restrict__ off2b, int32_t* __restrict__ cf2b,
+                                                           int32_t* __restrict__ classes2b, int32_t skip_share) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        int32_t nch = 0;
+        int32_t nch = 0, nchb = 0;
         for (int c = 0; c < C; ++c) {
             const int64_t a = bucket_off[c], n = bucket_off[c + 1] - a;
             const int64_t want = std::max(chunk_rows, (n / kXSampleDiv + 31) / 32 * 32);
@@ -1109,13 +1137,23 @@ __global__ __launch_bounds__(64) void x_sample_desc_kernel(const int64_t* __rest
             cf2[2 * c] = nch;
             nch += (int32_t)((sc + chunk_rows - 1) / chunk_rows);
             cf2[2 * c + 1] = nch;
+            // (a sample of at most 1 / skip_share of the bucket, LMI_X_SKIP_SHARE)
+            const int64_t skip = (skip_share > 0 && sc < n && sc * skip_share <= n) ? sc : 0;
+            off2b[2 * c] = a;
+            off2b[2 * c + 1] = a + skip;
+            cf2b[2 * c] = nchb;
+            cf2b[2 * c + 1] = nchb;
+            nchb += (int32_t)((n - skip + chunk_rows - 1) / chunk_rows);
         }
         off2[2 * C] = bucket_off[C];
         cf2[2 * C] = nch;
+        off2b[2 * C] = bucket_off[C];
+        cf2b[2 * C] = nchb;
     }
     for (int i = blockIdx.x * 64 + threadIdx.x; i < P; i += gridDim.x * 64) {
         const int32_t c = classes[i];
         classes2[i] = c < 0 ? c : (c < C ? 2 * c : 2 * C);
+        classes2b[i] = c < 0 ? c : (c < C ? 2 * c + 1 : 2 * C);
     }
 }
 
@@ -1535,7 +1573,8 @@ int lmi::bucket_topk_impl(const lmi_index_desc* idx, const float* q, int32_t nq,
     // and its candidate count
     if (wide && wide->mode == 2 && do_scan) {
         hipLaunchKernelGGL(set_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, pair_q, P,
-                           wide->bound_ord, (unsigned long long*)(ws + w.thr_g), wide->ccount);
+                           wide->bound_ord, (unsigned long long*)(ws + w.thr_g), wide->ccount, pair_bucket,
+                           idx->bucket_off, wide->app_d, wide->app_row, wide->app_k, wide->cand, wide->cap);
         LMI_LAUNCH_CHECK("set_bound_kernel");
     }
 
@@ -1687,8 +1726,9 @@ double split_eps(int d_pad) {
 
 namespace {
 struct XWs {
-    size_t qr, ld, lpos, bound, ccount, cand, failed, nfailed, wgl, fix, bins, sub_first, sub_rows, sub_take, off2, cf2,
-        classes2, qn32, grp, tailq, goff, region, region_bytes, region_s, region_s_bytes, total;
+    size_t qr, ld, lpos, srow, bound, ccount, cand, failed, nfailed, wgl, sfl, spd, spg, fix, bins, sub_first, sub_rows, sub_take,
+        off2, cf2, classes2, off2b, cf2b, classes2b, qn32, grp, tailq, goff, region, region_bytes, region_s,
+        region_s_bytes, total;
     int32_t cap;
 };
 // k <= 10: the k-th of a per-bucket sample (the product scan over
@@ -1703,6 +1743,16 @@ lmi_index_desc x_sample_desc(const lmi_index_desc* idx, const int64_t* off2, con
     // rows beyond one chunk)
     d.max_chunks = 2 + std::max(idx->max_chunks, 1) / kXSampleDiv;
     d.n_chunks = idx->n_buckets * d.max_chunks;
+    d.chunk_centroid = nullptr;
+    return d;
+}
+// the collect scan's: the rest of every bucket whose sample is skipped, the
+// others whole (x_sample_desc_kernel)
+lmi_index_desc x_collect_desc(const lmi_index_desc* idx, const int64_t* off2b, const int32_t* cf2b) {
+    lmi_index_desc d = *idx;
+    d.n_buckets = 2 * idx->n_buckets;
+    d.bucket_off = off2b;
+    d.chunk_first = cf2b;
     d.chunk_centroid = nullptr;
     return d;
 }
@@ -1730,6 +1780,7 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.qr = take((size_t)nq * idx->d_pad * 4);
     w.ld = take(P * std::max(k, 15) * 4);
     w.lpos = take(P * std::max(k, 15) * 4);
+    w.srow = take(P * std::max(k, 15) * 4);
     w.fix = take(P * 4);
     w.bins = take(P * 4);
     w.sub_first = take(((size_t)idx->n_buckets + 1) * 4);
@@ -1738,6 +1789,9 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.off2 = take(((size_t)2 * idx->n_buckets + 1) * 8);
     w.cf2 = take(((size_t)2 * idx->n_buckets + 1) * 4);
     w.classes2 = take(P * 4);
+    w.off2b = take(((size_t)2 * idx->n_buckets + 1) * 8);
+    w.cf2b = take(((size_t)2 * idx->n_buckets + 1) * 4);
+    w.classes2b = take(P * 4);
     w.qn32 = take((size_t)nq * idx->d_pad * 4);
     w.grp = take((size_t)R * idx->n_buckets * 4);
     w.tailq = take(P);
@@ -1746,12 +1800,18 @@ XWs x_ws(const lmi_index_desc* idx, int nq, int R, int k) {
     w.ccount = take(P * 4);
     w.cand = take(P * (size_t)cap * 8);
     w.failed = take(P * 4);
-    w.nfailed = take(256);  // (word 0: the failed pairs; word 16: the wgl pairs)
+    w.nfailed = take(256);  // (word 0: the failed pairs; word 8: the sfl pairs; word 16: the wgl pairs)
     w.wgl = take(P * 4);
+    w.sfl = take(P * 4);
+    // (the sliced sample fallback's lists)
+    w.spd = take((size_t)kXSlicedPairs * kXSlices * k * 8);
+    w.spg = take((size_t)kXSlicedPairs * kXSlices * k * 4);
     const lmi_index_desc bd = bound_desc(idx, kXLists, nullptr);
     const lmi_index_desc sd = x_sample_desc(idx, nullptr, nullptr);
+    const lmi_index_desc cd = x_collect_desc(idx, nullptr, nullptr);
     w.region_bytes = std::max({ws_layout(idx, nq, R, k, LMI_Q_F16).total, ws_layout(idx, nq, R, 10, LMI_Q_F16).total,
-                               ws_layout(&bd, nq, R, 15, LMI_Q_F16).total, ws_layout(&sd, nq, R, k, LMI_Q_F16).total});
+                               ws_layout(&bd, nq, R, 15, LMI_Q_F16).total, ws_layout(&sd, nq, R, k, LMI_Q_F16).total,
+                               ws_layout(&cd, nq, R, 10, LMI_Q_F16).total});
     w.region = take(w.region_bytes);
     // k <= 10: the sample scan's own region (ABI 11), so the plans of both
     // scans are laid down in one PLAN phase and the batch stream can run the
@@ -1805,7 +1865,10 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     const bool sampled = x_sampled(k);
     int32_t* fix = (int32_t*)(ws + w.fix);
     int rc;
-    const WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
+    WideScan m2{2, bound, cand, ccount, w.cap, nullptr, 0, nullptr, nullptr};
+    int32_t* srow = (int32_t*)(ws + w.srow);
+    auto* off2b = (int64_t*)(ws + w.off2b);
+    const lmi_index_desc cd = x_collect_desc(idx, off2b, (int32_t*)(ws + w.cf2b));
     if (x_sample(k)) {
         // (PLAN: the rounded queries and both scans' plans; SCAN: the sample
         // scan and its merge, the bound, the collect scan; MERGE: step 3)
@@ -1814,6 +1877,12 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
         auto* classes2 = (int32_t*)(ws + w.classes2);
         const lmi_index_desc sd = x_sample_desc(idx, off2, cf2);
         unsigned char* region_s = ws + w.region_s;
+        auto* classes2b = (int32_t*)(ws + w.classes2b);
+        // (the collect skips the samples it can: their candidates are the
+        // sample scan's lists, appended by set_bound_kernel)
+        m2.app_d = ld;
+        m2.app_row = srow;
+        m2.app_k = k;
         if (phases & kPhasePlan) {
             hipLaunchKernelGGL(x_round_queries_kernel, dim3((nq + kThreads / 64 - 1) / (kThreads / 64)),
                                dim3(kThreads), 0, s, q, ldq, q64, ldq64, nq, idx->d, idx->d_pad, qr);
@@ -1821,12 +1890,13 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
             LMI_TRY(fill_u32(ws + w.nfailed, 0u, 32, s));
             hipLaunchKernelGGL(x_sample_desc_kernel, dim3((unsigned)std::min(1024, (P + 63) / 64)), dim3(64), 0, s,
                                idx->bucket_off, idx->n_buckets, (int64_t)idx->chunk_rows, classes, P, off2, cf2,
-                               classes2);
+                               classes2, off2b, (int32_t*)(ws + w.cf2b), classes2b,
+                               std::max(0, env_config().x_skip));
             LMI_LAUNCH_CHECK("x_sample_desc_kernel");
-            rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
+            rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, srow, status,
                                   region_s, w.region_s_bytes, s, nullptr, 0, true, false, 0.0f, kPhasePlan);
             if (rc != LMI_OK) return rc;
-            rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status,
+            rc = bucket_topk_impl(&cd, qr, nq, idx->d_pad, classes2b, R, 10, LMI_Q_F16, ld, lpos, nullptr, status,
                                   region, w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhasePlan, &m2);
             if (rc != LMI_OK) return rc;
         }
@@ -1834,15 +1904,16 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
             // 1. the k-th of every pair's bucket sample (its first chunk_rows
             //    rows): the product scan over the 2C-bucket sample descriptor,
             //    then that k-th + 2 eps as the collect bound
-            rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, nullptr, status,
+            rc = bucket_topk_impl(&sd, qr, nq, idx->d_pad, classes2, R, k, LMI_Q_F16, ld, lpos, srow, status,
                                   region_s, w.region_s_bytes, s, nullptr, 0, true, false, 0.0f,
                                   kPhaseScan | kPhaseMerge);
             if (rc != LMI_OK) return rc;
             hipLaunchKernelGGL(x_bound_kernel, dim3((P + 255) / 256), dim3(256), 0, s, (int64_t)P, k, ld, two_eps,
                                bound);
             LMI_LAUNCH_CHECK("x_bound_kernel");
-            // 2. every row under the bound (the collect scan, as the wide path's)
-            rc = bucket_topk_impl(idx, qr, nq, idx->d_pad, classes, R, 10, LMI_Q_F16, ld, lpos, nullptr, status,
+            // 2. every row under the bound (the collect scan, as the wide path's,
+            //    over the rest of the buckets whose sample it skips)
+            rc = bucket_topk_impl(&cd, qr, nq, idx->d_pad, classes2b, R, 10, LMI_Q_F16, ld, lpos, nullptr, status,
                                   region, w.region_bytes, s, nullptr, 0, false, false, 0.0f, kPhaseScan, &m2);
             if (rc != LMI_OK) return rc;
         }
@@ -1896,7 +1967,7 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     if (rc != LMI_OK) return rc;
     }
     // 3. the candidates' exact distances, sorted; overflowed pairs whole
-    const WsLayout l = ws_layout(idx, nq, R, 10, LMI_Q_F16);
+    const WsLayout l = ws_layout(x_sample(k) ? &cd : idx, nq, R, 10, LMI_Q_F16);
     XArgs a{};
     a.rows32 = idx->corpus32;
     a.rows32n = idx->corpus32n;
@@ -1941,6 +2012,15 @@ int bucket_topk_x(const lmi_index_desc* idx, const float* q, int32_t nq, int32_t
     a.tailq = (const uint8_t*)(ws + w.tailq);
     a.goff = (const int64_t*)(ws + w.goff);
     a.plan_counts = (const int32_t*)(region + l.counts);
+    a.plan_cm = x_sample(k) ? 2 : 1;
+    if (x_sample(k)) {
+        a.soff = off2b;
+        a.skth = ld;
+        a.sfailed = (int32_t*)(ws + w.sfl);
+        a.n_sfailed = (int32_t*)(ws + w.nfailed) + 8;
+        a.spd = (double*)(ws + w.spd);
+        a.spg = (int32_t*)(ws + w.spg);
+    }
     // (pairs whose class is out of range keep the prefill of step 1's prep:
     // the outputs are prefilled here, by pair id, in step 3's own buffers)
     hipLaunchKernelGGL(x_prefill_kernel, dim3((unsigned)(((int64_t)P * k + 255) / 256)), dim3(256), 0, s,

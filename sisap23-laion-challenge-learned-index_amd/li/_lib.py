@@ -63,6 +63,7 @@ EXPORTS = (
     "lmi_f64_global_band",
     "lmi_bucket_topk_f64g",
     "lmi_refine_fallback_count",
+    "lmi_split_sample_fallback_count",
     "lmi_split_eps",
     "lmi_split_normalize",
     "lmi_replay_device_phase",
@@ -108,7 +109,7 @@ class MlpDesc(C.Structure):
     ]
 
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 
 class IndexDesc(C.Structure):
@@ -160,6 +161,7 @@ _SIGNATURES = {
                                           _P, _I64, _I32, _P, _P, _P, _P, _P, C.c_size_t, _P]),
     "lmi_refine_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _I32, _P,
                                             _P]),
+    "lmi_split_sample_fallback_count": (C.c_int, [_P, C.POINTER(IndexDesc), _I32, _I32, _I32, _P, _P]),
     "lmi_merge_topk_f64": (C.c_int, [_P, _P, _I32, _I64, _I32, _P, _P, _P]),
     "lmi_packed_rank_words": (C.c_int64, [_I64, _I32, _I32]),
     "lmi_merge_topk_packed": (C.c_int, [_P, _I32, _I64, _I64, _I32, _I32, _P, _P, _P, _P]),

@@ -673,6 +673,23 @@ def bucket_topk_f64(index: DeviceIndex, q: torch.Tensor, classes: torch.Tensor, 
     return out_d, out_pos, status, int(n.value)
 
 
+def split_sample_fallback_count(index: DeviceIndex, nq: int, R: int, k: int, ws=None,
+                                f64: bool = False, stream=None) -> int:
+    """The split mode (k <= 10, ABI 13): how many pairs of the last call on
+    this workspace (`ws`, else the index's own: bucket_topk's, or
+    bucket_topk_f64's with f64=True) had a band reaching their skipped
+    sample's k-th and were scored over the sample rows and candidates
+    (lmi_split_sample_fallback_count)."""
+    lib = _lib.load()
+    if ws is None:
+        ws = index._ws.get("f64" if f64 else "buf")
+    n = C.c_int32(0)
+    s = stream if stream is not None else _lib.stream_handle(index.device)
+    check("lmi_split_sample_fallback_count", lib.lmi_split_sample_fallback_count(
+        ptr(ws), C.byref(index.desc_for(k)), nq, R, k, C.byref(n), s))
+    return int(n.value)
+
+
 def global_band(index: DeviceIndex, nq: int, R: int, k: int, qmode: int) -> bool:
     """True when the float64 search of a striped index can decide its band
     over every rank's lists (lmi_f64_global_band: the band lists, k <= 10 on

@@ -14,7 +14,8 @@ import torch
 import lmi_oracle as O
 import workloads
 from li import _lib
-from li.index import DeviceIndex, DeviceRouter, Searcher, bucket_topk, bucket_topk_f64
+from li.index import (DeviceIndex, DeviceRouter, Searcher, bucket_topk, bucket_topk_f64,
+                      split_sample_fallback_count)
 from test_oracle_golden_r5 import BASES, CASES, G5, SINGLES, check, inputs_r5
 
 pytestmark = pytest.mark.gpu
@@ -82,6 +83,51 @@ def test_split_multi_chunk_sample(dist):
         tol = dict(atol=1e-12, tie=1e-12)
     assert int(st.item()) == 0
     assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), **tol) == 0
+
+
+@pytest.mark.parametrize("in_sample,n_near", [(16, 24), (8, 24), (16, 300)])
+def test_split_skipped_sample_rows(in_sample, n_near):
+    """Buckets of thousands of rows at 128-row chunks: the collect scan skips
+    each bucket's sample (n_c / 16 rows, under a quarter of it) and takes the
+    sample scan's own list for it.  16 near-copies of one vector at the front of a
+    bucket (all in its sample) and queries next to them: the pairs' band
+    reaches the sample's 10th, so they are scored over their sample rows and
+    candidates (the count says they were; 300 such pairs: past the 256 sliced
+    ones, a workgroup each); 8 in the sample and 8 at the
+    bucket's end: the list covers the sample.  Both arithmetics equal the oracle's lists."""
+    w, x, q = _x("router", 643, n=9000, nq=max(96, n_near + 20), C=2)
+    C = w["C"]
+    rng = np.random.default_rng(7)
+    b = 0
+    rows = np.nonzero(w["labels"] == b)[0]
+    assert rows.size >= 4 * 128
+    # (the sample: the bucket's first max(128, n_c / 16 rounded up to 32) rows)
+    near = np.concatenate([rows[:in_sample], rows[rows.size - (16 - in_sample):]])
+    x = x.copy()
+    # (a direction of its own, far from every clustered row: past the near
+    # copies, a bucket's next rows lie well outside any band)
+    v = rng.standard_normal(x.shape[1]) * (np.linalg.norm(x[near[0]]) / np.sqrt(x.shape[1]))
+    x[near] = (v * (1 + 1e-3 * rng.standard_normal((near.size, x.shape[1])))).astype(np.float32)
+    q = q.copy()
+    q[:n_near] = (v * (1 + 1e-3 * rng.standard_normal((n_near, x.shape[1])))).astype(np.float32)
+    ix = DeviceIndex(x, w["labels"], C, chunk_rows=128, device="cuda")
+    classes = np.tile(np.array([[b, 1 - b]], np.int64), (q.shape[0], 1))
+    cls = T(classes.astype(np.int32))
+    nq, R = q.shape[0], 2
+    d, p, st = bucket_topk(ix, T(q), cls, 10)
+    assert int(st.item()) == 0
+    ns = split_sample_fallback_count(ix, nq, R, 10)
+    assert (ns >= n_near) if in_sample == 16 else (ns < n_near)
+    ref_d, ref_p = O.bucket_lists(w["labels"], x, q, classes, R, 10, C)
+    assert O.compare_lists(ref_d, ref_p, d.cpu().numpy(), p.cpu().numpy(), atol=1e-5, tie=1e-6) == 0
+    q64 = q.astype(np.float64)
+    d64, p64, st64, nfb = bucket_topk_f64(ix, T(q64), cls, 10, fallback_count=True)
+    assert int(st64.item()) == 0 and nfb == 0
+    ns64 = split_sample_fallback_count(ix, nq, R, 10, f64=True)
+    assert (ns64 >= n_near) if in_sample == 16 else (ns64 < n_near)
+    ref_d64, ref_p64 = O.bucket_lists(w["labels"], x, q64, classes, R, 10, C)
+    assert O.compare_lists(ref_d64, ref_p64, d64.cpu().numpy(), p64.cpu().numpy(), atol=1e-12,
+                           tie=1e-12) == 0
 
 
 def test_split_overflow_takes_the_whole_shard():

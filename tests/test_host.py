@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
     assert declared == set(_lib.EXPORTS)
     for name in declared:
         assert getattr(lib, name) is not None
-    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 12
+    assert lib.lmi_abi_version() == _lib.ABI_VERSION == 13
 
 
 def test_invalid_arguments_fail_loudly_without_a_device():
