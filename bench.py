@@ -139,12 +139,16 @@ def algorithmic_bytes(index, classes, nq):
     rows = int(sum(loc[c + 1] - loc[c] for c in probed))
     if index.storage == "f32x":
         # the split mode's two scans (lmi_scan.hip bucket_topk_x): the sample
-        # scan over each probed bucket's first max(chunk_rows, n_c / 16) rows,
-        # then the collect scan over all its rows, both streaming the fp16
-        # rounding
+        # scan over each probed bucket's first s_c = max(chunk_rows, n_c / 16)
+        # rows, then the collect scan over the rest -- or over the whole bucket
+        # where the sample is more than a quarter of it (x_sample_desc_kernel,
+        # LMI_X_SKIP_SHARE), those sample rows read twice -- both streaming
+        # the fp16 rounding
         n_c = np.array([loc[c + 1] - loc[c] for c in probed], dtype=np.int64)
-        want = np.maximum(index.chunk_rows, (n_c // 16 + 31) // 32 * 32)
-        rows += int(np.minimum(n_c, want).sum())
+        s_c = np.minimum(n_c, np.maximum(index.chunk_rows, (n_c // 16 + 31) // 32 * 32))
+        share = int(os.environ.get("LMI_X_SKIP_SHARE", "4"))
+        skipped = (share > 0) & (s_c < n_c) & (s_c * max(share, 1) <= n_c)
+        rows += int(s_c[~skipped].sum())
     s = 4 if index.storage == "f32" else 2   # (f32x: its scans stream the fp16 rounding)
     byts = rows * (index.d_pad * s + 4) + nq * index.d_pad * s * (2 if index.storage == "f32x" else 1)
     sizes = np.diff(loc)
@@ -335,8 +339,14 @@ def pmc_traffic(kernel_ms, split=False):
     MI355X_MICROARCH.md HBM section) + WRITE_SIZE, in bytes; None when no
     summary is committed."""
     import glob
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))
-                   if ("split_pmc" in os.path.basename(f)) == split)
+    import re
+
+    def session(f):
+        # (rNN then the session letters a .. z, aa, ab, ...: the latest last)
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2), f) if m else (0, 0, "", f)
+    files = sorted((f for f in glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))
+                    if ("split_pmc" in os.path.basename(f)) == split), key=session)
     if not files:
         return None, None
     d = json.load(open(files[-1]))
