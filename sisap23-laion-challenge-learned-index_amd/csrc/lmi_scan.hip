@@ -578,48 +578,89 @@ __device__ inline int chunk_slot(int j, int nch_c, uint32_t sm, int S, int X) {
 // (distance, global position) in M; rows inside a chunk ascend in global
 // position, so mapping keeps each list ordered and the merge is by the
 // reference's (distance, g.index) order)
+//
+// The merges are bitonic over kMergeN = 16 register slots: two ascending
+// lists A, B -> A[i] = min(A[i], B[15 - i]) is bitonic and holds the union's
+// 16 smallest; four half-cleaner stages sort it.  48 compare-exchanges a merge
+// where inserting a list entry by entry cost up to 16 shifting inserts of 16
+// (the band lists' merge, 16 slots, took 2.4x the plain 10-slot merge's time
+// at W = 8: ~126 against 53 us after the scan, profiles/r06aj_w8_*_trace.txt).
+constexpr int kMergeN = 16;
+__device__ inline void bitonic_top(uint64_t (&A)[kMergeN], int32_t (&AW)[kMergeN], const uint64_t (&B)[kMergeN],
+                                   const int32_t (&BW)[kMergeN]) {
+#pragma unroll
+    for (int i = 0; i < kMergeN; ++i) {
+        const bool t = B[kMergeN - 1 - i] < A[i];
+        A[i] = t ? B[kMergeN - 1 - i] : A[i];
+        AW[i] = t ? BW[kMergeN - 1 - i] : AW[i];
+    }
+#pragma unroll
+    for (int d = kMergeN / 2; d > 0; d >>= 1) {
+#pragma unroll
+        for (int i = 0; i < kMergeN; ++i) {
+            if ((i & d) == 0) {
+                const uint64_t x = A[i], y = A[i + d];
+                const int32_t xw = AW[i], yw = AW[i + d];
+                const bool sw = y < x;
+                A[i] = sw ? y : x;
+                A[i + d] = sw ? x : y;
+                AW[i] = sw ? yw : xw;
+                AW[i + d] = sw ? xw : yw;
+            }
+        }
+    }
+}
+
+// one ascending list K of NE (distance, local row) entries into M (its first
+// KL exact): entries past M's KL-th distance are dropped before the gather
 template <int KL, int NE>
-__device__ inline void merge_chunk_list(const uint64_t (&K)[NE], uint64_t (&M)[KL], int32_t (&W)[KL],
+__device__ inline void merge_chunk_list(const uint64_t (&K)[NE], uint64_t (&M)[kMergeN], int32_t (&W)[kMergeN],
                                         const int32_t* __restrict__ gpos, int64_t n_rows,
                                         int32_t* __restrict__ status) {
+    static_assert(NE <= kMergeN && KL <= kMergeN, "merge slots");
+    const uint32_t thr = (uint32_t)(M[KL - 1] >> 32);
+    uint64_t B[kMergeN];
+    int32_t BW[kMergeN];
+#pragma unroll
+    for (int i = 0; i < kMergeN; ++i) {
+        B[i] = kEmptyKey;
+        BW[i] = -1;
+    }
     int32_t g[NE];
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
         const uint32_t lp = (uint32_t)K[i];
-        // (pre-filter on the distance part: past this lane's KL-th, an entry
-        // is past the union's too)
-        const bool live = K[i] != kEmptyKey && (K[i] >> 32) <= (M[KL - 1] >> 32);
+        const bool live = K[i] != kEmptyKey && (uint32_t)(K[i] >> 32) <= thr;
         const bool ok = lp < (uint32_t)n_rows;
         if (live && !ok) atomicOr(status, LMI_STATUS_INTERNAL);  // never for a sound scan
         g[i] = (live && ok) ? gpos[lp] : -1;
     }
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
-        if (g[i] < 0) continue;
-        const uint64_t key = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
-        if (key < M[KL - 1]) list_insert_pair<KL>(M, W, key, (int32_t)(uint32_t)K[i]);
+        if (g[i] >= 0) {
+            B[i] = (K[i] & 0xffffffff00000000ull) | (uint32_t)g[i];
+            BW[i] = (int32_t)(uint32_t)K[i];
+        }
     }
+    bitonic_top(M, W, B, BW);
 }
 
 // The lanes of a pair merge their lists (xor butterfly inside the pair's
 // kMergeLanes-lane group): after the rounds every lane holds the union's
-// KL smallest keys
-template <int KL>
-__device__ inline void merge_lanes(uint64_t (&M)[KL], int32_t (&W)[KL]) {
+// kMergeN smallest keys
+__device__ inline void merge_lanes(uint64_t (&M)[kMergeN], int32_t (&W)[kMergeN]) {
 #pragma unroll
     for (int off = 1; off < kMergeLanes; off <<= 1) {
-        uint64_t o[KL];
-        int32_t ow[KL];
+        uint64_t o[kMergeN];
+        int32_t ow[kMergeN];
 #pragma unroll
-        for (int i = 0; i < KL; ++i) {
+        for (int i = 0; i < kMergeN; ++i) {
             const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)M[i], off);
             const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(M[i] >> 32), off);
             o[i] = ((uint64_t)hi << 32) | lo;
             ow[i] = __shfl_xor(W[i], off);
         }
-#pragma unroll
-        for (int i = 0; i < KL; ++i)
-            if (o[i] < M[KL - 1]) list_insert_pair<KL>(M, W, o[i], ow[i]);
+        bitonic_top(M, W, o, ow);
     }
 }
 
@@ -633,9 +674,13 @@ __device__ inline void merge_pair(const uint64_t* __restrict__ partial, int32_t 
                                   uint32_t* ub) {
     const int nch = nch_c + (S - 1) * __popc(sm);
     const int X = max_chunks / S;
-    list_clear<KL>(M);
+    uint64_t MM[kMergeN];
+    int32_t WW[kMergeN];
 #pragma unroll
-    for (int i = 0; i < KL; ++i) W[i] = -1;
+    for (int i = 0; i < kMergeN; ++i) {
+        MM[i] = kEmptyKey;
+        WW[i] = -1;
+    }
     uint64_t Kn[NE];
     uint32_t ubn = 0xffffffffu;
     auto load = [&](int j) {
@@ -651,9 +696,14 @@ __device__ inline void merge_pair(const uint64_t* __restrict__ partial, int32_t 
         for (int i = 0; i < NE; ++i) K[i] = Kn[i];
         if constexpr (BAND) *ub = std::min(*ub, ubn);
         if (j + kMergeLanes < nch) load(j + kMergeLanes);
-        merge_chunk_list<KL, NE>(K, M, W, gpos, n_rows, status);
+        merge_chunk_list<KL, NE>(K, MM, WW, gpos, n_rows, status);
     }
-    merge_lanes<KL>(M, W);
+    merge_lanes(MM, WW);
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+        M[i] = MM[i];
+        W[i] = WW[i];
+    }
 }
 
 template <int KL, bool ROWS>
